@@ -1,0 +1,149 @@
+/* mjx355 — MI355X-native batched MuJoCo step: the C ABI of the drop-in boundary.
+ *
+ * This header is the seam that replaces the reference's physics boundary
+ * `mjlab.sim.Simulation` (src/mjlab/sim/sim.py:100-286) and the MuJoCo-Warp calls
+ * behind it:
+ *
+ *   mjx_model_create   <- mujoco_warp.put_model(mj_model)            sim/sim.py:139
+ *   mjx_sim_create     <- mujoco_warp.put_data(..., nworld, nconmax,  sim/sim.py:143-149
+ *                         njmax) + create_graph()                     sim/sim.py:164-191
+ *   mjx_step           <- mujoco_warp.step / wp.capture_launch        sim/sim.py:267-273
+ *   mjx_forward        <- mujoco_warp.forward                         sim/sim.py:260-265
+ *   mjx_reset          <- mujoco_warp.reset_data(reset=mask)          sim/sim.py:275-286
+ *   mjx_field          <- WarpBridge.__getattr__ -> wp.to_torch       sim/sim_data.py:177-240
+ *                         (here: a DLPack DLManagedTensor aliasing device memory)
+ *   mjx_expand_field   <- expand_model_fields / repeat_array_kernel   sim/sim.py:226-240,
+ *                                                                     sim/randomization.py:9-54
+ *
+ * Conventions: plain C, no exceptions cross the ABI, every call returns an int status
+ * (0 = ok) and `mjx_last_error()` gives the message of the last failure on this thread.
+ * All device work is enqueued on the HIP stream passed in (`void*` = hipStream_t, NULL =
+ * legacy default stream); nothing in step/forward/reset synchronises the host.
+ */
+#ifndef MJX355_H_
+#define MJX355_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MJX_ABI_VERSION 1
+
+/* geom types (MuJoCo mjtGeom numbering) */
+enum { MJX_GEOM_PLANE = 0, MJX_GEOM_HFIELD = 1, MJX_GEOM_SPHERE = 2, MJX_GEOM_CAPSULE = 3,
+       MJX_GEOM_ELLIPSOID = 4, MJX_GEOM_CYLINDER = 5, MJX_GEOM_BOX = 6, MJX_GEOM_MESH = 7 };
+/* joint types (mjtJoint) */
+enum { MJX_JNT_FREE = 0, MJX_JNT_BALL = 1, MJX_JNT_SLIDE = 2, MJX_JNT_HINGE = 3 };
+/* sensor types (subset of mjtSensor used by mjlab tasks) */
+enum { MJX_SENS_GYRO = 0, MJX_SENS_VELOCIMETER = 1, MJX_SENS_ACCELEROMETER = 2,
+       MJX_SENS_SUBTREEANGMOM = 3, MJX_SENS_CONTACT = 4, MJX_SENS_FRAMEPOS = 5,
+       MJX_SENS_FRAMEQUAT = 6, MJX_SENS_JOINTPOS = 7, MJX_SENS_JOINTVEL = 8 };
+/* object types for sensors */
+enum { MJX_OBJ_NONE = 0, MJX_OBJ_BODY = 1, MJX_OBJ_XBODY = 2, MJX_OBJ_JOINT = 3,
+       MJX_OBJ_GEOM = 5, MJX_OBJ_SITE = 6 };
+/* contact sensor reduce modes (sensor/contact_sensor.py:39-44) */
+enum { MJX_REDUCE_NONE = 0, MJX_REDUCE_MINDIST = 1, MJX_REDUCE_MAXFORCE = 2,
+       MJX_REDUCE_NETFORCE = 3 };
+enum { MJX_INT_EULER = 0, MJX_INT_IMPLICITFAST = 1 };
+#define MJX_MASK_WORDS 4 /* contact-sensor geom masks: 128 geoms */
+
+/* Host-side compiled model (fp64 / int32).  Field names follow mjModel.  Array
+ * widths per element are in the trailing comment.  Filled by the Python scene
+ * compiler (mjlab-1_amd/mjlab_amd/compiler/model.py); consumed by mjx_model_create
+ * (uploaded to HBM as fp32) and by the CPU oracle (oracle/oracle.c, fp64). */
+typedef struct mjxModelDesc_ {
+  int abi_version;
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
+  int nhfield, nhfielddata, nlevel;
+  int iterations, ls_iterations, integrator, cone;
+  double timestep, tolerance, ls_tolerance, impratio, meaninertia;
+  double gravity[3];
+  /* bodies */
+  const int32_t *body_parentid, *body_rootid, *body_weldid, *body_jntnum, *body_jntadr,
+      *body_dofnum, *body_dofadr, *body_level, *body_childadr /* nbody+1 */,
+      *body_child /* >=1 */, *body_mocapid;
+  const double *body_pos /*3*/, *body_quat /*4*/, *body_ipos /*3*/, *body_iquat /*4*/,
+      *body_mass, *body_inertia /*3*/, *body_subtreemass, *body_invweight0 /*2*/;
+  const int32_t *level_start /* nlevel+1 */, *level_body /* nbody */;
+  /* joints */
+  const int32_t *jnt_type, *jnt_qposadr, *jnt_dofadr, *jnt_bodyid, *jnt_limited;
+  const double *jnt_pos /*3*/, *jnt_axis /*3*/, *jnt_range /*2*/, *jnt_solref /*2*/,
+      *jnt_solimp /*5*/, *jnt_margin, *jnt_stiffness;
+  const double *qpos0 /* nq */, *qpos_spring /* nq */;
+  /* dofs */
+  const int32_t *dof_bodyid, *dof_jntid, *dof_parentid;
+  const uint64_t *dof_bodymask; /* bit b set: dof is on the kinematic chain of body b */
+  const double *dof_armature, *dof_damping, *dof_invweight0, *dof_frictionloss;
+  /* geoms */
+  const int32_t *geom_type, *geom_bodyid, *geom_contype, *geom_conaffinity, *geom_condim,
+      *geom_priority, *geom_dataid;
+  const double *geom_size /*3*/, *geom_pos /*3*/, *geom_quat /*4*/, *geom_friction /*3*/,
+      *geom_solmix, *geom_solref /*2*/, *geom_solimp /*5*/, *geom_margin, *geom_gap,
+      *geom_rbound;
+  /* sites */
+  const int32_t *site_bodyid;
+  const double *site_pos /*3*/, *site_quat /*4*/;
+  /* actuators (joint transmission, gain fixed, bias affine: <position>/<motor>) */
+  const int32_t *actuator_trnid, *actuator_forcelimited, *actuator_ctrllimited;
+  const double *actuator_gear, *actuator_gainprm /*3*/, *actuator_biasprm /*3*/,
+      *actuator_forcerange /*2*/, *actuator_ctrlrange /*2*/;
+  /* sensors */
+  const int32_t *sensor_type, *sensor_objtype, *sensor_objid, *sensor_reftype, *sensor_refid,
+      *sensor_adr, *sensor_dim, *sensor_intprm /*3*/;
+  const uint32_t *sensor_geommask1 /*MASK_WORDS*/, *sensor_geommask2 /*MASK_WORDS*/;
+  /* static broadphase: candidate geom pairs, geom1 has the lower geom type */
+  const int32_t *pair_geom1, *pair_geom2;
+  /* heightfields */
+  const int32_t *hfield_nrow, *hfield_ncol, *hfield_adr;
+  const double *hfield_size /*4*/, *hfield_data /* nhfielddata, normalised [0,1] */;
+} mjxModelDesc;
+
+size_t mjx_model_desc_size(void); /* sizeof(mjxModelDesc): ABI check for FFI bindings */
+
+typedef struct mjxModel_ mjxModel; /* device-resident fp32 model (opaque) */
+typedef struct mjxSim_ mjxSim;     /* nworld batched data + workspace (opaque) */
+
+const char* mjx_last_error(void);
+int mjx_abi_version(void);
+
+/* Upload a compiled model to HBM (fp32).  `device` = HIP device ordinal. */
+int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out);
+int mjx_model_destroy(mjxModel* model);
+
+/* Allocate batched data for `nworld` worlds.  nconmax: contacts per world (the
+ * reference's per-world budget, sim/sim.py:82-92); njmax: constraint rows per world.
+ * Data starts at qpos0 (mj_resetData semantics). */
+int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mjxSim** out);
+int mjx_sim_destroy(mjxSim* sim);
+
+/* One mj_step (forward + implicitfast/Euler integration) for every world, repeated
+ * `nsubstep` times inside ONE kernel launch (ctrl/xfrc/qfrc_applied held fixed). */
+int mjx_step(mjxSim* sim, int nsubstep, void* stream);
+/* mj_forward without integration (kinematics/sensors/acc for the current state). */
+int mjx_forward(mjxSim* sim, void* stream);
+/* mj_resetData on worlds where mask[w] != 0 (mask: device uint8[nworld]; NULL = all). */
+int mjx_reset(mjxSim* sim, const uint8_t* mask, void* stream);
+
+/* Field access.  Data fields have a leading nworld dimension; model fields a
+ * leading dimension of 1 (shared, world stride 0) or nworld after expansion.
+ * The returned DLManagedTensor aliases library memory (float32/int32 on the sim's
+ * device); call its deleter when done.  Pointers are stable for the sim's
+ * lifetime except that mjx_expand_field reallocates that model field. */
+struct DLManagedTensor;
+int mjx_field(mjxSim* sim, const char* name, struct DLManagedTensor** out);
+int mjx_field_count(const mjxSim* sim);
+const char* mjx_field_name(const mjxSim* sim, int i);
+int mjx_expand_field(mjxSim* sim, const char* name, void* stream);
+int mjx_field_is_expanded(const mjxSim* sim, const char* name);
+
+/* Diagnostics: per-sim counters (max contacts/rows seen, overflow events) as
+ * int32[8] written to host `out`; synchronises the stream. */
+int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJX355_H_ */

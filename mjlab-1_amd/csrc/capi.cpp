@@ -1,0 +1,396 @@
+// capi.cpp — the extern "C" boundary declared in include/mjx355.h.
+//
+// Owns every device buffer (model blob, per-field data arrays, stats), hands out
+// DLPack aliases, and enqueues the engine kernels on the caller's HIP stream.  The
+// Python host mirror of mjlab.sim.Simulation (mjlab_amd/sim/sim.py) binds this with
+// ctypes; INTEGRATION.md shows the same binding for other hosts.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mjx355.h"
+#include "engine.h"
+
+// ---------------------------------------------------------------- minimal DLPack ABI
+extern "C" {
+typedef struct { int32_t device_type; int32_t device_id; } DLDevice;
+typedef struct { uint8_t code; uint8_t bits; uint16_t lanes; } DLDataType;
+typedef struct {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+} DLTensor;
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(struct DLManagedTensor*);
+};
+}
+static const int32_t kDLROCM = 10;
+
+namespace {
+thread_local std::string g_err;
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) return fail(std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct FieldInfo {
+  void* ptr;
+  bool is_float;
+  int64_t count, width;
+  bool per_world;     // data field (leading nworld) or expanded model field
+  bool model;
+};
+}  // namespace
+
+struct mjxModel_ {
+  int device;
+  mjx::Dims d;
+  mjx::Opt o;
+  mjx::DModel dm;
+  std::vector<void*> allocs;
+  // host fp32 copies of float fields (defaults for expansion)
+  std::map<std::string, std::vector<float>> host_float;
+  std::map<std::string, std::pair<int64_t, int64_t>> float_dims;  // count, width
+  std::map<std::string, std::pair<int64_t, int64_t>> int_dims;
+};
+
+struct mjxSim_ {
+  const mjxModel_* model;
+  int nworld;
+  mjx::Dims d;
+  mjx::DModel dm;  // per-sim copy: expanded fields point to per-world buffers
+  mjx::DData dd;
+  mjx::Lds lds;
+  void* arena = nullptr;
+  mjx::Params* dparams = nullptr;  // device copy of the launch parameters
+  std::vector<void*> expanded_allocs;
+  std::map<std::string, FieldInfo> fields;
+  std::vector<std::string> names;
+  int32_t* stats = nullptr;
+};
+
+static mjx::Params host_params(const mjxSim_* s) {
+  mjx::Params p;
+  p.d = s->d;
+  p.o = s->model->o;
+  p.m = s->dm;
+  p.D = s->dd;
+  p.L = s->lds;
+  return p;
+}
+
+// Upload the launch parameters (stream-ordered, so later launches see the new copy).
+static int sync_params(mjxSim_* s, void* stream) {
+  static thread_local mjx::Params staging;
+  staging = host_params(s);
+  HIPCHK(hipMemcpyAsync(s->dparams, &staging, sizeof(mjx::Params), hipMemcpyHostToDevice,
+                        (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+extern "C" {
+
+const char* mjx_last_error(void) { return g_err.c_str(); }
+int mjx_abi_version(void) { return MJX_ABI_VERSION; }
+size_t mjx_model_desc_size(void) { return sizeof(mjxModelDesc); }
+
+int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
+  if (!desc || !out) return fail("null argument");
+  if (desc->abi_version != MJX_ABI_VERSION) return fail("ABI version mismatch");
+  if (desc->nbody > mjx::kMaxBodies) return fail("at most 64 bodies per world supported");
+  if (desc->cone != 0) return fail("only pyramidal cones are supported");
+  HIPCHK(hipSetDevice(device));
+  auto* m = new mjxModel_();
+  m->device = device;
+  mjx::Dims& d = m->d;
+  d.nq = desc->nq; d.nv = desc->nv; d.nu = desc->nu; d.nbody = desc->nbody; d.njnt = desc->njnt;
+  d.ngeom = desc->ngeom; d.nsite = desc->nsite; d.nsensor = desc->nsensor;
+  d.nsensordata = desc->nsensordata; d.npair = desc->npair; d.nhfield = desc->nhfield;
+  d.nhfielddata = desc->nhfielddata; d.nlevel = desc->nlevel;
+  d.nchild = desc->body_childadr[desc->nbody];
+  if (d.nchild < 1) d.nchild = 1;
+  d.nmocap = 0;
+  for (int b = 0; b < d.nbody; b++)
+    if (desc->body_mocapid[b] >= 0) d.nmocap++;
+  d.nconmax = 0; d.njmax = 0;
+  mjx::Opt& o = m->o;
+  o.timestep = (float)desc->timestep; o.tolerance = (float)desc->tolerance;
+  o.ls_tolerance = (float)desc->ls_tolerance; o.impratio = (float)desc->impratio;
+  o.meaninertia = (float)desc->meaninertia;
+  for (int i = 0; i < 3; i++) o.gravity[i] = (float)desc->gravity[i];
+  o.iterations = desc->iterations; o.ls_iterations = desc->ls_iterations;
+  o.integrator = desc->integrator; o.cone = desc->cone;
+
+  auto upload = [&](const void* src, size_t bytes, void** dst) -> int {
+    size_t nb = bytes > 0 ? bytes : 4;
+    HIPCHK(hipMalloc(dst, nb));
+    m->allocs.push_back(*dst);
+    if (bytes > 0) HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(*dst, 0, nb));
+    return 0;
+  };
+#define X_INT(name, cnt, w)                                                              \
+  {                                                                                      \
+    size_t n_ = (size_t)(cnt) * (w);                                                     \
+    void* p_ = nullptr;                                                                  \
+    if (upload(desc->name, n_ * sizeof(int32_t), &p_)) { delete m; return -1; }         \
+    m->dm.name = (const int32_t*)p_;                                                     \
+    m->int_dims[#name] = {(int64_t)(cnt), (int64_t)(w)};                                 \
+  }
+#define X_FLT(name, cnt, w)                                                              \
+  {                                                                                      \
+    size_t n_ = (size_t)(cnt) * (w);                                                     \
+    std::vector<float> h_(n_);                                                           \
+    for (size_t i = 0; i < n_; i++) h_[i] = (float)desc->name[i];                        \
+    void* p_ = nullptr;                                                                  \
+    if (upload(h_.data(), n_ * sizeof(float), &p_)) { delete m; return -1; }            \
+    m->dm.name = (const float*)p_;                                                       \
+    m->dm.name##_ws = 0;                                                                 \
+    m->host_float[#name] = std::move(h_);                                                \
+    m->float_dims[#name] = {(int64_t)(cnt), (int64_t)(w)};                               \
+  }
+  MJX_MODEL_INT_FIELDS(X_INT)
+  MJX_MODEL_FLOAT_FIELDS(X_FLT)
+#undef X_INT
+#undef X_FLT
+  void* p = nullptr;
+  if (upload(desc->dof_bodymask, sizeof(uint64_t) * d.nv, &p)) { delete m; return -1; }
+  m->dm.dof_bodymask = (const uint64_t*)p;
+  if (upload(desc->sensor_geommask1, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
+  m->dm.sensor_geommask1 = (const uint32_t*)p;
+  if (upload(desc->sensor_geommask2, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
+  m->dm.sensor_geommask2 = (const uint32_t*)p;
+  *out = m;
+  return 0;
+}
+
+int mjx_model_destroy(mjxModel* m) {
+  if (!m) return 0;
+  for (void* p : m->allocs) (void)hipFree(p);
+  delete m;
+  return 0;
+}
+
+int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mjxSim** out) {
+  if (!model || !out) return fail("null argument");
+  if (nworld <= 0) return fail("nworld must be positive");
+  if (nconmax <= 0 || nconmax > mjx::kWave)
+    return fail("nconmax (contacts held per world) must be in [1, 64]");
+  if (njmax <= 0) return fail("njmax must be positive");
+  HIPCHK(hipSetDevice(model->device));
+  auto* s = new mjxSim_();
+  s->model = model;
+  s->nworld = nworld;
+  s->d = model->d;
+  s->d.nconmax = nconmax;
+  s->d.njmax = njmax;
+  s->dm = model->dm;
+  s->lds = mjx::make_lds(s->d);
+  if ((size_t)s->lds.total * 4 > 160 * 1024) {
+    delete s;
+    return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
+  }
+  const mjx::Dims& d = s->d;
+  // data arena: one allocation, 256-B aligned sub-buffers
+  size_t off = 0;
+  std::vector<std::pair<std::string, size_t>> offs;
+  auto reserve = [&](const std::string& name, size_t bytes) {
+    offs.push_back({name, off});
+    off += (bytes + 255) & ~(size_t)255;
+  };
+#define X_FLT(name, cnt, w) reserve(#name, sizeof(float) * (size_t)nworld * (cnt) * (w));
+#define X_INT(name, cnt, w) reserve(#name, sizeof(int32_t) * (size_t)nworld * (cnt) * (w));
+  MJX_DATA_FLOAT_FIELDS(X_FLT)
+  MJX_DATA_INT_FIELDS(X_INT)
+#undef X_FLT
+#undef X_INT
+  reserve("__stats", sizeof(int32_t) * 8);
+  hipError_t e = hipMalloc(&s->arena, off);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }
+  e = hipMemset(s->arena, 0, off);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
+  size_t k = 0;
+  char* base = (char*)s->arena;
+#define X_FLT(name, cnt, w)                                                                  \
+  s->dd.name = (float*)(base + offs[k++].second);                                            \
+  s->fields[#name] = FieldInfo{s->dd.name, true, (int64_t)(cnt), (int64_t)(w), true, false}; \
+  s->names.push_back(#name);
+#define X_INT(name, cnt, w)                                                                    \
+  s->dd.name = (int32_t*)(base + offs[k++].second);                                            \
+  s->fields[#name] = FieldInfo{s->dd.name, false, (int64_t)(cnt), (int64_t)(w), true, false};  \
+  s->names.push_back(#name);
+  MJX_DATA_FLOAT_FIELDS(X_FLT)
+  MJX_DATA_INT_FIELDS(X_INT)
+#undef X_FLT
+#undef X_INT
+  s->dd.stats = (int32_t*)(base + offs[k++].second);
+  s->stats = s->dd.stats;
+  // model fields visible as "model.<name>"
+  for (auto& kv : model->float_dims) {
+    FieldInfo fi{nullptr, true, kv.second.first, kv.second.second, false, true};
+    s->fields["model." + kv.first] = fi;
+    s->names.push_back("model." + kv.first);
+  }
+  for (auto& kv : model->int_dims) {
+    FieldInfo fi{nullptr, false, kv.second.first, kv.second.second, false, true};
+    s->fields["model." + kv.first] = fi;
+    s->names.push_back("model." + kv.first);
+  }
+  e = hipMalloc((void**)&s->dparams, sizeof(mjx::Params));
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc params: ") + hipGetErrorString(e)); }
+  if (sync_params(s, nullptr)) { delete s; return -1; }
+  // initial state: mj_resetData
+  if (mjx::launch_reset(d, s->dm, s->dd, nullptr, nworld, nullptr) != hipSuccess) {
+    delete s;
+    return fail("reset launch failed");
+  }
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) { delete s; return fail(std::string("sync: ") + hipGetErrorString(e)); }
+  *out = s;
+  return 0;
+}
+
+int mjx_sim_destroy(mjxSim* s) {
+  if (!s) return 0;
+  if (s->arena) (void)hipFree(s->arena);
+  if (s->dparams) (void)hipFree(s->dparams);
+  for (void* p : s->expanded_allocs) (void)hipFree(p);
+  delete s;
+  return 0;
+}
+
+int mjx_step(mjxSim* s, int nsubstep, void* stream) {
+  if (!s) return fail("null sim");
+  if (nsubstep < 1) return fail("nsubstep must be >= 1");
+  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, nsubstep, 1,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) return fail(std::string("step launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int mjx_forward(mjxSim* s, void* stream) {
+  if (!s) return fail("null sim");
+  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, 1, 0,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) return fail(std::string("forward launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int mjx_reset(mjxSim* s, const uint8_t* mask, void* stream) {
+  if (!s) return fail("null sim");
+  hipError_t e = mjx::launch_reset(s->d, s->dm, s->dd, mask, s->nworld, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(std::string("reset launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+static void dl_deleter(DLManagedTensor* t) {
+  if (!t) return;
+  delete[] t->dl_tensor.shape;
+  delete t;
+}
+
+static const void* model_field_ptr(const mjxSim_* s, const std::string& name, int* ws) {
+  *ws = 0;
+#define X_FLT(n, cnt, w) if (name == #n) { *ws = s->dm.n##_ws; return s->dm.n; }
+#define X_INT(n, cnt, w) if (name == #n) { return s->dm.n; }
+  MJX_MODEL_FLOAT_FIELDS(X_FLT)
+  MJX_MODEL_INT_FIELDS(X_INT)
+#undef X_FLT
+#undef X_INT
+  return nullptr;
+}
+
+int mjx_field(mjxSim* s, const char* cname, DLManagedTensor** out) {
+  if (!s || !cname || !out) return fail("null argument");
+  std::string name(cname);
+  auto it = s->fields.find(name);
+  if (it == s->fields.end()) return fail("unknown field '" + name + "'");
+  const FieldInfo& fi = it->second;
+  void* ptr = fi.ptr;
+  int64_t lead = s->nworld;
+  if (fi.model) {
+    int ws = 0;
+    ptr = const_cast<void*>(model_field_ptr(s, name.substr(6), &ws));
+    lead = ws > 0 ? s->nworld : 1;
+  }
+  auto* t = new DLManagedTensor();
+  std::vector<int64_t> shape;
+  shape.push_back(lead);
+  if (!(fi.count == 1 && fi.width == 1 && !fi.model)) shape.push_back(fi.count);
+  if (fi.width > 1) shape.push_back(fi.width);
+  t->dl_tensor.data = ptr;
+  t->dl_tensor.device = DLDevice{kDLROCM, s->model->device};
+  t->dl_tensor.ndim = (int32_t)shape.size();
+  t->dl_tensor.dtype = fi.is_float ? DLDataType{2, 32, 1} : DLDataType{0, 32, 1};
+  t->dl_tensor.shape = new int64_t[shape.size()];
+  for (size_t i = 0; i < shape.size(); i++) t->dl_tensor.shape[i] = shape[i];
+  t->dl_tensor.strides = nullptr;  // compact row-major
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = nullptr;
+  t->deleter = dl_deleter;
+  *out = t;
+  return 0;
+}
+
+int mjx_field_count(const mjxSim* s) { return s ? (int)s->names.size() : 0; }
+const char* mjx_field_name(const mjxSim* s, int i) {
+  if (!s || i < 0 || i >= (int)s->names.size()) return nullptr;
+  return s->names[i].c_str();
+}
+
+int mjx_field_is_expanded(const mjxSim* s, const char* cname) {
+  if (!s || !cname) return 0;
+  int ws = 0;
+  model_field_ptr(s, std::string(cname), &ws);
+  return ws > 0;
+}
+
+int mjx_expand_field(mjxSim* s, const char* cname, void* stream) {
+  if (!s || !cname) return fail("null argument");
+  std::string name(cname);
+  auto hit = s->model->host_float.find(name);
+  if (hit == s->model->host_float.end())
+    return fail("field '" + name + "' is not an expandable float model field");
+  const std::vector<float>& h = hit->second;
+  size_t per = h.size();
+  float* buf = nullptr;
+  size_t bytes = sizeof(float) * (per > 0 ? per : 1) * (size_t)s->nworld;
+  HIPCHK(hipMalloc((void**)&buf, bytes));
+  s->expanded_allocs.push_back(buf);
+  // tile the CURRENT values (default model values) to every world
+  int ws = 0;
+  const float* cur = (const float*)model_field_ptr(s, name, &ws);
+  if (ws > 0) return fail("field '" + name + "' already expanded");
+  for (int w = 0; w < s->nworld; w++)
+    HIPCHK(hipMemcpyAsync(buf + (size_t)w * per, cur, sizeof(float) * per, hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
+#define X_FLT(n, cnt, w) if (name == #n) { s->dm.n = buf; s->dm.n##_ws = (int)per; }
+  MJX_MODEL_FLOAT_FIELDS(X_FLT)
+#undef X_FLT
+  return sync_params(s, stream);
+}
+
+int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {
+  if (!s || !out) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(out, s->stats, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

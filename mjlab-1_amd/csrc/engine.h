@@ -1,0 +1,90 @@
+// engine.h — device-side model/data descriptors and kernel launchers of the mjx355
+// HIP engine (gfx950).  Host code (capi.cpp) fills these structs; engine.hip reads
+// them.  Layout and ownership are described in DESIGN.md section 3.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fields.h"
+
+namespace mjx {
+
+constexpr int kWave = 64;        // CDNA wavefront width
+constexpr int kMaskWords = 4;    // contact-sensor geom masks (128 geoms)
+constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
+constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
+
+struct Dims {
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
+  int nhfield, nhfielddata, nlevel, nchild, nmocap;
+  int nconmax;  // contacts per world held in LDS
+  int njmax;    // constraint rows per world held in LDS
+};
+
+struct Opt {
+  float timestep, tolerance, ls_tolerance, impratio, meaninertia;
+  float gravity[3];
+  int iterations, ls_iterations, integrator, cone;
+};
+
+// Device model: int fields shared, float fields with a per-world stride (0 = shared).
+struct DModel {
+#define X_INT(name, cnt, w) const int32_t* name;
+#define X_FLT(name, cnt, w) const float* name; int name##_ws;
+  MJX_MODEL_INT_FIELDS(X_INT)
+  MJX_MODEL_FLOAT_FIELDS(X_FLT)
+#undef X_INT
+#undef X_FLT
+  const uint64_t* dof_bodymask;
+  const uint32_t* sensor_geommask1;
+  const uint32_t* sensor_geommask2;
+};
+
+struct DData {
+#define X_FLT(name, cnt, w) float* name;
+#define X_INT(name, cnt, w) int32_t* name;
+  MJX_DATA_FLOAT_FIELDS(X_FLT)
+  MJX_DATA_INT_FIELDS(X_INT)
+#undef X_FLT
+#undef X_INT
+  int32_t* stats;  // [8] global counters (atomics)
+};
+
+// Per-world LDS carve (offsets in 4-byte words).
+struct Lds {
+  int qpos, qvel, ctrl, qacc_ws, qfrc_applied, xfrc;
+  int xpos, xquat, xmat, xipos, ximat, xanchor, xaxis;
+  int stmass, subtree_com, cinert, crb, cvel, cacc, stlin, stang;
+  int cdof, cdofdot, gxpos, gxmat, sxpos, sxmat;
+  int M, H;
+  int qfrc_bias, qfrc_passive, qfrc_act, qfrc_smooth, qacc_smooth, x, Mx, grad, srch, Ms,
+      qfrc_con, vtmp, act_force, act_len, act_vel;
+  int con_g1, con_g2, con_key, con_dist, con_pos, con_frame, con_mu, con_solref,
+      con_solimp, con_imargin, con_dim, con_efc;
+  int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_type;
+  int red;      // 2*kWave scratch for reductions
+  int ints;     // small int block: [0]=ncon [1]=nefc [2]=nlimit [3]=overflow
+  int total;
+};
+
+Lds make_lds(const Dims& d);
+
+// Everything a launch needs, resident in device memory (read through the scalar cache
+// instead of occupying ~500 SGPRs of kernarg space).
+struct Params {
+  Dims d;
+  Opt o;
+  DModel m;
+  DData D;
+  Lds L;
+};
+
+// Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
+// `host`; `host` is used only for the launch geometry.
+hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
+                       int integrate, hipStream_t stream);
+hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
+                        int nworld, hipStream_t stream);
+
+}  // namespace mjx

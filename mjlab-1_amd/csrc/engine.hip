@@ -1,0 +1,1491 @@
+// engine.hip — batched mj_step for MI355X (gfx950): one wavefront (64 lanes) per world.
+//
+// Each workgroup is ONE wave that owns ONE world.  The world's state and every
+// intermediate (body frames, com-based inertias, mass matrix, contacts, dense
+// constraint Jacobian, Newton Hessian) lives in that workgroup's LDS for the whole
+// step, so HBM sees only the coalesced load of the state at the start and the
+// coalesced store of state + API-visible kinematics at the end (the "algorithmic
+// bytes" of DESIGN.md section 4).  Stages map to lanes as:
+//   tree recursions  -> one lane per body of the current tree level (level-synchronous)
+//   dof stages       -> one lane per dof (M rows, Jacobian columns, J^T f)
+//   broad+narrowphase-> one lane per candidate geom pair, LDS-atomic append, then a
+//                       64-lane bitonic sort on (pair, sub-contact) so contact order is
+//                       deterministic and equals the CPU oracle's pair order
+//   constraint rows  -> one lane per row
+//   Cholesky / H     -> one lane per lower-triangle element (right-looking, in LDS)
+// Semantics follow the reference's mujoco_warp.step (src/mjlab/sim/sim.py:267-273)
+// stage by stage, restated in oracle/oracle.c (the parity checker).
+#include <float.h>
+#include <math.h>
+
+#include "engine.h"
+
+namespace mjx {
+
+#define MINVAL 1e-15f
+#define MINMU 1e-5f
+#define MINIMP 0.0001f
+#define MAXIMP 0.9999f
+
+enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
+enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
+enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum { SENS_GYRO = 0, SENS_VELOCIMETER = 1, SENS_ACCELEROMETER = 2, SENS_SUBTREEANGMOM = 3,
+       SENS_CONTACT = 4, SENS_FRAMEPOS = 5, SENS_FRAMEQUAT = 6, SENS_JOINTPOS = 7,
+       SENS_JOINTVEL = 8 };
+enum { OBJ_SITE = 6 };
+enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
+
+// --------------------------------------------------------------------------- host: LDS
+Lds make_lds(const Dims& d) {
+  Lds L{};
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };  // 16-B aligned carve
+  const int nb = d.nbody, nv = d.nv, C = d.nconmax, R = d.njmax;
+  L.qpos = take(d.nq); L.qvel = take(nv); L.ctrl = take(d.nu); L.qacc_ws = take(nv);
+  L.qfrc_applied = take(nv); L.xfrc = take(6 * nb);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.ximat = take(9 * nb); L.xanchor = take(3 * d.njnt); L.xaxis = take(3 * d.njnt);
+  L.stmass = take(nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb);
+  L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.stlin = take(3 * nb);
+  L.stang = take(3 * nb);
+  L.cdof = take(6 * nv); L.cdofdot = take(6 * nv);
+  L.gxpos = take(3 * d.ngeom); L.gxmat = take(9 * d.ngeom);
+  L.sxpos = take(3 * d.nsite); L.sxmat = take(9 * d.nsite);
+  L.M = take(nv * nv); L.H = take(nv * nv);
+  L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_act = take(nv);
+  L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.x = take(nv); L.Mx = take(nv);
+  L.grad = take(nv); L.srch = take(nv); L.Ms = take(nv); L.qfrc_con = take(nv);
+  L.vtmp = take(nv); L.act_force = take(d.nu); L.act_len = take(d.nu); L.act_vel = take(d.nu);
+  L.con_g1 = take(C); L.con_g2 = take(C); L.con_key = take(C); L.con_dist = take(C);
+  L.con_pos = take(3 * C); L.con_frame = take(9 * C); L.con_mu = take(2 * C);
+  L.con_solref = take(2 * C); L.con_solimp = take(5 * C); L.con_imargin = take(C);
+  L.con_dim = take(C); L.con_efc = take(C);
+  L.efc_J = take(R * nv); L.efc_aref = take(R); L.efc_D = take(R); L.efc_jar = take(R);
+  L.efc_Js = take(R); L.efc_force = take(R); L.efc_cid = take(R); L.efc_type = take(R);
+  L.red = take(2 * kWave);
+  L.ints = take(8);
+  L.total = o;
+  return L;
+}
+
+// --------------------------------------------------------------------------- device math
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(const float* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ void st3(float* p, V3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float norm(V3 a) { return sqrtf(dot(a, a)); }
+// row-major 3x3
+__device__ __forceinline__ V3 mulv(const float* M, V3 v) {
+  return {M[0] * v.x + M[1] * v.y + M[2] * v.z, M[3] * v.x + M[4] * v.y + M[5] * v.z,
+          M[6] * v.x + M[7] * v.y + M[8] * v.z};
+}
+__device__ __forceinline__ V3 mulTv(const float* M, V3 v) {
+  return {M[0] * v.x + M[3] * v.y + M[6] * v.z, M[1] * v.x + M[4] * v.y + M[7] * v.z,
+          M[2] * v.x + M[5] * v.y + M[8] * v.z};
+}
+__device__ __forceinline__ void mat3mul(float* R, const float* A, const float* B) {
+  float t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) R[i] = t[i];
+}
+struct Q4 { float w, x, y, z; };
+__device__ __forceinline__ Q4 q4(const float* p) { return {p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ void st4(float* p, Q4 q) { p[0] = q.w; p[1] = q.x; p[2] = q.y; p[3] = q.z; }
+__device__ __forceinline__ Q4 qmul(Q4 a, Q4 b) {
+  return {a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+          a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x, a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w};
+}
+__device__ __forceinline__ Q4 qnorm(Q4 q) {
+  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  if (n < MINVAL) return {1, 0, 0, 0};
+  float s = 1.0f / n;
+  return {q.w * s, q.x * s, q.y * s, q.z * s};
+}
+__device__ __forceinline__ void qmat(float* M, Q4 q) {
+  q = qnorm(q);
+  float w = q.w, x = q.x, y = q.y, z = q.z;
+  M[0] = 1 - 2 * (y * y + z * z); M[1] = 2 * (x * y - w * z); M[2] = 2 * (x * z + w * y);
+  M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
+  M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ Q4 qaxisangle(V3 a, float ang) {
+  float s = sinf(0.5f * ang);
+  return {cosf(0.5f * ang), a.x * s, a.y * s, a.z * s};
+}
+// spatial algebra, vectors [ang; lin]
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* s) {
+  V3 w = v3(v), u = v3(v + 3), a = v3(s), b = v3(s + 3);
+  st3(r, cross(w, a));
+  st3(r + 3, cross(w, b) + cross(u, a));
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  V3 w = v3(v), u = v3(v + 3), a = v3(f), b = v3(f + 3);
+  st3(r, cross(w, a) + cross(u, b));
+  st3(r + 3, cross(w, b));
+}
+__device__ __forceinline__ void inert_mul(float* r, const float* I, const float* v) {
+  V3 w = v3(v), u = v3(v + 3), h = v3(I + 6);
+  float m = I[9];
+  V3 t = {I[0] * w.x + I[3] * w.y + I[4] * w.z, I[3] * w.x + I[1] * w.y + I[5] * w.z,
+          I[4] * w.x + I[5] * w.y + I[2] * w.z};
+  st3(r, t + cross(h, u));
+  st3(r + 3, u * m - cross(h, w));
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// --------------------------------------------------------------------------- wave utils
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  *total = __shfl(x, kWave - 1);
+  return x - v;
+}
+__device__ __forceinline__ void sync() { __syncthreads(); }
+
+#define MF(f) (m.f + (size_t)w * m.f##_ws)
+
+// Dense Cholesky of the nv x nv SPD matrix A (row-major, lower used) in place.
+// Right-looking; the trailing update is spread over lanes by lower-triangle element.
+__device__ void chol_lds(float* A, int n, int lane) {
+  for (int k = 0; k < n; k++) {
+    float piv = A[k * n + k];
+    piv = sqrtf(fmaxf(piv, MINVAL));
+    float inv = 1.0f / piv;
+    sync();
+    if (lane == 0) A[k * n + k] = piv;
+    for (int i = k + 1 + lane; i < n; i += kWave) A[i * n + k] *= inv;
+    sync();
+    int m = n - k - 1;  // trailing size
+    int cnt = m * (m + 1) / 2;
+    for (int e = lane; e < cnt; e += kWave) {
+      // e -> (i, j), i >= j, over the trailing block
+      int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
+      while ((i + 1) * (i + 2) / 2 <= e) i++;
+      while (i * (i + 1) / 2 > e) i--;
+      int j = e - i * (i + 1) / 2;
+      i += k + 1; j += k + 1;
+      A[i * n + j] -= A[i * n + k] * A[j * n + k];
+    }
+    sync();
+  }
+}
+// Solve L L^T x = b in place (b in LDS vector).
+__device__ void chol_solve_lds(const float* L, int n, float* x, int lane) {
+  for (int k = 0; k < n; k++) {
+    float xk = x[k] / L[k * n + k];
+    sync();
+    if (lane == 0) x[k] = xk;
+    for (int i = k + 1 + lane; i < n; i += kWave) x[i] -= L[i * n + k] * xk;
+    sync();
+  }
+  for (int k = n - 1; k >= 0; k--) {
+    float xk = x[k] / L[k * n + k];
+    sync();
+    if (lane == 0) x[k] = xk;
+    for (int i = lane; i < k; i += kWave) x[i] -= L[k * n + i] * xk;
+    sync();
+  }
+}
+
+// --------------------------------------------------------------------------- collision
+struct ConOut {
+  float* S;
+  int* ints;
+  const Lds* L;
+  int cap;
+};
+__device__ __forceinline__ void append(const ConOut& co, int key, int g1, int g2, float dist,
+                                       V3 pos, V3 n) {
+  int slot = atomicAdd(&co.ints[0], 1);
+  if (slot >= co.cap) {
+    atomicOr(&co.ints[3], 1);
+    return;
+  }
+  const Lds& L = *co.L;
+  int* Si = reinterpret_cast<int*>(co.S);
+  Si[L.con_key + slot] = key;
+  Si[L.con_g1 + slot] = g1;
+  Si[L.con_g2 + slot] = g2;
+  co.S[L.con_dist + slot] = dist;
+  st3(co.S + L.con_pos + 3 * slot, pos);
+  st3(co.S + L.con_frame + 9 * slot, n);
+}
+__device__ __forceinline__ int plane_sphere(const ConOut& co, int key, int g1, int g2, V3 pp,
+                                            V3 n, V3 c, float r, float margin) {
+  float dist = dot(c - pp, n) - r;
+  if (dist > margin) return 0;
+  append(co, key, g1, g2, dist, c - n * (r + 0.5f * dist), n);
+  return 1;
+}
+__device__ __forceinline__ int sphere_sphere(const ConOut& co, int key, int g1, int g2, V3 p1,
+                                             float r1, V3 p2, float r2, float margin) {
+  V3 dif = p2 - p1;
+  float cd = norm(dif);
+  float dist = cd - r1 - r2;
+  if (dist > margin) return 0;
+  V3 n = cd < MINVAL ? V3{1, 0, 0} : dif * (1.0f / cd);
+  append(co, key, g1, g2, dist, p1 + n * (r1 + 0.5f * dist), n);
+  return 1;
+}
+__device__ __forceinline__ float clamp01(float t) { return t < 0 ? 0 : (t > 1 ? 1 : t); }
+__device__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
+  V3 u = a1 - a0, v = b1 - b0, wv = a0 - b0;
+  float a = dot(u, u), b = dot(u, v), c = dot(v, v), dd = dot(u, wv), e = dot(v, wv);
+  float den = a * c - b * b, s, t;
+  if (a < MINVAL && c < MINVAL) { s = t = 0; }
+  else if (a < MINVAL) { s = 0; t = clamp01(e / c); }
+  else if (c < MINVAL) { t = 0; s = clamp01(-dd / a); }
+  else {
+    s = den > MINVAL * a * c ? (b * e - c * dd) / den : 0;
+    s = clamp01(s);
+    t = (b * s + e) / c;
+    if (t < 0) { t = 0; s = clamp01(-dd / a); }
+    else if (t > 1) { t = 1; s = clamp01((b - dd) / a); }
+  }
+  *pa = a0 + u * s;
+  *pb = b0 + v * t;
+}
+
+// --------------------------------------------------------------------------- impedance
+__device__ float impedance(const float* si, float pos, float margin) {
+  float dmin = fminf(MAXIMP, fmaxf(MINIMP, si[0])), dmax = fminf(MAXIMP, fmaxf(MINIMP, si[1]));
+  float width = fmaxf(0.f, si[2]), mid = fminf(1.f, fmaxf(MINIMP, si[3])), power = fmaxf(1.f, si[4]);
+  if (dmin == dmax || width <= MINVAL) return 0.5f * (dmin + dmax);
+  float x = fabsf(pos - margin) / width;
+  if (x >= 1 || x <= 0) return x >= 1 ? dmax : dmin;
+  float y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1);
+  else y = 1 - powf(1 - x, power) / powf(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+// --------------------------------------------------------------------------- kernel
+__global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ P, int nworld,
+                                                     int nsubstep, int integrate) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  const Dims& d = P->d;
+  const Opt& o = P->o;
+  const DModel& m = P->m;
+  const DData& D = P->D;
+  const Lds& L = P->L;
+  const int w = blockIdx.x;
+  if (w >= nworld) return;
+  const int lane = threadIdx.x;
+  int* Si = reinterpret_cast<int*>(S);
+  int* ints = Si + L.ints;
+  const int nv = d.nv, nb = d.nbody, nq = d.nq, nu = d.nu;
+  const float h = o.timestep;
+
+  // ------------------------------------------------------------- load state (coalesced)
+  for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
+  for (int i = lane; i < nv; i += kWave) {
+    S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
+    S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
+    S[L.qfrc_applied + i] = D.qfrc_applied[(size_t)w * nv + i];
+  }
+  for (int i = lane; i < nu; i += kWave) S[L.ctrl + i] = D.ctrl[(size_t)w * nu + i];
+  for (int i = lane; i < 6 * nb; i += kWave) S[L.xfrc + i] = D.xfrc_applied[(size_t)w * 6 * nb + i];
+  float time = D.time[w];
+  int any_xfrc = 0;
+  for (int i = lane; i < 6 * nb; i += kWave) any_xfrc |= (D.xfrc_applied[(size_t)w * 6 * nb + i] != 0.f);
+  any_xfrc = __any(any_xfrc);
+  sync();
+
+  const float* body_pos = MF(body_pos);
+  const float* body_quat = MF(body_quat);
+  const float* body_ipos = MF(body_ipos);
+  const float* body_iquat = MF(body_iquat);
+  const float* body_mass = MF(body_mass);
+  const float* body_inertia = MF(body_inertia);
+  const float* jnt_pos = MF(jnt_pos);
+  const float* jnt_axis = MF(jnt_axis);
+  const float* qpos0 = MF(qpos0);
+
+  int niter_last = 0;
+  for (int sub = 0; sub < nsubstep; sub++) {
+    // =========================================================== kinematics (levels)
+    if (lane == 0) {
+      S[L.xpos + 0] = S[L.xpos + 1] = S[L.xpos + 2] = 0;
+      S[L.xquat + 0] = 1; S[L.xquat + 1] = S[L.xquat + 2] = S[L.xquat + 3] = 0;
+    }
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float Rp[9];
+        qmat(Rp, q4(S + L.xquat + 4 * p));
+        V3 pos = v3(S + L.xpos + 3 * p) + mulv(Rp, v3(body_pos + 3 * b));
+        Q4 q = qmul(q4(S + L.xquat + 4 * p), q4(body_quat + 4 * b));
+        int mid = m.body_mocapid[b];
+        if (mid >= 0) {
+          pos = v3(D.mocap_pos + ((size_t)w * d.nmocap + mid) * 3);
+          q = q4(D.mocap_quat + ((size_t)w * d.nmocap + mid) * 4);
+        }
+        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
+        for (int k = j0; k < j1; k++) {
+          int a = m.jnt_qposadr[k];
+          float R[9];
+          if (m.jnt_type[k] == JNT_FREE) {
+            pos = v3(S + L.qpos + a);
+            q = qnorm(q4(S + L.qpos + a + 3));
+            st3(S + L.xanchor + 3 * k, pos);
+            qmat(R, q);
+            st3(S + L.xaxis + 3 * k, mulv(R, v3(jnt_axis + 3 * k)));
+            continue;
+          }
+          qmat(R, q);
+          V3 anchor = mulv(R, v3(jnt_pos + 3 * k)) + pos;
+          V3 axis = mulv(R, v3(jnt_axis + 3 * k));
+          st3(S + L.xanchor + 3 * k, anchor);
+          st3(S + L.xaxis + 3 * k, axis);
+          if (m.jnt_type[k] == JNT_HINGE) {
+            q = qmul(q, qaxisangle(v3(jnt_axis + 3 * k), S[L.qpos + a] - qpos0[a]));
+            qmat(R, q);
+            pos = anchor - mulv(R, v3(jnt_pos + 3 * k));
+          } else if (m.jnt_type[k] == JNT_SLIDE) {
+            pos = pos + axis * (S[L.qpos + a] - qpos0[a]);
+          }
+        }
+        q = qnorm(q);
+        st3(S + L.xpos + 3 * b, pos);
+        st4(S + L.xquat + 4 * b, q);
+      }
+      sync();
+    }
+    for (int b = lane; b < nb; b += kWave) {
+      float* R = S + L.xmat + 9 * b;
+      qmat(R, q4(S + L.xquat + 4 * b));
+      st3(S + L.xipos + 3 * b, v3(S + L.xpos + 3 * b) + mulv(R, v3(body_ipos + 3 * b)));
+      float Ri[9];
+      qmat(Ri, q4(body_iquat + 4 * b));
+      mat3mul(S + L.ximat + 9 * b, R, Ri);
+    }
+    sync();
+    {
+      const float* gpos = MF(geom_pos);
+      const float* gquat = MF(geom_quat);
+      for (int g = lane; g < d.ngeom; g += kWave) {
+        int b = m.geom_bodyid[g];
+        const float* R = S + L.xmat + 9 * b;
+        st3(S + L.gxpos + 3 * g, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
+        float Rg[9];
+        qmat(Rg, q4(gquat + 4 * g));
+        mat3mul(S + L.gxmat + 9 * g, R, Rg);
+      }
+      const float* spos = MF(site_pos);
+      const float* squat = MF(site_quat);
+      for (int s = lane; s < d.nsite; s += kWave) {
+        int b = m.site_bodyid[s];
+        const float* R = S + L.xmat + 9 * b;
+        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + mulv(R, v3(spos + 3 * s)));
+        float Rs[9];
+        qmat(Rs, q4(squat + 4 * s));
+        mat3mul(S + L.sxmat + 9 * s, R, Rs);
+      }
+    }
+    // =========================================================== com / cinert / cdof
+    for (int b = lane; b < nb; b += kWave) {
+      float ms = body_mass[b];
+      S[L.stmass + b] = ms;
+      st3(S + L.subtree_com + 3 * b, v3(S + L.xipos + 3 * b) * ms);
+    }
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        float ms = S[L.stmass + b];
+        V3 c = v3(S + L.subtree_com + 3 * b);
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
+          int ch = m.body_child[k];
+          ms += S[L.stmass + ch];
+          c = c + v3(S + L.subtree_com + 3 * ch);
+        }
+        S[L.stmass + b] = ms;
+        st3(S + L.subtree_com + 3 * b, c);
+      }
+      sync();
+    }
+    for (int b = lane; b < nb; b += kWave) {
+      float ms = S[L.stmass + b];
+      V3 c = ms > MINVAL ? v3(S + L.subtree_com + 3 * b) * (1.0f / ms) : v3(S + L.xipos + 3 * b);
+      st3(S + L.subtree_com + 3 * b, c);
+    }
+    sync();
+    for (int b = lane; b < nb; b += kWave) {
+      float* c = S + L.cinert + 10 * b;
+      if (b == 0) {
+        for (int i = 0; i < 10; i++) c[i] = 0;
+        continue;
+      }
+      V3 off = v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      const float* R = S + L.ximat + 9 * b;
+      const float* I = body_inertia + 3 * b;
+      float full[9];
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+          full[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] +
+                            R[3 * i + 2] * I[2] * R[3 * j + 2];
+      V3 dv = v3(S + L.xipos + 3 * b) - off;
+      float ms = body_mass[b], dd = dot(dv, dv);
+      c[0] = full[0] + ms * (dd - dv.x * dv.x);
+      c[1] = full[4] + ms * (dd - dv.y * dv.y);
+      c[2] = full[8] + ms * (dd - dv.z * dv.z);
+      c[3] = full[1] - ms * dv.x * dv.y;
+      c[4] = full[2] - ms * dv.x * dv.z;
+      c[5] = full[5] - ms * dv.y * dv.z;
+      c[6] = ms * dv.x; c[7] = ms * dv.y; c[8] = ms * dv.z; c[9] = ms;
+    }
+    for (int k = lane; k < d.njnt; k += kWave) {
+      int b = m.jnt_bodyid[k], dof = m.jnt_dofadr[k];
+      V3 rel = v3(S + L.subtree_com + 3 * m.body_rootid[b]) - v3(S + L.xanchor + 3 * k);
+      int t = m.jnt_type[k];
+      if (t == JNT_FREE) {
+        for (int i = 0; i < 3; i++) {
+          float* c = S + L.cdof + 6 * (dof + i);
+          for (int j = 0; j < 6; j++) c[j] = 0;
+          c[3 + i] = 1;
+        }
+        const float* R = S + L.xmat + 9 * b;
+        for (int i = 0; i < 3; i++) {
+          float* c = S + L.cdof + 6 * (dof + 3 + i);
+          V3 ax = {R[i], R[3 + i], R[6 + i]};
+          st3(c, ax);
+          st3(c + 3, cross(ax, rel));
+        }
+      } else if (t == JNT_HINGE) {
+        float* c = S + L.cdof + 6 * dof;
+        V3 ax = v3(S + L.xaxis + 3 * k);
+        st3(c, ax);
+        st3(c + 3, cross(ax, rel));
+      } else if (t == JNT_SLIDE) {
+        float* c = S + L.cdof + 6 * dof;
+        c[0] = c[1] = c[2] = 0;
+        st3(c + 3, v3(S + L.xaxis + 3 * k));
+      }
+    }
+    sync();
+    // =========================================================== CRB + mass matrix
+    for (int i = lane; i < 10 * nb; i += kWave) S[L.crb + i] = S[L.cinert + i];
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        float acc[10];
+        for (int j = 0; j < 10; j++) acc[j] = S[L.crb + 10 * b + j];
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
+          int ch = m.body_child[k];
+          for (int j = 0; j < 10; j++) acc[j] += S[L.crb + 10 * ch + j];
+        }
+        for (int j = 0; j < 10; j++) S[L.crb + 10 * b + j] = acc[j];
+      }
+      sync();
+    }
+    for (int i = lane; i < nv * nv; i += kWave) S[L.M + i] = 0;
+    sync();
+    {
+      const float* arm = MF(dof_armature);
+      for (int i = lane; i < nv; i += kWave) {
+        float f[6];
+        inert_mul(f, S + L.crb + 10 * m.dof_bodyid[i], S + L.cdof + 6 * i);
+        for (int j = i; j >= 0; j = m.dof_parentid[j]) {
+          float v = dot6(S + L.cdof + 6 * j, f);
+          S[L.M + i * nv + j] = v;
+          S[L.M + j * nv + i] = v;
+        }
+        S[L.M + i * nv + i] += arm[i];
+      }
+    }
+    if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
+    sync();
+    // =========================================================== collision
+    {
+      ConOut co{S, ints, &L, d.nconmax};
+      const float* gsize = MF(geom_size);
+      const float* grb = MF(geom_rbound);
+      const float* gmargin = MF(geom_margin);
+      for (int p = lane; p < d.npair; p += kWave) {
+        int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+        int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        float margin = fmaxf(gmargin[g1], gmargin[g2]);
+        V3 p1 = v3(S + L.gxpos + 3 * g1), p2 = v3(S + L.gxpos + 3 * g2);
+        float r1 = grb[g1], r2 = grb[g2];
+        if (r1 > 0 && r2 > 0 && t1 != GEOM_HFIELD) {
+          if (norm(p2 - p1) > r1 + r2 + margin) continue;
+        }
+        const float* s1 = gsize + 3 * g1;
+        const float* s2 = gsize + 3 * g2;
+        int key = p * 8;
+        if (t1 == GEOM_PLANE) {
+          const float* Rp = S + L.gxmat + 9 * g1;
+          V3 n = {Rp[2], Rp[5], Rp[8]};
+          if (t2 == GEOM_SPHERE) {
+            plane_sphere(co, key, g1, g2, p1, n, p2, s2[0], margin);
+          } else if (t2 == GEOM_CAPSULE) {
+            const float* R2 = S + L.gxmat + 9 * g2;
+            V3 ax = {R2[2], R2[5], R2[8]};
+            int k = key;
+            k += plane_sphere(co, k, g1, g2, p1, n, p2 + ax * s2[1], s2[0], margin);
+            plane_sphere(co, k, g1, g2, p1, n, p2 - ax * s2[1], s2[0], margin);
+          } else if (t2 == GEOM_BOX) {
+            float dist = dot(p2 - p1, n);
+            const float* R2 = S + L.gxmat + 9 * g2;
+            int cnt = 0;
+            for (int i = 0; i < 8 && cnt < 4; i++) {
+              V3 v = {(i & 1) ? s2[0] : -s2[0], (i & 2) ? s2[1] : -s2[1], (i & 4) ? s2[2] : -s2[2]};
+              V3 corner = mulv(R2, v);
+              float ld = dot(n, corner);
+              if (dist + ld > margin || ld > 0) continue;
+              append(co, key + cnt, g1, g2, dist + ld, corner + p2 - n * (0.5f * (dist + ld)), n);
+              cnt++;
+            }
+          } else {
+            atomicOr(&ints[3], 4);
+          }
+        } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+          sphere_sphere(co, key, g1, g2, p1, s1[0], p2, s2[0], margin);
+        } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+          const float* R2 = S + L.gxmat + 9 * g2;
+          V3 ax = {R2[2], R2[5], R2[8]};
+          V3 pa, pb;
+          seg_seg(p1, p1, p2 + ax * s2[1], p2 - ax * s2[1], &pa, &pb);
+          sphere_sphere(co, key, g1, g2, p1, s1[0], pb, s2[0], margin);
+        } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+          const float* R1 = S + L.gxmat + 9 * g1;
+          const float* R2 = S + L.gxmat + 9 * g2;
+          V3 a1 = {R1[2], R1[5], R1[8]}, a2 = {R2[2], R2[5], R2[8]};
+          V3 pa, pb;
+          seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
+          sphere_sphere(co, key, g1, g2, pa, s1[0], pb, s2[0], margin);
+        } else {
+          atomicOr(&ints[3], 4);
+        }
+      }
+    }
+    sync();
+    // deterministic order: bitonic sort of (key, slot) over 64 lanes, then permute
+    int ncon = min(ints[0], d.nconmax);
+    {
+      int key = lane < ncon ? Si[L.con_key + lane] : 0x7fffffff;
+      int idx = lane;
+#pragma unroll
+      for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          int pk = __shfl_xor(key, j);
+          int pi = __shfl_xor(idx, j);
+          bool up = (lane & k) == 0;
+          bool lower = (lane & j) == 0;
+          bool sw = lower ? (up ? key > pk : key < pk) : (up ? key < pk : key > pk);
+          if (sw) { key = pk; idx = pi; }
+        }
+      }
+      // lane holds the source slot of sorted position `lane`
+      int g1 = 0, g2 = 0;
+      float dist = 0, px = 0, py = 0, pz = 0, nx = 0, ny = 0, nz = 0;
+      if (lane < ncon) {
+        g1 = Si[L.con_g1 + idx]; g2 = Si[L.con_g2 + idx]; dist = S[L.con_dist + idx];
+        px = S[L.con_pos + 3 * idx]; py = S[L.con_pos + 3 * idx + 1]; pz = S[L.con_pos + 3 * idx + 2];
+        nx = S[L.con_frame + 9 * idx]; ny = S[L.con_frame + 9 * idx + 1]; nz = S[L.con_frame + 9 * idx + 2];
+      }
+      sync();
+      if (lane < ncon) {
+        Si[L.con_g1 + lane] = g1; Si[L.con_g2 + lane] = g2; S[L.con_dist + lane] = dist;
+        S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
+        // contact frame (mju_makeFrame) from the normal
+        V3 n = {nx, ny, nz};
+        n = n * (1.0f / fmaxf(norm(n), MINVAL));
+        V3 t = fabsf(n.y) < 0.5f ? V3{0, 1, 0} : V3{0, 0, 1};
+        t = t - n * dot(n, t);
+        t = t * (1.0f / fmaxf(norm(t), MINVAL));
+        V3 b = cross(n, t);
+        float* fr = S + L.con_frame + 9 * lane;
+        st3(fr, n); st3(fr + 3, t); st3(fr + 6, b);
+        // contact parameters (mj_contactParam semantics)
+        const float* fri = MF(geom_friction);
+        const float* sref = MF(geom_solref);
+        const float* simp = MF(geom_solimp);
+        const float* smix = MF(geom_solmix);
+        const float* gmar = MF(geom_margin);
+        const float* ggap = MF(geom_gap);
+        int p1 = m.geom_priority[g1], p2 = m.geom_priority[g2];
+        int dim;
+        float f0, f1;
+        float* sr = S + L.con_solref + 2 * lane;
+        float* si = S + L.con_solimp + 5 * lane;
+        if (p1 != p2) {
+          int g = p1 > p2 ? g1 : g2;
+          dim = m.geom_condim[g];
+          f0 = fri[3 * g]; f1 = fri[3 * g + 1];
+          sr[0] = sref[2 * g]; sr[1] = sref[2 * g + 1];
+          for (int i = 0; i < 5; i++) si[i] = simp[5 * g + i];
+        } else {
+          dim = max(m.geom_condim[g1], m.geom_condim[g2]);
+          f0 = fmaxf(fri[3 * g1], fri[3 * g2]);
+          f1 = fmaxf(fri[3 * g1 + 1], fri[3 * g2 + 1]);
+          float s1 = smix[g1], s2 = smix[g2], mix;
+          if (s1 < MINVAL && s2 < MINVAL) mix = 0.5f;
+          else if (s1 < MINVAL) mix = 0.f;
+          else if (s2 < MINVAL) mix = 1.f;
+          else mix = s1 / (s1 + s2);
+          const float* r1 = sref + 2 * g1;
+          const float* r2 = sref + 2 * g2;
+          if (r1[0] > 0 && r2[0] > 0) {
+            sr[0] = mix * r1[0] + (1 - mix) * r2[0];
+            sr[1] = mix * r1[1] + (1 - mix) * r2[1];
+          } else {
+            sr[0] = fminf(r1[0], r2[0]);
+            sr[1] = fminf(r1[1], r2[1]);
+          }
+          for (int i = 0; i < 5; i++) si[i] = mix * simp[5 * g1 + i] + (1 - mix) * simp[5 * g2 + i];
+        }
+        (void)f1;
+        S[L.con_mu + 2 * lane] = fmaxf(MINMU, f0);
+        S[L.con_mu + 2 * lane + 1] = fmaxf(MINMU, f0);
+        Si[L.con_dim + lane] = dim;
+        S[L.con_imargin + lane] = fmaxf(gmar[g1], gmar[g2]) - fmaxf(ggap[g1], ggap[g2]);
+      }
+      sync();
+    }
+    // =========================================================== constraints
+    {
+      // row counts: limits (lane per joint) then contacts (lane per contact)
+      const float* jrange = MF(jnt_range);
+      const float* jmargin = MF(jnt_margin);
+      int nlim_rows = 0;
+      int lim_mask = 0;  // bit0 lower, bit1 upper
+      if (lane < d.njnt && m.jnt_limited[lane] &&
+          (m.jnt_type[lane] == JNT_HINGE || m.jnt_type[lane] == JNT_SLIDE)) {
+        float q = S[L.qpos + m.jnt_qposadr[lane]];
+        float mg = jmargin[lane];
+        if (q - jrange[2 * lane] < mg) lim_mask |= 1;
+        if (jrange[2 * lane + 1] - q < mg) lim_mask |= 2;
+        nlim_rows = (lim_mask & 1) + ((lim_mask >> 1) & 1);
+      }
+      int lim_total, lim_off = wave_excl_scan(nlim_rows, lane, &lim_total);
+      int cdim = lane < ncon ? Si[L.con_dim + lane] : 0;
+      int crow = lane < ncon ? (cdim == 1 ? 1 : 2 * (cdim - 1)) : 0;
+      if (lane < ncon && cdim != 1 && cdim != 3) atomicOr(&ints[3], 4);
+      int con_total, con_off = wave_excl_scan(crow, lane, &con_total);
+      int nefc = lim_total + con_total;
+      if (nefc > d.njmax) {
+        if (lane == 0) atomicOr(&ints[3], 2);
+      }
+      // contacts whose rows do not fit are dropped as whole contacts
+      int keep_con = ncon;
+      {
+        bool fits = lane < ncon && lim_total + con_off + crow <= d.njmax;
+        unsigned long long bal = __ballot(lane < ncon && !fits);
+        if (bal) keep_con = __ffsll((long long)bal) - 1;
+        keep_con = min(keep_con, ncon);
+      }
+      ncon = keep_con;
+      nefc = lim_total + (ncon > 0 ? __shfl(con_off + crow, ncon - 1) : 0);
+      if (lim_total > d.njmax) { nefc = 0; ncon = 0; }
+      const float* dinvw = MF(dof_invweight0);
+      const float* binvw = MF(body_invweight0);
+      const float* jsolref = MF(jnt_solref);
+      const float* jsolimp = MF(jnt_solimp);
+      // limit rows metadata (J set below) -- lane per joint
+      if (lim_mask && nefc > 0) {
+        int r = lim_off;
+        float q = S[L.qpos + m.jnt_qposadr[lane]];
+        for (int side = -1; side <= 1; side += 2) {
+          if (!((side < 0 ? lim_mask & 1 : lim_mask & 2))) continue;
+          float dist = side * (jrange[2 * lane + (side + 1) / 2] - q);
+          Si[L.efc_type + r] = EFC_LIMIT;
+          Si[L.efc_cid + r] = -1 - lane;  // negative: limit of joint lane
+          S[L.efc_aref + r] = dist;       // temporarily: pos
+          S[L.efc_D + r] = (float)(-side);  // temporarily: jacobian sign
+          r++;
+        }
+      }
+      if (lane < ncon) {
+        int r0 = lim_total + con_off;
+        Si[L.con_efc + lane] = r0;
+        for (int k = 0; k < crow; k++) {
+          Si[L.efc_type + r0 + k] = cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL;
+          Si[L.efc_cid + r0 + k] = lane;
+        }
+      }
+      sync();
+      // Jacobian rows: lane per dof
+      for (int i = lane; i < nv; i += kWave) {
+        // limits
+        for (int r = 0; r < lim_total && r < nefc; r++) {
+          int j = -1 - Si[L.efc_cid + r];
+          S[L.efc_J + r * nv + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
+        }
+        uint64_t bm = m.dof_bodymask[i];
+        const float* cd = S + L.cdof + 6 * i;
+        V3 cang = v3(cd), clin = v3(cd + 3);
+        for (int c = 0; c < ncon; c++) {
+          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
+          V3 pos = v3(S + L.con_pos + 3 * c);
+          V3 jd = {0, 0, 0};
+          if (b2 > 0 && ((bm >> b2) & 1ull))
+            jd = jd + clin + cross(cang, pos - v3(S + L.subtree_com + 3 * m.body_rootid[b2]));
+          if (b1 > 0 && ((bm >> b1) & 1ull))
+            jd = jd - (clin + cross(cang, pos - v3(S + L.subtree_com + 3 * m.body_rootid[b1])));
+          const float* fr = S + L.con_frame + 9 * c;
+          float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
+          int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) {
+            S[L.efc_J + r0 * nv + i] = jn;
+          } else {
+            float jt1 = fr[3] * jd.x + fr[4] * jd.y + fr[5] * jd.z;
+            float jt2 = fr[6] * jd.x + fr[7] * jd.y + fr[8] * jd.z;
+            float mu0 = S[L.con_mu + 2 * c], mu1 = S[L.con_mu + 2 * c + 1];
+            S[L.efc_J + (r0 + 0) * nv + i] = jn + mu0 * jt1;
+            S[L.efc_J + (r0 + 1) * nv + i] = jn - mu0 * jt1;
+            S[L.efc_J + (r0 + 2) * nv + i] = jn + mu1 * jt2;
+            S[L.efc_J + (r0 + 3) * nv + i] = jn - mu1 * jt2;
+          }
+        }
+      }
+      sync();
+      // row parameters: lane per row
+      for (int r = lane; r < nefc; r += kWave) {
+        int type = Si[L.efc_type + r];
+        float pos, margin, diag;
+        const float *sref, *simp;
+        if (type == EFC_LIMIT) {
+          int j = -1 - Si[L.efc_cid + r];
+          pos = S[L.efc_aref + r];
+          margin = jmargin[j];
+          diag = dinvw[m.jnt_dofadr[j]];
+          sref = jsolref + 2 * j;
+          simp = jsolimp + 5 * j;
+        } else {
+          int c = Si[L.efc_cid + r];
+          pos = S[L.con_dist + c];
+          margin = S[L.con_imargin + c];
+          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
+          float tran = binvw[2 * b1] + binvw[2 * b2];
+          if (type == EFC_FRICTIONLESS) {
+            diag = tran;
+          } else {
+            float mu = S[L.con_mu + 2 * c + ((r - Si[L.con_efc + c]) >> 1)];
+            diag = (tran + mu * mu * tran) / o.impratio;
+          }
+          sref = S + L.con_solref + 2 * c;
+          simp = S + L.con_solimp + 5 * c;
+        }
+        float imp = impedance(simp, pos, margin);
+        float Rr = fmaxf(MINVAL, (1 - imp) * diag / imp);
+        float dmax = fminf(MAXIMP, fmaxf(MINIMP, simp[1]));
+        float K, B;
+        if (sref[0] > 0) {
+          float tc = fmaxf(sref[0], 2 * h), dr = sref[1];
+          K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+          B = 2.0f / (dmax * tc);
+        } else {
+          K = -sref[0] / (dmax * dmax);
+          B = -sref[1] / dmax;
+        }
+        float vel = 0;
+        const float* J = S + L.efc_J + r * nv;
+        for (int i = 0; i < nv; i++) vel += J[i] * S[L.qvel + i];
+        S[L.efc_D + r] = 1.0f / Rr;
+        S[L.efc_aref + r] = -B * vel - K * imp * (pos - margin);
+      }
+      if (lane == 0) { ints[1] = nefc; ints[2] = lim_total; ints[4] = ncon; }
+      sync();
+    }
+    const int nefc = ints[1];
+    ncon = ints[4];
+    // =========================================================== velocity stage
+    if (lane < 6) S[L.cvel + lane] = 0;
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float v[6];
+        for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
+        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
+        for (int k = j0; k < j1; k++) {
+          int dof = m.jnt_dofadr[k];
+          if (m.jnt_type[k] == JNT_FREE) {
+            for (int a = 0; a < 3; a++) {
+              for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+            }
+            for (int a = 3; a < 6; a++) cross_motion(S + L.cdofdot + 6 * (dof + a), v, S + L.cdof + 6 * (dof + a));
+            for (int a = 3; a < 6; a++)
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+          } else {
+            cross_motion(S + L.cdofdot + 6 * dof, v, S + L.cdof + 6 * dof);
+            for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * dof + j] * S[L.qvel + dof];
+          }
+        }
+        for (int j = 0; j < 6; j++) S[L.cvel + 6 * b + j] = v[j];
+      }
+      sync();
+    }
+    // RNE (flg_acc = 0): cacc with gravity, body forces into crb scratch (reused as cfrc)
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+        float f1[6], iv[6], f2[6];
+        inert_mul(f1, S + L.cinert + 10 * b, a);
+        inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
+        cross_force(f2, S + L.cvel + 6 * b, iv);
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = f1[j] + f2[j];
+      }
+      sync();
+    }
+    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        float acc[6];
+        for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
+          int ch = m.body_child[k];
+          for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
+        }
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
+      }
+      sync();
+    }
+    {
+      const float* damping = MF(dof_damping);
+      const float* jstiff = MF(jnt_stiffness);
+      const float* qspring = MF(qpos_spring);
+      for (int i = lane; i < nv; i += kWave) {
+        S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * m.dof_bodyid[i]);
+        float pf = -damping[i] * S[L.qvel + i];
+        int j = m.dof_jntid[i];
+        int t = m.jnt_type[j];
+        if ((t == JNT_HINGE || t == JNT_SLIDE) && jstiff[j] != 0.f) {
+          int a = m.jnt_qposadr[j];
+          pf -= jstiff[j] * (S[L.qpos + a] - qspring[a]);
+        }
+        S[L.qfrc_passive + i] = pf;
+        S[L.qfrc_act + i] = 0.f;
+      }
+    }
+    sync();
+    // actuation: position / motor actuators on joints
+    {
+      const float* gear = MF(actuator_gear);
+      const float* gain = MF(actuator_gainprm);
+      const float* bias = MF(actuator_biasprm);
+      const float* frange = MF(actuator_forcerange);
+      const float* crange = MF(actuator_ctrlrange);
+      for (int u = lane; u < nu; u += kWave) {
+        int j = m.actuator_trnid[u];
+        int dof = m.jnt_dofadr[j], a = m.jnt_qposadr[j];
+        float g = gear[u];
+        float len = g * S[L.qpos + a], vel = g * S[L.qvel + dof];
+        float c = S[L.ctrl + u];
+        if (m.actuator_ctrllimited[u]) c = fminf(fmaxf(c, crange[2 * u]), crange[2 * u + 1]);
+        float f = gain[3 * u] * c + bias[3 * u] + bias[3 * u + 1] * len + bias[3 * u + 2] * vel;
+        if (m.actuator_forcelimited[u]) f = fminf(fmaxf(f, frange[2 * u]), frange[2 * u + 1]);
+        S[L.act_force + u] = f;
+        S[L.act_len + u] = len;
+        S[L.act_vel + u] = vel;
+        atomicAdd(S + L.qfrc_act + dof, g * f);
+      }
+    }
+    sync();
+    for (int i = lane; i < nv; i += kWave) {
+      float f = S[L.qfrc_passive + i] - S[L.qfrc_bias + i] + S[L.qfrc_applied + i] + S[L.qfrc_act + i];
+      if (any_xfrc) {
+        uint64_t bm = m.dof_bodymask[i];
+        const float* cd = S + L.cdof + 6 * i;
+        V3 cang = v3(cd), clin = v3(cd + 3);
+        for (int b = 1; b < nb; b++) {
+          if (!((bm >> b) & 1ull)) continue;
+          const float* xf = S + L.xfrc + 6 * b;
+          V3 jp = clin + cross(cang, v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+          f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
+        }
+      }
+      S[L.qfrc_smooth + i] = f;
+      S[L.qacc_smooth + i] = f;
+    }
+    // subtree momenta (for subtreeangmom sensors)
+    for (int b = lane; b < nb; b += kWave) {
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      st3(S + L.stlin + 3 * b, vc * body_mass[b]);
+      const float* Ri = S + L.ximat + 9 * b;
+      V3 wl = mulTv(Ri, v3(cv));
+      V3 hl = {body_inertia[3 * b] * wl.x, body_inertia[3 * b + 1] * wl.y, body_inertia[3 * b + 2] * wl.z};
+      st3(S + L.stang + 3 * b, mulv(Ri, hl));
+      // stash body com velocity in cacc? no: recompute when needed
+    }
+    sync();
+    // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
+    for (int i = lane; i < nv * nv; i += kWave) S[L.H + i] = S[L.M + i];
+    sync();
+    chol_lds(S + L.H, nv, lane);
+    chol_solve_lds(S + L.H, nv, S + L.qacc_smooth, lane);
+    // linear momentum of subtrees -> velocity of subtree com
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        V3 acc = v3(S + L.stlin + 3 * b);
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++)
+          acc = acc + v3(S + L.stlin + 3 * m.body_child[k]);
+        st3(S + L.stlin + 3 * b, acc);
+      }
+      sync();
+    }
+    for (int b = lane; b < nb; b += kWave) {
+      float sm = S[L.stmass + b];
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
+      st3(S + L.stlin + 3 * b, lin);
+    }
+    sync();
+    for (int b = lane; b < nb; b += kWave) {
+      if (b == 0) continue;
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
+      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * body_mass[b];
+      st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
+    }
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int p = m.level_body[i];
+        V3 acc = v3(S + L.stang + 3 * p);
+        for (int k = m.body_childadr[p]; k < m.body_childadr[p + 1]; k++) {
+          int b = m.body_child[k];
+          V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
+          V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
+          acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
+        }
+        st3(S + L.stang + 3 * p, acc);
+      }
+      sync();
+    }
+    // =========================================================== Newton solver
+    int niter = 0;
+    if (nefc == 0) {
+      for (int i = lane; i < nv; i += kWave) {
+        S[L.x + i] = S[L.qacc_smooth + i];
+        S[L.qfrc_con + i] = 0.f;
+      }
+      sync();
+    } else {
+      const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
+      // cost(x) helper over rows; Mx must be valid.  Returns total cost (wave-uniform).
+      auto eval_cost = [&](const float* xv, const float* Mxv) -> float {
+        float g = 0.f;
+        for (int i = lane; i < nv; i += kWave)
+          g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
+        float c = 0.f;
+        for (int r = lane; r < nefc; r += kWave) {
+          const float* J = S + L.efc_J + r * nv;
+          float v = -S[L.efc_aref + r];
+          for (int i = 0; i < nv; i++) v += J[i] * xv[i];
+          S[L.efc_jar + r] = v;
+          if (v < 0) c += 0.5f * S[L.efc_D + r] * v * v;
+        }
+        return wave_sum(g + c);
+      };
+      auto mulM = [&](float* out, const float* xv) {
+        for (int i = lane; i < nv; i += kWave) {
+          float s = 0.f;
+          const float* Mr = S + L.M + i * nv;
+          for (int j = 0; j < nv; j++) s += Mr[j] * xv[j];
+          out[i] = s;
+        }
+      };
+      // warmstart choice
+      for (int i = lane; i < nv; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
+      sync();
+      mulM(S + L.Mx, S + L.x);
+      sync();
+      float cost_ws = eval_cost(S + L.x, S + L.Mx);
+      sync();
+      float cost_sm = eval_cost(S + L.qacc_smooth, S + L.qfrc_smooth);
+      sync();
+      if (cost_sm < cost_ws) {
+        for (int i = lane; i < nv; i += kWave) {
+          S[L.x + i] = S[L.qacc_smooth + i];
+          S[L.Mx + i] = S[L.qfrc_smooth + i];
+        }
+      }
+      sync();
+      float cost = eval_cost(S + L.x, S + L.Mx);
+      sync();
+      for (int iter = 0; iter < o.iterations; iter++) {
+        // gradient
+        for (int i = lane; i < nv; i += kWave) {
+          float g = S[L.Mx + i] - S[L.qfrc_smooth + i];
+          for (int r = 0; r < nefc; r++) {
+            float jar = S[L.efc_jar + r];
+            if (jar < 0) g += S[L.efc_J + r * nv + i] * S[L.efc_D + r] * jar;
+          }
+          S[L.grad + i] = g;
+        }
+        // Hessian H = M + J^T D J over active rows (lower triangle by element)
+        {
+          int cnt = nv * (nv + 1) / 2;
+          for (int e = lane; e < cnt; e += kWave) {
+            int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
+            while ((i + 1) * (i + 2) / 2 <= e) i++;
+            while (i * (i + 1) / 2 > e) i--;
+            int j = e - i * (i + 1) / 2;
+            float hsum = S[L.M + i * nv + j];
+            for (int r = 0; r < nefc; r++) {
+              float jar = S[L.efc_jar + r];
+              if (jar < 0) hsum += S[L.efc_J + r * nv + i] * S[L.efc_D + r] * S[L.efc_J + r * nv + j];
+            }
+            S[L.H + i * nv + j] = hsum;
+          }
+        }
+        sync();
+        float gn = 0.f;
+        for (int i = lane; i < nv; i += kWave) gn += S[L.grad + i] * S[L.grad + i];
+        gn = sqrtf(wave_sum(gn));
+        if (iter > 0 && scale * gn < o.tolerance) break;
+        chol_lds(S + L.H, nv, lane);
+        for (int i = lane; i < nv; i += kWave) S[L.srch + i] = -S[L.grad + i];
+        sync();
+        chol_solve_lds(S + L.H, nv, S + L.srch, lane);
+        mulM(S + L.Ms, S + L.srch);
+        float g1 = 0.f, g2 = 0.f, sn = 0.f;
+        for (int i = lane; i < nv; i += kWave) {
+          float s = S[L.srch + i];
+          g1 += s * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
+          sn += s * s;
+        }
+        for (int r = lane; r < nefc; r += kWave) {
+          const float* J = S + L.efc_J + r * nv;
+          float js = 0.f;
+          for (int i = 0; i < nv; i++) js += J[i] * S[L.srch + i];
+          S[L.efc_Js + r] = js;
+        }
+        sync();
+        for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
+        g1 = wave_sum(g1);
+        g2 = wave_sum(g2);
+        sn = sqrtf(wave_sum(sn));
+        const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
+        // line search (same algorithm as the oracle): derivative at alpha
+        auto ls_eval = [&](float alpha, float* der, float* der2) {
+          float f1 = 0.f, f2 = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float js = S[L.efc_Js + r];
+            float v = S[L.efc_jar + r] + alpha * js;
+            if (v < 0) {
+              float Dr = S[L.efc_D + r];
+              f1 += Dr * v * js;
+              f2 += Dr * js * js;
+            }
+          }
+          *der = g1 + alpha * g2 + wave_sum(f1);
+          *der2 = g2 + wave_sum(f2);
+        };
+        float d0, dd0;
+        ls_eval(0.f, &d0, &dd0);
+        float alpha = 0.f;
+        if (d0 < 0) {
+          float c0 = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float jar = S[L.efc_jar + r], js = S[L.efc_Js + r];
+            if (jar < 0 || (jar == 0 && js < 0)) c0 += S[L.efc_D + r] * js * js;
+          }
+          c0 = g2 + wave_sum(c0);
+          float lo = 0.f, hi = -1.f, best = 0.f;
+          float a = -d0 / c0;
+          bool done = false;
+          for (int it = 0; it < o.ls_iterations; it++) {
+            float der, der2;
+            ls_eval(a, &der, &der2);
+            if (fabsf(der) <= gtol) { alpha = a; done = true; break; }
+            if (der < 0) { lo = a; best = a; } else { hi = a; }
+            float next = der2 > 0 ? a - der / der2 : a * 2;
+            if (hi >= 0 && !(next > lo && next < hi)) next = 0.5f * (lo + hi);
+            if (hi < 0 && next <= lo) next = lo + (lo > 0 ? lo : 1.0f);
+            a = next;
+          }
+          if (!done) alpha = best > 0 ? best : a;
+        }
+        niter = iter + 1;
+        if (alpha == 0.f) break;
+        for (int i = lane; i < nv; i += kWave) {
+          S[L.x + i] += alpha * S[L.srch + i];
+          S[L.Mx + i] += alpha * S[L.Ms + i];
+        }
+        sync();
+        float old = cost;
+        cost = eval_cost(S + L.x, S + L.Mx);
+        sync();
+        if (scale * (old - cost) < o.tolerance) break;
+      }
+      // constraint forces and qfrc_constraint = J^T f
+      for (int r = lane; r < nefc; r += kWave) {
+        float jar = S[L.efc_jar + r];
+        S[L.efc_force + r] = jar < 0 ? -S[L.efc_D + r] * jar : 0.f;
+      }
+      sync();
+      for (int i = lane; i < nv; i += kWave) {
+        float f = 0.f;
+        for (int r = 0; r < nefc; r++) f += S[L.efc_J + r * nv + i] * S[L.efc_force + r];
+        S[L.qfrc_con + i] = f;
+      }
+      sync();
+    }
+    niter_last = niter;
+    // =========================================================== post-constraint acc
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++)
+            a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+      }
+      sync();
+    }
+    // =========================================================== sensors
+    for (int s = lane; s < d.nsensor; s += kWave) {
+      float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
+      int obj = m.sensor_objid[s];
+      int type = m.sensor_type[s];
+      if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
+        int b = m.site_bodyid[obj];
+        const float* R = S + L.sxmat + 9 * obj;
+        const float* cv = S + L.cvel + 6 * b;
+        V3 rel = v3(S + L.sxpos + 3 * obj) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+        V3 r;
+        if (type == SENS_GYRO) {
+          r = mulTv(R, v3(cv));
+        } else {
+          V3 v = v3(cv + 3) + cross(v3(cv), rel);
+          if (type == SENS_VELOCIMETER) {
+            r = mulTv(R, v);
+          } else {
+            const float* ca = S + L.cacc + 6 * b;
+            V3 a = v3(ca + 3) + cross(v3(ca), rel) + cross(v3(cv), v);
+            r = mulTv(R, a);
+          }
+        }
+        out[0] = r.x; out[1] = r.y; out[2] = r.z;
+      } else if (type == SENS_SUBTREEANGMOM) {
+        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+      } else if (type == SENS_FRAMEPOS) {
+        const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
+        out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+      } else if (type == SENS_JOINTPOS) {
+        out[0] = S[L.qpos + m.jnt_qposadr[obj]];
+      } else if (type == SENS_JOINTVEL) {
+        out[0] = S[L.qvel + m.jnt_dofadr[obj]];
+      } else if (type == SENS_CONTACT) {
+        const int32_t* ip = m.sensor_intprm + 3 * s;
+        int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
+        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
+        int dim = m.sensor_dim[s];
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        int found = 0;
+        V3 net = {0, 0, 0};
+        int sel[8];
+        float key[8];
+        int nsel = 0;
+        for (int c = 0; c < ncon; c++) {
+          int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+          bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+          bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+          if (!a1 && !a2) continue;
+          found++;
+          // contact force in contact frame
+          int r0 = Si[L.con_efc + c];
+          V3 f = {0, 0, 0};
+          if (Si[L.con_dim + c] == 1) {
+            f.x = S[L.efc_force + r0];
+          } else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          net = net + fg * (a1 ? 1.f : -1.f);
+          float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
+                  : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
+          if (nsel < nslot || k < key[nsel - 1]) {
+            int pos = nsel < nslot ? nsel++ : nslot - 1;
+            while (pos > 0 && key[pos - 1] > k) { key[pos] = key[pos - 1]; sel[pos] = sel[pos - 1]; pos--; }
+            key[pos] = k;
+            sel[pos] = c * 2 + (a1 ? 0 : 1);
+          }
+        }
+        if (reduce == REDUCE_NETFORCE) {
+          if (bits & 1) out[0] = (float)found;
+          else if (bits & 2) { out[0] = net.x; out[1] = net.y; out[2] = net.z; }
+        } else {
+          for (int k = 0; k < nsel; k++) {
+            int c = sel[k] >> 1;
+            float sg = (sel[k] & 1) ? -1.f : 1.f;
+            float* oo = out + k * fdim;
+            if (bits & 1) oo[0] = (float)found;
+            else if (bits & 8) oo[0] = S[L.con_dist + c];
+            else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 2) {
+              int r0 = Si[L.con_efc + c];
+              if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
+              else {
+                float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+                float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+                oo[0] = e0 + e1 + e2 + e3;
+                oo[1] = (e0 - e1) * S[L.con_mu + 2 * c];
+                oo[2] = (e2 - e3) * S[L.con_mu + 2 * c + 1];
+              }
+            }
+          }
+        }
+      }
+    }
+    // =========================================================== write kinematics outputs
+    const bool last = (sub == nsubstep - 1);
+    if (last) {
+      size_t wb = (size_t)w * nb;
+      for (int i = lane; i < 3 * nb; i += kWave) {
+        D.xpos[wb * 3 + i] = S[L.xpos + i];
+        D.xipos[wb * 3 + i] = S[L.xipos + i];
+        D.subtree_com[wb * 3 + i] = S[L.subtree_com + i];
+        D.subtree_linvel[wb * 3 + i] = S[L.stlin + i];
+        D.subtree_angmom[wb * 3 + i] = S[L.stang + i];
+      }
+      for (int i = lane; i < 4 * nb; i += kWave) D.xquat[wb * 4 + i] = S[L.xquat + i];
+      for (int i = lane; i < 9 * nb; i += kWave) {
+        D.xmat[wb * 9 + i] = S[L.xmat + i];
+        D.ximat[wb * 9 + i] = S[L.ximat + i];
+      }
+      for (int i = lane; i < 6 * nb; i += kWave) {
+        D.cvel[wb * 6 + i] = S[L.cvel + i];
+        D.cacc[wb * 6 + i] = S[L.cacc + i];
+      }
+      size_t wg = (size_t)w * d.ngeom;
+      for (int i = lane; i < 3 * d.ngeom; i += kWave) D.geom_xpos[wg * 3 + i] = S[L.gxpos + i];
+      for (int i = lane; i < 9 * d.ngeom; i += kWave) D.geom_xmat[wg * 9 + i] = S[L.gxmat + i];
+      size_t ws = (size_t)w * d.nsite;
+      for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
+      for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];
+      for (int i = lane; i < nv; i += kWave) {
+        size_t k = (size_t)w * nv + i;
+        D.qacc[k] = S[L.x + i];
+        D.qacc_smooth[k] = S[L.qacc_smooth + i];
+        D.qfrc_bias[k] = S[L.qfrc_bias + i];
+        D.qfrc_passive[k] = S[L.qfrc_passive + i];
+        D.qfrc_actuator[k] = S[L.qfrc_act + i];
+        D.qfrc_constraint[k] = S[L.qfrc_con + i];
+        D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
+      }
+      for (int u = lane; u < nu; u += kWave) {
+        size_t k = (size_t)w * nu + u;
+        D.actuator_force[k] = S[L.act_force + u];
+        D.actuator_length[k] = S[L.act_len + u];
+        D.actuator_velocity[k] = S[L.act_vel + u];
+      }
+      size_t wc = (size_t)w * d.nconmax;
+      for (int c = lane; c < d.nconmax; c += kWave) {
+        bool v = c < ncon;
+        D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
+        D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
+        D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
+        for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
+        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? S[L.con_frame + 9 * c + t] : 0.f;
+        V3 f = {0, 0, 0};
+        if (v && nefc > 0) {
+          int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) f.x = S[L.efc_force + r0];
+          else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+        }
+        D.contact_force[(wc + c) * 3] = f.x;
+        D.contact_force[(wc + c) * 3 + 1] = f.y;
+        D.contact_force[(wc + c) * 3 + 2] = f.z;
+      }
+      if (lane == 0) {
+        D.ncon[w] = ncon;
+        D.nefc[w] = nefc;
+        D.solver_niter[w] = niter_last;
+        atomicMax(&D.stats[0], ints[0]);
+        atomicMax(&D.stats[1], nefc);
+        if (ints[3] & 1) atomicAdd(&D.stats[2], 1);
+        if (ints[3] & 2) atomicAdd(&D.stats[3], 1);
+        if (ints[3] & 4) atomicAdd(&D.stats[4], 1);
+        atomicMax(&D.stats[5], niter_last);
+      }
+    }
+    if (!integrate) break;
+    // =========================================================== implicitfast / Euler
+    sync();
+    {
+      for (int i = lane; i < nv * nv; i += kWave) S[L.H + i] = S[L.M + i];
+      sync();
+      const float* damping = MF(dof_damping);
+      for (int i = lane; i < nv; i += kWave) S[L.H + i * nv + i] += h * damping[i];
+      if (o.integrator == 1) {
+        const float* gear = MF(actuator_gear);
+        const float* bias = MF(actuator_biasprm);
+        const float* frange = MF(actuator_forcerange);
+        sync();
+        for (int u = lane; u < nu; u += kWave) {
+          if (m.actuator_forcelimited[u]) {
+            float fo = S[L.act_force + u];
+            if (fo <= frange[2 * u] || fo >= frange[2 * u + 1]) continue;
+          }
+          float bv = bias[3 * u + 2];
+          if (bv == 0.f) continue;
+          int dof = m.jnt_dofadr[m.actuator_trnid[u]];
+          float g = gear[u];
+          atomicAdd(S + L.H + dof * nv + dof, -h * g * g * bv);
+        }
+      }
+      for (int i = lane; i < nv; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
+      sync();
+      chol_lds(S + L.H, nv, lane);
+      chol_solve_lds(S + L.H, nv, S + L.vtmp, lane);
+      for (int i = lane; i < nv; i += kWave) S[L.qvel + i] += h * S[L.vtmp + i];
+      sync();
+      for (int k = lane; k < d.njnt; k += kWave) {
+        int a = m.jnt_qposadr[k], dof = m.jnt_dofadr[k];
+        int t = m.jnt_type[k];
+        if (t == JNT_FREE) {
+          for (int i = 0; i < 3; i++) S[L.qpos + a + i] += h * S[L.qvel + dof + i];
+          V3 wv = v3(S + L.qvel + dof + 3);
+          float nw = norm(wv);
+          V3 ax = nw < MINVAL ? V3{1, 0, 0} : wv * (1.0f / nw);
+          Q4 q = qnorm(q4(S + L.qpos + a + 3));
+          q = qmul(q, qaxisangle(ax, h * nw));
+          st4(S + L.qpos + a + 3, q);
+        } else if (t == JNT_HINGE || t == JNT_SLIDE) {
+          S[L.qpos + a] += h * S[L.qvel + dof];
+        }
+      }
+      for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = S[L.x + i];
+      time += h;
+      sync();
+    }
+  }
+  // ------------------------------------------------------------- store state
+  if (integrate) {
+    for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];
+    for (int i = lane; i < nv; i += kWave) {
+      D.qvel[(size_t)w * nv + i] = S[L.qvel + i];
+      D.qacc_warmstart[(size_t)w * nv + i] = S[L.qacc_ws + i];
+    }
+    if (lane == 0) D.time[w] = time;
+  }
+}
+
+// --------------------------------------------------------------------------- reset
+__global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int nworld) {
+  const int w = blockIdx.x;
+  if (w >= nworld) return;
+  if (mask && !mask[w]) return;
+  const int lane = threadIdx.x;
+  const float* qpos0 = m.qpos0 + (size_t)w * m.qpos0_ws;
+  for (int i = lane; i < d.nq; i += blockDim.x) D.qpos[(size_t)w * d.nq + i] = qpos0[i];
+  for (int i = lane; i < d.nv; i += blockDim.x) {
+    size_t k = (size_t)w * d.nv + i;
+    D.qvel[k] = 0; D.qacc_warmstart[k] = 0; D.qacc[k] = 0; D.qfrc_applied[k] = 0;
+    D.qacc_smooth[k] = 0; D.qfrc_constraint[k] = 0;
+  }
+  for (int i = lane; i < d.nu; i += blockDim.x) {
+    D.ctrl[(size_t)w * d.nu + i] = 0; D.actuator_force[(size_t)w * d.nu + i] = 0;
+  }
+  for (int i = lane; i < 6 * d.nbody; i += blockDim.x) D.xfrc_applied[(size_t)w * 6 * d.nbody + i] = 0;
+  for (int i = lane; i < d.nsensordata; i += blockDim.x) D.sensordata[(size_t)w * d.nsensordata + i] = 0;
+  for (int b = lane; b < d.nbody; b += blockDim.x) {
+    int mid = m.body_mocapid[b];
+    if (mid < 0) continue;
+    const float* bp = m.body_pos + (size_t)w * m.body_pos_ws + 3 * b;
+    const float* bq = m.body_quat + (size_t)w * m.body_quat_ws + 4 * b;
+    for (int t = 0; t < 3; t++) D.mocap_pos[((size_t)w * d.nmocap + mid) * 3 + t] = bp[t];
+    for (int t = 0; t < 4; t++) D.mocap_quat[((size_t)w * d.nmocap + mid) * 4 + t] = bq[t];
+  }
+  if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
+}
+
+hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
+                       int integrate, hipStream_t stream) {
+  if (nworld <= 0) return hipSuccess;
+  size_t shmem = (size_t)host.L.total * 4;
+  if (shmem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)step_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(step_kernel, dim3(nworld), dim3(kWave), shmem, stream, dev, nworld,
+                     nsubstep, integrate);
+  return hipGetLastError();
+}
+
+hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
+                        int nworld, hipStream_t stream) {
+  if (nworld <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reset_kernel, dim3(nworld), dim3(kWave), 0, stream, d, m, dd, mask, nworld);
+  return hipGetLastError();
+}
+
+}  // namespace mjx

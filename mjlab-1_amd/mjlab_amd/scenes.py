@@ -1,0 +1,113 @@
+"""Compiled task scenes for the hot path: velocity G1 / Go1, tracking G1, jump G1.
+
+Each builder reproduces the reference scene assembly for one task id
+(`src/mjlab/tasks/velocity/config/g1/env_cfgs.py:20-56`,
+`src/mjlab/tasks/velocity/config/go1/env_cfgs.py:15-49`,
+`src/mjlab/tasks/tracking/config/g1/env_cfgs.py`, `src/mjlab/tasks/jump/config/g1/env_cfgs.py`)
+from the robot MJCF.  Because the reference's MJCF files do not travel to the GPU
+box, `scripts/build_assets.py` compiles each scene here and stores the numeric
+model as `mjlab_amd/assets/<scene>.npz`; `load_scene()` reads that file.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import re
+
+import numpy as np
+
+from . import asset_zoo as az
+from .compiler.mjcf import parse_mjcf
+from .compiler.model import ContactSensorSpec, EntitySpec, Model, compile_scene
+
+ASSET_DIR = os.path.join(os.path.dirname(__file__), "assets")
+
+# Simulation options of the velocity task (`tasks/velocity/velocity_env_cfg.py:343-351`).
+VELOCITY_SIM = dict(timestep=0.005, iterations=10, ls_iterations=20)
+# Jump task: dt 0.002 (`tasks/jump/jump_env_cfg.py:324-352`).
+JUMP_SIM = dict(timestep=0.002, iterations=10, ls_iterations=20)
+
+
+def _g1_entity(xml_path, init=az.G1_KNEES_BENT):
+  return EntitySpec("robot", parse_mjcf(xml_path), collisions=(az.G1_FULL_COLLISION,),
+                    actuators=az.g1_actuators(), init_pos=init["pos"],
+                    init_joint_pos=init["joint_pos"])
+
+
+def _g1_contact_sensors(self_collision=True):
+  out = [ContactSensorSpec(
+    name="feet_ground_contact", primary_mode="subtree",
+    primary_names=["robot/left_ankle_roll_link", "robot/right_ankle_roll_link"],
+    secondary_mode="body", secondary_name="terrain", fields=("found", "force"),
+    reduce="netforce", num_slots=1)]
+  if self_collision:
+    out.append(ContactSensorSpec(
+      name="self_collision", primary_mode="subtree", primary_names=["robot/pelvis"],
+      secondary_mode="subtree", secondary_name="robot/pelvis", fields=("found",),
+      reduce="none", num_slots=1))
+  return out
+
+
+def build_g1_velocity(xml_path: str) -> Model:
+  return compile_scene([_g1_entity(xml_path)], contact_sensors=_g1_contact_sensors(),
+                       **VELOCITY_SIM)
+
+
+def build_go1_velocity(xml_path: str) -> Model:
+  ent = EntitySpec("robot", parse_mjcf(xml_path), collisions=(az.GO1_FULL_COLLISION,),
+                   actuators=az.go1_actuators(), init_pos=az.GO1_INIT["pos"],
+                   init_joint_pos=az.GO1_INIT["joint_pos"])
+  feet = [f"robot/{n}_foot_collision" for n in ("FR", "FL", "RR", "RL")]
+  tmp = compile_scene([ent], **VELOCITY_SIM)
+  nonfoot = [n for n in tmp.names["geom"]
+             if n.startswith("robot/") and re.fullmatch(r".*_collision\d*$", n[6:])
+             and n not in feet]
+  sensors = [
+    ContactSensorSpec("feet_ground_contact", "geom", feet, "body", "terrain",
+                      ("found", "force"), "netforce", 1),
+    ContactSensorSpec("nonfoot_ground_touch", "geom", nonfoot, "body", "terrain",
+                      ("found",), "none", 1),
+  ]
+  return compile_scene([ent], contact_sensors=sensors, **VELOCITY_SIM)
+
+
+SCENE_BUILDERS = {
+  "g1_velocity": ("unitree_g1/xmls/g1.xml", build_g1_velocity),
+  "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
+}
+
+
+# ----------------------------------------------------------------------------- npz io
+_SCALARS = ("nq", "nv", "nu", "nbody", "njnt", "ngeom", "nsite", "nsensor", "nsensordata",
+            "npair", "nhfield", "nhfielddata", "timestep", "iterations", "ls_iterations",
+            "tolerance", "ls_tolerance", "impratio", "integrator", "cone", "solver",
+            "meaninertia")
+
+
+def save_model(m: Model, path: str) -> None:
+  payload = {f"a_{k}": v for k, v in m.arrays.items()}
+  meta = {k: getattr(m, k) for k in _SCALARS}
+  meta["gravity"] = list(map(float, m.gravity))
+  meta["names"] = m.names
+  payload["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+  np.savez_compressed(path, **payload)
+
+
+def load_model(path: str) -> Model:
+  with np.load(path, allow_pickle=False) as z:
+    meta = json.loads(bytes(z["meta"]).decode())
+    m = Model()
+    for k in _SCALARS:
+      setattr(m, k, meta[k])
+    m.gravity = np.array(meta["gravity"])
+    m.names = meta["names"]
+    m.arrays = {k[2:]: z[k].copy() for k in z.files if k.startswith("a_")}
+  return m
+
+
+def load_scene(name: str) -> Model:
+  path = os.path.join(ASSET_DIR, f"{name}.npz")
+  if not os.path.exists(path):
+    raise FileNotFoundError(f"compiled scene {path} missing; run scripts/build_assets.py")
+  return load_model(path)

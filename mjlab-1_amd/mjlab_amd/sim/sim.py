@@ -1,0 +1,227 @@
+"""`Simulation`: the drop-in replacement of mjlab's physics boundary on MI355X.
+
+Same classes, fields and methods as `src/mjlab/sim/sim.py:42-286`
+(`MujocoCfg`, `SimulationCfg`, `Simulation.{step,forward,reset,expand_model_fields,
+get_default_field,create_graph}` and the `model`/`data`/`mj_model` properties), backed
+by libmjx355 (one HIP kernel per step, all worlds, one wavefront per world) instead of
+MuJoCo-Warp.  `model` is the compiled host `Model` (mjlab_amd.compiler.model) where the
+reference passes a `mujoco.MjModel`.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import ctypes
+from dataclasses import dataclass, field
+from typing import Literal
+
+import numpy as np
+import torch
+
+from .._capi import make_desc
+from .._lib import MjxError, check, lib
+from .sim_data import DeviceBridge, field_tensor
+
+_INTEGRATORS = {"euler": 0, "implicitfast": 1}
+
+
+@dataclass
+class MujocoCfg:
+  """Configuration for MuJoCo simulation parameters (sim/sim.py:42-79)."""
+
+  timestep: float = 0.002
+  integrator: Literal["euler", "implicitfast"] = "implicitfast"
+  impratio: float = 1.0
+  cone: Literal["pyramidal", "elliptic"] = "pyramidal"
+  jacobian: Literal["auto", "dense", "sparse"] = "auto"
+  solver: Literal["newton", "cg", "pgs"] = "newton"
+  iterations: int = 100
+  tolerance: float = 1e-8
+  ls_iterations: int = 50
+  ls_tolerance: float = 0.01
+  ccd_iterations: int = 50
+  gravity: tuple[float, float, float] = (0, 0, -9.81)
+
+  def apply(self, model) -> None:
+    """Apply configuration settings to a compiled model (MujocoCfg.apply)."""
+    if self.cone != "pyramidal":
+      raise NotImplementedError("only pyramidal friction cones are implemented")
+    if self.solver != "newton":
+      raise NotImplementedError("only the Newton solver is implemented")
+    model.integrator = _INTEGRATORS[self.integrator]
+    model.cone = 0
+    model.timestep = float(self.timestep)
+    model.impratio = float(self.impratio)
+    model.gravity = np.asarray(self.gravity, dtype=np.float64)
+    model.iterations = int(self.iterations)
+    model.tolerance = float(self.tolerance)
+    model.ls_iterations = int(self.ls_iterations)
+    model.ls_tolerance = float(self.ls_tolerance)
+
+
+@dataclass
+class NanGuardCfg:
+  """`utils/nan_guard.py` config; the dump tool is out of scope, `watch()` is a no-op."""
+  enabled: bool = False
+  buffer_size: int = 100
+  output_dir: str = "/tmp/mjlab/nan_dumps"
+  max_envs_to_dump: int = 5
+
+
+class NanGuard:
+  def __init__(self, cfg: NanGuardCfg, num_envs: int, model) -> None:
+    self.cfg = cfg
+
+  @contextlib.contextmanager
+  def watch(self, data):
+    yield
+
+
+@dataclass(kw_only=True)
+class SimulationCfg:
+  nconmax: int | None = None
+  """Contacts per world (engine holds at most 64 per world in LDS)."""
+  njmax: int | None = None
+  """Constraint rows per world held in LDS."""
+  ls_parallel: bool = True  # accepted for API compatibility; the line search is exact
+  contact_sensor_maxmatch: int = 64
+  mujoco: MujocoCfg = field(default_factory=MujocoCfg)
+  nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
+
+
+def _stream_handle(device: torch.device) -> int:
+  return torch.cuda.current_stream(device).cuda_stream
+
+
+def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
+  """Per-world contact/row capacities held in LDS."""
+  ncon = cfg.nconmax if cfg.nconmax is not None else 48
+  ncon = int(min(64, max(ncon, 48)))
+  rows = cfg.njmax if cfg.njmax is not None else 160
+  nlim = int(np.sum(model.jnt_limited)) if model.njnt else 0
+  rows = int(max(1, min(rows, 4 * ncon + 2 * nlim, 160)))
+  return ncon, rows
+
+
+class Simulation:
+  """GPU-batched MuJoCo physics on MI355X (see module docstring)."""
+
+  def __init__(self, num_envs: int, cfg: SimulationCfg, model, device: str):
+    self.cfg = cfg
+    self.device = device
+    self.num_envs = int(num_envs)
+    self._default_model_fields: dict[str, torch.Tensor] = {}
+    dev = torch.device(device)
+    if dev.type != "cuda":
+      raise MjxError("mjlab_amd.Simulation runs only on a ROCm GPU (device 'cuda:N'); "
+                     "there is no CPU fallback in the product path")
+    self._torch_device = torch.device("cuda", dev.index if dev.index is not None else
+                                      torch.cuda.current_device())
+    self._mj_model = model
+    cfg.mujoco.apply(self._mj_model)
+    L = lib()
+    desc, keep = make_desc(model)
+    self._model_ptr = ctypes.c_void_p()
+    check(L.mjx_model_create(ctypes.byref(desc), self._torch_device.index,
+                             ctypes.byref(self._model_ptr)))
+    del keep
+    self.nconmax, self.njmax = world_capacity(cfg, model)
+    self._sim = ctypes.c_void_p()
+    check(L.mjx_sim_create(self._model_ptr, self.num_envs, self.nconmax, self.njmax,
+                           ctypes.byref(self._sim)))
+    self._field_names = {L.mjx_field_name(self._sim, i).decode()
+                         for i in range(L.mjx_field_count(self._sim))}
+    self._data_bridge = DeviceBridge(self, "", None)
+    self._model_bridge = DeviceBridge(self, "model.", self.num_envs)
+    self._reset_mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self._torch_device)
+    self.nan_guard = NanGuard(cfg.nan_guard, self.num_envs, self._mj_model)
+    self.create_graph()
+
+  def __del__(self):
+    try:
+      if getattr(self, "_sim", None) and self._sim.value:
+        torch.cuda.synchronize(self._torch_device)
+        lib().mjx_sim_destroy(self._sim)
+        self._sim = ctypes.c_void_p()
+      if getattr(self, "_model_ptr", None) and self._model_ptr.value:
+        lib().mjx_model_destroy(self._model_ptr)
+        self._model_ptr = ctypes.c_void_p()
+    except Exception:
+      pass
+
+  def create_graph(self) -> None:
+    """API parity with sim/sim.py:164-191.  A step is ONE kernel launch over all worlds
+    with stable device pointers, so there is nothing to capture; callers that want to
+    amortise host launch cost over a whole env step capture it with torch.cuda.graph."""
+    self.step_graph = None
+    self.forward_graph = None
+    self.reset_graph = None
+
+  # Properties.
+  @property
+  def mj_model(self):
+    return self._mj_model
+
+  @property
+  def data(self) -> DeviceBridge:
+    return self._data_bridge
+
+  @property
+  def model(self) -> DeviceBridge:
+    return self._model_bridge
+
+  @property
+  def default_model_fields(self) -> dict[str, torch.Tensor]:
+    return self._default_model_fields
+
+  # Methods.
+  def expand_model_fields(self, fields: tuple[str, ...]) -> None:
+    if not fields:
+      return
+    invalid = [f for f in fields if f not in self._mj_model.arrays]
+    if invalid:
+      raise ValueError(f"Fields not found in model: {invalid}")
+    stream = _stream_handle(self._torch_device)
+    for f in fields:
+      if lib().mjx_field_is_expanded(self._sim, f.encode()):
+        continue
+      check(lib().mjx_expand_field(self._sim, f.encode(), stream))
+    self._model_bridge.clear_cache()
+    self.create_graph()
+
+  def get_default_field(self, field: str) -> torch.Tensor:
+    if field not in self._default_model_fields:
+      if field not in self._mj_model.arrays:
+        raise ValueError(f"Field '{field}' not found in model")
+      model_field = getattr(self.model, field)
+      self._default_model_fields[field] = torch.as_tensor(
+        np.asarray(self._mj_model.arrays[field]), dtype=model_field.dtype,
+        device=self._torch_device).reshape(model_field.shape[1:]).clone()
+    return self._default_model_fields[field]
+
+  def forward(self) -> None:
+    check(lib().mjx_forward(self._sim, _stream_handle(self._torch_device)))
+
+  def step(self, nsubstep: int = 1) -> None:
+    """One mj_step for every world (or `nsubstep` steps fused in one launch)."""
+    with self.nan_guard.watch(self.data):
+      check(lib().mjx_step(self._sim, int(nsubstep), _stream_handle(self._torch_device)))
+
+  def reset(self, env_ids: torch.Tensor | None = None) -> None:
+    stream = _stream_handle(self._torch_device)
+    if env_ids is None:
+      check(lib().mjx_reset(self._sim, None, stream))
+      return
+    self._reset_mask.fill_(0)
+    self._reset_mask[env_ids] = 1
+    check(lib().mjx_reset(self._sim, ctypes.c_void_p(self._reset_mask.data_ptr()), stream))
+
+  def stats(self) -> dict:
+    """Engine counters: max contacts/rows seen, overflow and unsupported-pair events."""
+    out = (ctypes.c_int32 * 8)()
+    check(lib().mjx_sim_stats(self._sim, out, _stream_handle(self._torch_device)))
+    return dict(max_ncon=out[0], max_nefc=out[1], con_overflow=out[2], row_overflow=out[3],
+                unsupported=out[4], max_niter=out[5])
+
+  def field(self, name: str) -> torch.Tensor:
+    return field_tensor(self._sim, name)

@@ -1,0 +1,1394 @@
+/* oracle.c — CPU fp64 restatement of MuJoCo's mj_step for the mjlab hot-path subset.
+ *
+ * TEST INFRASTRUCTURE (see oracle.h).  Written for clarity, not speed: dense mass
+ * matrix, dense constraint Jacobian, dense Cholesky, serial loops over bodies in
+ * index order (parents precede children).
+ *
+ * Stage order follows MuJoCo's mj_step = mj_forward + integrate, which the reference
+ * reaches through mujoco_warp.step (src/mjlab/sim/sim.py:267-273):
+ *   kinematics -> comPos -> crb -> collision -> makeConstraint -> transmission ->
+ *   sensorPos -> comVel -> passive -> rne -> subtreeVel -> sensorVel -> actuation ->
+ *   fwdAcceleration -> Newton solve -> rnePostConstraint -> sensorAcc ->
+ *   implicitfast (or Euler) integration.
+ * Conventions pinned by mjlab itself: free-joint qpos = pos + quat(wxyz), qvel = world
+ * linear + BODY angular (src/mjlab/entity/data.py:89-110); cvel = [ang; lin at
+ * subtree_com(root)] (src/mjlab/entity/data.py:20-31); position actuator
+ * force = kp*ctrl - kp*q - kd*qd clamped to forcerange (src/mjlab/utils/spec.py:122-165,
+ * tests/test_spec_utils.py:26-102).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MINVAL 1e-15
+#define MINMU 1e-5
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+
+enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
+
+/* ------------------------------------------------------------------ small math */
+static void v3_copy(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+static void v3_add(double* r, const double* a, const double* b) {
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+}
+static void v3_sub(double* r, const double* a, const double* b) {
+  r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2];
+}
+static void v3_scl(double* r, const double* a, double s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+static double v3_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void v3_cross(double* r, const double* a, const double* b) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static double v3_norm(const double* a) { return sqrt(v3_dot(a, a)); }
+static double v3_normalize(double* a) {
+  double n = v3_norm(a);
+  if (n < MINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; return 0; }
+  a[0] /= n; a[1] /= n; a[2] /= n;
+  return n;
+}
+/* r = M*v, M row-major 3x3 */
+static void m3_mulv(double* r, const double* M, const double* v) {
+  double t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  double t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  double t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+/* r = M^T*v */
+static void m3_mulTv(double* r, const double* M, const double* v) {
+  double t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  double t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  double t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static void m3_mul(double* R, const double* A, const double* B) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+  memcpy(R, t, sizeof(t));
+}
+static void q_mul(double* r, const double* a, const double* b) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static void q_normalize(double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+static void q_tomat(double* M, const double* qin) {
+  double q[4] = {qin[0], qin[1], qin[2], qin[3]};
+  q_normalize(q);
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  M[0] = 1 - 2 * (y * y + z * z); M[1] = 2 * (x * y - w * z); M[2] = 2 * (x * z + w * y);
+  M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
+  M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
+}
+static void q_axisangle(double* q, const double* axis, double ang) {
+  double s = sin(0.5 * ang);
+  q[0] = cos(0.5 * ang); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+/* spatial motion cross product: r = v x s, v = [w; u] */
+static void cross_motion(double* r, const double* v, const double* s) {
+  double t[6], a[3];
+  v3_cross(t, v, s);
+  v3_cross(t + 3, v, s + 3);
+  v3_cross(a, v + 3, s);
+  t[3] += a[0]; t[4] += a[1]; t[5] += a[2];
+  memcpy(r, t, sizeof(t));
+}
+/* spatial force cross product: r = v x* f */
+static void cross_force(double* r, const double* v, const double* f) {
+  double t[6], a[3];
+  v3_cross(t, v, f);
+  v3_cross(a, v + 3, f + 3);
+  t[0] += a[0]; t[1] += a[1]; t[2] += a[2];
+  v3_cross(t + 3, v, f + 3);
+  memcpy(r, t, sizeof(t));
+}
+/* cinert (10: Ixx Iyy Izz Ixy Ixz Iyz, m*d(3), m) times motion v -> force */
+static void inert_mul(double* r, const double* I, const double* v) {
+  const double* w = v; const double* u = v + 3;
+  const double* h = I + 6; double m = I[9];
+  double t[6];
+  t[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
+  t[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
+  t[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
+  double a[3];
+  v3_cross(a, h, u); /* (m d) x u */
+  t[0] += a[0]; t[1] += a[1]; t[2] += a[2];
+  v3_cross(a, h, w); /* (m d) x w */
+  t[3] = m * u[0] - a[0]; t[4] = m * u[1] - a[1]; t[5] = m * u[2] - a[2];
+  memcpy(r, t, sizeof(t));
+}
+static double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+/* contact frame from normal (mju_makeFrame semantics) */
+static void make_frame(double* f) {
+  double tmp[3];
+  v3_normalize(f);
+  f[3] = f[4] = f[5] = 0;
+  if (fabs(f[1]) < 0.5) f[4] = 1; else f[5] = 1;
+  v3_scl(tmp, f, v3_dot(f, f + 3));
+  v3_sub(f + 3, f + 3, tmp);
+  v3_normalize(f + 3);
+  v3_cross(f + 6, f, f + 3);
+}
+/* dense Cholesky in place (lower), returns 0 on success */
+static int chol(double* A, int n) {
+  for (int j = 0; j < n; j++) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+    if (s < MINVAL) s = MINVAL;
+    double l = sqrt(s);
+    A[j * n + j] = l;
+    for (int i = j + 1; i < n; i++) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / l;
+    }
+  }
+  return 0;
+}
+static void chol_solve(const double* L, int n, double* x) {
+  for (int i = 0; i < n; i++) {
+    double t = x[i];
+    for (int k = 0; k < i; k++) t -= L[i * n + k] * x[k];
+    x[i] = t / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double t = x[i];
+    for (int k = i + 1; k < n; k++) t -= L[k * n + i] * x[k];
+    x[i] = t / L[i * n + i];
+  }
+}
+
+/* ------------------------------------------------------------------ data alloc */
+orcData* orc_data_new(const mjxModelDesc* m, int nconmax, int njmax) {
+  orcData* d = (orcData*)calloc(1, sizeof(orcData));
+  int nb = m->nbody, nv = m->nv;
+  d->nconmax = nconmax;
+  d->njmax = njmax;
+#define A(f, n) d->f = (double*)calloc((size_t)((n) > 0 ? (n) : 1), sizeof(double))
+  A(qpos, m->nq); A(qvel, nv); A(qacc_warmstart, nv); A(ctrl, m->nu); A(qfrc_applied, nv);
+  A(xfrc_applied, 6 * nb);
+  A(xpos, 3 * nb); A(xquat, 4 * nb); A(xmat, 9 * nb); A(xipos, 3 * nb); A(ximat, 9 * nb);
+  A(xanchor, 3 * m->njnt); A(xaxis, 3 * m->njnt);
+  A(geom_xpos, 3 * m->ngeom); A(geom_xmat, 9 * m->ngeom); A(site_xpos, 3 * m->nsite);
+  A(site_xmat, 9 * m->nsite);
+  A(subtree_com, 3 * nb); A(cinert, 10 * nb); A(cdof, 6 * nv); A(crb, 10 * nb); A(qM, nv * nv);
+  A(cvel, 6 * nb); A(cdof_dot, 6 * nv); A(qfrc_bias, nv); A(qfrc_passive, nv);
+  A(subtree_linvel, 3 * nb); A(subtree_angmom, 3 * nb);
+  A(actuator_force, m->nu); A(qfrc_actuator, nv); A(qfrc_smooth, nv); A(qacc_smooth, nv);
+  A(qacc, nv); A(qfrc_constraint, nv); A(cacc, 6 * nb); A(sensordata, m->nsensordata);
+  A(efc_J, njmax * nv); A(efc_pos, njmax); A(efc_margin, njmax); A(efc_D, njmax);
+  A(efc_R, njmax); A(efc_aref, njmax); A(efc_vel, njmax); A(efc_force, njmax);
+  A(efc_diagApprox, njmax); A(efc_frame_mu, njmax);
+  A(work, 8 * nv * nv + 32 * nv + 8 * njmax + 16 * nb + 64);
+#undef A
+  d->contact = (orcContact*)calloc((size_t)(nconmax > 0 ? nconmax : 1), sizeof(orcContact));
+  d->efc_type = (int*)calloc((size_t)(njmax > 0 ? njmax : 1), sizeof(int));
+  d->efc_id = (int*)calloc((size_t)(njmax > 0 ? njmax : 1), sizeof(int));
+  orc_reset(m, d);
+  return d;
+}
+
+void orc_data_free(orcData* d) {
+  if (!d) return;
+  double** p[] = {&d->qpos, &d->qvel, &d->qacc_warmstart, &d->ctrl, &d->qfrc_applied,
+                  &d->xfrc_applied, &d->xpos, &d->xquat, &d->xmat, &d->xipos, &d->ximat,
+                  &d->xanchor, &d->xaxis, &d->geom_xpos, &d->geom_xmat, &d->site_xpos,
+                  &d->site_xmat, &d->subtree_com, &d->cinert, &d->cdof, &d->crb, &d->qM,
+                  &d->cvel, &d->cdof_dot, &d->qfrc_bias, &d->qfrc_passive, &d->subtree_linvel,
+                  &d->subtree_angmom, &d->actuator_force, &d->qfrc_actuator, &d->qfrc_smooth,
+                  &d->qacc_smooth, &d->qacc, &d->qfrc_constraint, &d->cacc, &d->sensordata,
+                  &d->efc_J, &d->efc_pos, &d->efc_margin, &d->efc_D, &d->efc_R, &d->efc_aref,
+                  &d->efc_vel, &d->efc_force, &d->efc_diagApprox, &d->efc_frame_mu, &d->work};
+  for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
+  free(d->contact); free(d->efc_type); free(d->efc_id);
+  free(d);
+}
+
+void orc_reset(const mjxModelDesc* m, orcData* d) {
+  memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+  memset(d->qvel, 0, sizeof(double) * m->nv);
+  memset(d->qacc_warmstart, 0, sizeof(double) * m->nv);
+  memset(d->qacc, 0, sizeof(double) * m->nv);
+  memset(d->ctrl, 0, sizeof(double) * m->nu);
+  memset(d->qfrc_applied, 0, sizeof(double) * m->nv);
+  memset(d->xfrc_applied, 0, sizeof(double) * 6 * m->nbody);
+  memset(d->sensordata, 0, sizeof(double) * m->nsensordata);
+  d->time = 0;
+  d->ncon = d->nefc = 0;
+}
+
+/* ------------------------------------------------------------------ position stage */
+static void kinematics(const mjxModelDesc* m, orcData* d) {
+  d->xpos[0] = d->xpos[1] = d->xpos[2] = 0;
+  d->xquat[0] = 1; d->xquat[1] = d->xquat[2] = d->xquat[3] = 0;
+  q_tomat(d->xmat, d->xquat);
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parentid[b];
+    double pos[3], q[4], R[9];
+    m3_mulv(pos, d->xmat + 9 * p, m->body_pos + 3 * b);
+    v3_add(pos, pos, d->xpos + 3 * p);
+    q_mul(q, d->xquat + 4 * p, m->body_quat + 4 * b);
+    for (int k = m->body_jntadr[b]; k < m->body_jntadr[b] + m->body_jntnum[b]; k++) {
+      int a = m->jnt_qposadr[k];
+      if (m->jnt_type[k] == MJX_JNT_FREE) {
+        v3_copy(pos, d->qpos + a);
+        memcpy(q, d->qpos + a + 3, 4 * sizeof(double));
+        q_normalize(q);
+        v3_copy(d->xanchor + 3 * k, pos);
+        q_tomat(R, q);
+        m3_mulv(d->xaxis + 3 * k, R, m->jnt_axis + 3 * k);
+        continue;
+      }
+      q_tomat(R, q);
+      m3_mulv(d->xanchor + 3 * k, R, m->jnt_pos + 3 * k);
+      v3_add(d->xanchor + 3 * k, d->xanchor + 3 * k, pos);
+      m3_mulv(d->xaxis + 3 * k, R, m->jnt_axis + 3 * k);
+      if (m->jnt_type[k] == MJX_JNT_HINGE) {
+        double qr[4], off[3];
+        q_axisangle(qr, m->jnt_axis + 3 * k, d->qpos[a] - m->qpos0[a]);
+        q_mul(q, q, qr);
+        q_tomat(R, q);
+        m3_mulv(off, R, m->jnt_pos + 3 * k);
+        v3_sub(pos, d->xanchor + 3 * k, off);
+      } else if (m->jnt_type[k] == MJX_JNT_SLIDE) {
+        double s = d->qpos[a] - m->qpos0[a];
+        for (int i = 0; i < 3; i++) pos[i] += d->xaxis[3 * k + i] * s;
+      }
+    }
+    q_normalize(q);
+    v3_copy(d->xpos + 3 * b, pos);
+    memcpy(d->xquat + 4 * b, q, sizeof(q));
+    q_tomat(d->xmat + 9 * b, q);
+  }
+  for (int b = 0; b < m->nbody; b++) {
+    double Ri[9], t[3];
+    m3_mulv(t, d->xmat + 9 * b, m->body_ipos + 3 * b);
+    v3_add(d->xipos + 3 * b, d->xpos + 3 * b, t);
+    q_tomat(Ri, m->body_iquat + 4 * b);
+    m3_mul(d->ximat + 9 * b, d->xmat + 9 * b, Ri);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    double Rg[9], t[3];
+    m3_mulv(t, d->xmat + 9 * b, m->geom_pos + 3 * g);
+    v3_add(d->geom_xpos + 3 * g, d->xpos + 3 * b, t);
+    q_tomat(Rg, m->geom_quat + 4 * g);
+    m3_mul(d->geom_xmat + 9 * g, d->xmat + 9 * b, Rg);
+  }
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    double Rs[9], t[3];
+    m3_mulv(t, d->xmat + 9 * b, m->site_pos + 3 * s);
+    v3_add(d->site_xpos + 3 * s, d->xpos + 3 * b, t);
+    q_tomat(Rs, m->site_quat + 4 * s);
+    m3_mul(d->site_xmat + 9 * s, d->xmat + 9 * b, Rs);
+  }
+}
+
+static void com_pos(const mjxModelDesc* m, orcData* d) {
+  int nb = m->nbody;
+  double* mass = d->work; /* nb */
+  for (int b = 0; b < nb; b++) {
+    mass[b] = m->body_mass[b];
+    v3_scl(d->subtree_com + 3 * b, d->xipos + 3 * b, m->body_mass[b]);
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    mass[p] += mass[b];
+    v3_add(d->subtree_com + 3 * p, d->subtree_com + 3 * p, d->subtree_com + 3 * b);
+  }
+  for (int b = 0; b < nb; b++) {
+    if (mass[b] > MINVAL) v3_scl(d->subtree_com + 3 * b, d->subtree_com + 3 * b, 1.0 / mass[b]);
+    else v3_copy(d->subtree_com + 3 * b, d->xipos + 3 * b);
+  }
+  /* cinert: inertia about subtree_com(root), world frame */
+  for (int b = 0; b < nb; b++) {
+    double* c = d->cinert + 10 * b;
+    memset(c, 0, 10 * sizeof(double));
+    if (b == 0) continue;
+    const double* off = d->subtree_com + 3 * m->body_rootid[b];
+    const double* R = d->ximat + 9 * b;
+    const double* I = m->body_inertia + 3 * b;
+    double full[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        full[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
+    double dv[3], ms = m->body_mass[b];
+    v3_sub(dv, d->xipos + 3 * b, off);
+    double dd = v3_dot(dv, dv);
+    c[0] = full[0] + ms * (dd - dv[0] * dv[0]);
+    c[1] = full[4] + ms * (dd - dv[1] * dv[1]);
+    c[2] = full[8] + ms * (dd - dv[2] * dv[2]);
+    c[3] = full[1] - ms * dv[0] * dv[1];
+    c[4] = full[2] - ms * dv[0] * dv[2];
+    c[5] = full[5] - ms * dv[1] * dv[2];
+    c[6] = ms * dv[0]; c[7] = ms * dv[1]; c[8] = ms * dv[2];
+    c[9] = ms;
+  }
+  /* cdof */
+  for (int k = 0; k < m->njnt; k++) {
+    int b = m->jnt_bodyid[k], dof = m->jnt_dofadr[k];
+    const double* off = d->subtree_com + 3 * m->body_rootid[b];
+    double rel[3];
+    v3_sub(rel, off, d->xanchor + 3 * k);
+    switch (m->jnt_type[k]) {
+      case MJX_JNT_FREE:
+        for (int i = 0; i < 3; i++) {
+          double* c = d->cdof + 6 * (dof + i);
+          memset(c, 0, 6 * sizeof(double));
+          c[3 + i] = 1;
+        }
+        for (int i = 0; i < 3; i++) {
+          double* c = d->cdof + 6 * (dof + 3 + i);
+          double ax[3] = {d->xmat[9 * b + i], d->xmat[9 * b + 3 + i], d->xmat[9 * b + 6 + i]};
+          v3_copy(c, ax);
+          v3_cross(c + 3, ax, rel);
+        }
+        break;
+      case MJX_JNT_HINGE: {
+        double* c = d->cdof + 6 * dof;
+        v3_copy(c, d->xaxis + 3 * k);
+        v3_cross(c + 3, d->xaxis + 3 * k, rel);
+      } break;
+      case MJX_JNT_SLIDE: {
+        double* c = d->cdof + 6 * dof;
+        c[0] = c[1] = c[2] = 0;
+        v3_copy(c + 3, d->xaxis + 3 * k);
+      } break;
+    }
+  }
+}
+
+static void crb(const mjxModelDesc* m, orcData* d) {
+  int nb = m->nbody, nv = m->nv;
+  memcpy(d->crb, d->cinert, sizeof(double) * 10 * nb);
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p > 0)
+      for (int i = 0; i < 10; i++) d->crb[10 * p + i] += d->crb[10 * b + i];
+  }
+  memset(d->qM, 0, sizeof(double) * nv * nv);
+  for (int i = 0; i < nv; i++) {
+    double f[6];
+    inert_mul(f, d->crb + 10 * m->dof_bodyid[i], d->cdof + 6 * i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = dot6(d->cdof + 6 * j, f);
+      d->qM[i * nv + j] = v;
+      d->qM[j * nv + i] = v;
+    }
+    d->qM[i * nv + i] += m->dof_armature[i];
+  }
+}
+
+/* ------------------------------------------------------------------ collision */
+static int add_contact(orcData* d, int g1, int g2, double dist, const double* pos, const double* n) {
+  if (d->ncon >= d->nconmax) { d->overflow |= 1; return 0; }
+  orcContact* c = d->contact + d->ncon++;
+  memset(c, 0, sizeof(*c));
+  c->geom1 = g1; c->geom2 = g2; c->dist = dist;
+  v3_copy(c->pos, pos);
+  v3_copy(c->frame, n);
+  make_frame(c->frame);
+  return 1;
+}
+
+static int col_sphere_sphere(orcData* d, int g1, int g2, const double* p1, double r1,
+                             const double* p2, double r2, double margin) {
+  double dif[3];
+  v3_sub(dif, p2, p1);
+  double cd = v3_norm(dif);
+  double dist = cd - r1 - r2;
+  if (dist > margin) return 0;
+  double n[3];
+  if (cd < MINVAL) { n[0] = 1; n[1] = n[2] = 0; }
+  else v3_scl(n, dif, 1.0 / cd);
+  double pos[3];
+  for (int i = 0; i < 3; i++) pos[i] = p1[i] + n[i] * (r1 + 0.5 * dist);
+  return add_contact(d, g1, g2, dist, pos, n);
+}
+
+static int col_plane_sphere(orcData* d, int g1, int g2, const double* pp, const double* n,
+                            const double* c, double r, double margin) {
+  double t[3];
+  v3_sub(t, c, pp);
+  double dist = v3_dot(t, n) - r;
+  if (dist > margin) return 0;
+  double pos[3];
+  for (int i = 0; i < 3; i++) pos[i] = c[i] - n[i] * (r + 0.5 * dist);
+  return add_contact(d, g1, g2, dist, pos, n);
+}
+
+/* closest points between segments [a0,a1] and [b0,b1] (clamped) */
+static void seg_seg(const double* a0, const double* a1, const double* b0, const double* b1,
+                    double* pa, double* pb) {
+  double u[3], v[3], w[3];
+  v3_sub(u, a1, a0); v3_sub(v, b1, b0); v3_sub(w, a0, b0);
+  double a = v3_dot(u, u), b = v3_dot(u, v), c = v3_dot(v, v), dd = v3_dot(u, w), e = v3_dot(v, w);
+  double den = a * c - b * b, s, t;
+  if (a < MINVAL && c < MINVAL) { s = t = 0; }
+  else if (a < MINVAL) { s = 0; t = e / c; t = t < 0 ? 0 : (t > 1 ? 1 : t); }
+  else if (c < MINVAL) { t = 0; s = -dd / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+  else {
+    s = den > MINVAL * a * c ? (b * e - c * dd) / den : 0;
+    s = s < 0 ? 0 : (s > 1 ? 1 : s);
+    t = (b * s + e) / c;
+    if (t < 0) { t = 0; s = -dd / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+    else if (t > 1) { t = 1; s = (b - dd) / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+  }
+  for (int i = 0; i < 3; i++) { pa[i] = a0[i] + s * u[i]; pb[i] = b0[i] + t * v[i]; }
+}
+
+static void capsule_ends(const orcData* d, const mjxModelDesc* m, int g, double* e0, double* e1) {
+  const double* p = d->geom_xpos + 3 * g;
+  const double* R = d->geom_xmat + 9 * g;
+  double h = m->geom_size[3 * g + 1];
+  for (int i = 0; i < 3; i++) {
+    e0[i] = p[i] + R[3 * i + 2] * h;
+    e1[i] = p[i] - R[3 * i + 2] * h;
+  }
+}
+
+static void contact_params(const mjxModelDesc* m, orcContact* c) {
+  int g1 = c->geom1, g2 = c->geom2;
+  int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
+  double fr[3];
+  if (p1 != p2) {
+    int g = p1 > p2 ? g1 : g2;
+    c->dim = m->geom_condim[g];
+    v3_copy(fr, m->geom_friction + 3 * g);
+    memcpy(c->solref, m->geom_solref + 2 * g, 2 * sizeof(double));
+    memcpy(c->solimp, m->geom_solimp + 5 * g, 5 * sizeof(double));
+  } else {
+    c->dim = m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
+    for (int i = 0; i < 3; i++)
+      fr[i] = fmax(m->geom_friction[3 * g1 + i], m->geom_friction[3 * g2 + i]);
+    double s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2], mix;
+    if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+    else if (s1 < MINVAL) mix = 0.0;
+    else if (s2 < MINVAL) mix = 1.0;
+    else mix = s1 / (s1 + s2);
+    const double *r1 = m->geom_solref + 2 * g1, *r2 = m->geom_solref + 2 * g2;
+    if (r1[0] > 0 && r2[0] > 0)
+      for (int i = 0; i < 2; i++) c->solref[i] = mix * r1[i] + (1 - mix) * r2[i];
+    else
+      for (int i = 0; i < 2; i++) c->solref[i] = fmin(r1[i], r2[i]);
+    for (int i = 0; i < 5; i++)
+      c->solimp[i] = mix * m->geom_solimp[5 * g1 + i] + (1 - mix) * m->geom_solimp[5 * g2 + i];
+  }
+  c->friction[0] = c->friction[1] = fmax(MINMU, fr[0]);
+  c->friction[2] = fmax(MINMU, fr[1]);
+  c->friction[3] = c->friction[4] = fmax(MINMU, fr[2]);
+  double mg = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+  double gp = fmax(m->geom_gap[g1], m->geom_gap[g2]);
+  c->includemargin = mg - gp;
+}
+
+/* heightfield helpers: prism triangles under a sphere.  The hfield surface is the
+ * piecewise-linear interpolation over a regular grid, two triangles per cell. */
+static double hfield_height(const mjxModelDesc* m, int h, int r, int c) {
+  return m->hfield_data[m->hfield_adr[h] + r * m->hfield_ncol[h] + c] * m->hfield_size[4 * h + 2];
+}
+
+static int col_hfield_sphere(const mjxModelDesc* m, orcData* d, int g1, int g2,
+                             const double* center, double r, double margin) {
+  /* sphere against the hfield surface: closest point over the triangles of the cells
+   * under the sphere's footprint; one contact (deepest). */
+  int h = m->geom_dataid[g1];
+  const double* hp = d->geom_xpos + 3 * g1;
+  const double* R = d->geom_xmat + 9 * g1;
+  double loc[3], t[3];
+  v3_sub(t, center, hp);
+  m3_mulTv(loc, R, t);
+  int nr = m->hfield_nrow[h], nc = m->hfield_ncol[h];
+  double sx = m->hfield_size[4 * h], sy = m->hfield_size[4 * h + 1];
+  double dx = 2 * sx / (nc - 1), dy = 2 * sy / (nr - 1);
+  int c0 = (int)floor((loc[0] - r + sx) / dx), c1 = (int)floor((loc[0] + r + sx) / dx);
+  int r0 = (int)floor((loc[1] - r + sy) / dy), r1 = (int)floor((loc[1] + r + sy) / dy);
+  if (c1 < 0 || r1 < 0 || c0 > nc - 2 || r0 > nr - 2) return 0;
+  c0 = c0 < 0 ? 0 : c0; r0 = r0 < 0 ? 0 : r0;
+  c1 = c1 > nc - 2 ? nc - 2 : c1; r1 = r1 > nr - 2 ? nr - 2 : r1;
+  double best = 1e30, bestp[3] = {0, 0, 0}, bestn[3] = {0, 0, 1};
+  int found = 0;
+  for (int rr = r0; rr <= r1; rr++)
+    for (int cc = c0; cc <= c1; cc++) {
+      double x0 = -sx + cc * dx, y0 = -sy + rr * dy;
+      double p00[3] = {x0, y0, hfield_height(m, h, rr, cc)};
+      double p10[3] = {x0 + dx, y0, hfield_height(m, h, rr, cc + 1)};
+      double p01[3] = {x0, y0 + dy, hfield_height(m, h, rr + 1, cc)};
+      double p11[3] = {x0 + dx, y0 + dy, hfield_height(m, h, rr + 1, cc + 1)};
+      const double* tri[2][3] = {{p00, p10, p11}, {p00, p11, p01}};
+      for (int k = 0; k < 2; k++) {
+        double e1[3], e2[3], n[3];
+        v3_sub(e1, tri[k][1], tri[k][0]);
+        v3_sub(e2, tri[k][2], tri[k][0]);
+        v3_cross(n, e1, e2);
+        v3_normalize(n);
+        double w[3];
+        v3_sub(w, loc, tri[k][0]);
+        double sd = v3_dot(w, n);
+        /* project to plane, barycentric test */
+        double pp[3] = {loc[0] - sd * n[0], loc[1] - sd * n[1], loc[2] - sd * n[2]};
+        double v0[3], v1[3], v2[3];
+        v3_copy(v0, e2); v3_copy(v1, e1);
+        v3_sub(v2, pp, tri[k][0]);
+        double d00 = v3_dot(v0, v0), d01 = v3_dot(v0, v1), d11 = v3_dot(v1, v1);
+        double d20 = v3_dot(v2, v0), d21 = v3_dot(v2, v1);
+        double den = d00 * d11 - d01 * d01;
+        double u = (d11 * d20 - d01 * d21) / den, vv = (d00 * d21 - d01 * d20) / den;
+        double q[3] = {0, 0, 0};
+        if (u >= 0 && vv >= 0 && u + vv <= 1) {
+          v3_copy(q, pp);
+        } else {
+          /* closest point on the triangle edges */
+          double bestd = 1e30;
+          for (int e = 0; e < 3; e++) {
+            const double* a = tri[k][e];
+            const double* b = tri[k][(e + 1) % 3];
+            double ab[3], ap[3];
+            v3_sub(ab, b, a); v3_sub(ap, loc, a);
+            double tt = v3_dot(ap, ab) / fmax(v3_dot(ab, ab), MINVAL);
+            tt = tt < 0 ? 0 : (tt > 1 ? 1 : tt);
+            double cp[3] = {a[0] + tt * ab[0], a[1] + tt * ab[1], a[2] + tt * ab[2]};
+            double df[3];
+            v3_sub(df, loc, cp);
+            double dd = v3_dot(df, df);
+            if (dd < bestd) { bestd = dd; v3_copy(q, cp); }
+          }
+        }
+        double diff[3];
+        v3_sub(diff, loc, q);
+        double dist = v3_norm(diff);
+        double nn[3];
+        if (dist < MINVAL || sd < 0) { v3_copy(nn, n); dist = sd; }
+        else { v3_scl(nn, diff, 1.0 / dist); if (sd < 0) dist = -dist; }
+        dist -= r;
+        if (dist < best) { best = dist; v3_copy(bestp, q); v3_copy(bestn, nn); found = 1; }
+      }
+    }
+  if (!found || best > margin) return 0;
+  double nw[3], pw[3], tmp[3];
+  m3_mulv(nw, R, bestn);
+  for (int i = 0; i < 3; i++) tmp[i] = loc[i] - bestn[i] * (r + 0.5 * best);
+  m3_mulv(pw, R, tmp);
+  v3_add(pw, pw, hp);
+  (void)bestp;
+  return add_contact(d, g1, g2, best, pw, nw);
+}
+
+static void collision(const mjxModelDesc* m, orcData* d) {
+  d->ncon = 0;
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+    int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+    double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+    /* bounding-sphere test (planes / hfields have rbound 0 = infinite) */
+    if (m->geom_rbound[g1] > 0 && m->geom_rbound[g2] > 0 && t1 != MJX_GEOM_HFIELD) {
+      double dif[3];
+      v3_sub(dif, d->geom_xpos + 3 * g2, d->geom_xpos + 3 * g1);
+      if (v3_norm(dif) > m->geom_rbound[g1] + m->geom_rbound[g2] + margin) continue;
+    }
+    int n0 = d->ncon;
+    const double *p1 = d->geom_xpos + 3 * g1, *p2 = d->geom_xpos + 3 * g2;
+    const double *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
+    if (t1 == MJX_GEOM_PLANE) {
+      double n[3] = {d->geom_xmat[9 * g1 + 2], d->geom_xmat[9 * g1 + 5], d->geom_xmat[9 * g1 + 8]};
+      if (t2 == MJX_GEOM_SPHERE) {
+        col_plane_sphere(d, g1, g2, p1, n, p2, s2[0], margin);
+      } else if (t2 == MJX_GEOM_CAPSULE) {
+        double e0[3], e1[3];
+        capsule_ends(d, m, g2, e0, e1);
+        col_plane_sphere(d, g1, g2, p1, n, e0, s2[0], margin);
+        col_plane_sphere(d, g1, g2, p1, n, e1, s2[0], margin);
+      } else if (t2 == MJX_GEOM_BOX) {
+        double t[3];
+        v3_sub(t, p2, p1);
+        double dist = v3_dot(t, n);
+        const double* R = d->geom_xmat + 9 * g2;
+        int cnt = 0;
+        for (int i = 0; i < 8 && cnt < 4; i++) {
+          double v[3] = {(i & 1) ? s2[0] : -s2[0], (i & 2) ? s2[1] : -s2[1], (i & 4) ? s2[2] : -s2[2]};
+          double corner[3];
+          m3_mulv(corner, R, v);
+          double ld = v3_dot(n, corner);
+          if (dist + ld > margin || ld > 0) continue;
+          double pos[3];
+          for (int k = 0; k < 3; k++) pos[k] = corner[k] + p2[k] - n[k] * 0.5 * (dist + ld);
+          cnt += add_contact(d, g1, g2, dist + ld, pos, n);
+        }
+      } else {
+        d->overflow |= 4;
+      }
+    } else if (t1 == MJX_GEOM_HFIELD) {
+      if (t2 == MJX_GEOM_SPHERE) {
+        col_hfield_sphere(m, d, g1, g2, p2, s2[0], margin);
+      } else if (t2 == MJX_GEOM_CAPSULE) {
+        double e0[3], e1[3];
+        capsule_ends(d, m, g2, e0, e1);
+        col_hfield_sphere(m, d, g1, g2, e0, s2[0], margin);
+        col_hfield_sphere(m, d, g1, g2, e1, s2[0], margin);
+      } else {
+        d->overflow |= 4;
+      }
+    } else if (t1 == MJX_GEOM_SPHERE && t2 == MJX_GEOM_SPHERE) {
+      col_sphere_sphere(d, g1, g2, p1, s1[0], p2, s2[0], margin);
+    } else if (t1 == MJX_GEOM_SPHERE && t2 == MJX_GEOM_CAPSULE) {
+      double e0[3], e1[3], pa[3], pb[3];
+      capsule_ends(d, m, g2, e0, e1);
+      seg_seg(p1, p1, e0, e1, pa, pb);
+      col_sphere_sphere(d, g1, g2, p1, s1[0], pb, s2[0], margin);
+    } else if (t1 == MJX_GEOM_CAPSULE && t2 == MJX_GEOM_CAPSULE) {
+      double a0[3], a1[3], b0[3], b1[3], pa[3], pb[3];
+      capsule_ends(d, m, g1, a0, a1);
+      capsule_ends(d, m, g2, b0, b1);
+      seg_seg(a0, a1, b0, b1, pa, pb);
+      col_sphere_sphere(d, g1, g2, pa, s1[0], pb, s2[0], margin);
+    } else {
+      d->overflow |= 4;
+    }
+    for (int c = n0; c < d->ncon; c++) contact_params(m, d->contact + c);
+  }
+}
+
+/* ------------------------------------------------------------------ constraints */
+static void jac_point(const mjxModelDesc* m, const orcData* d, int body, const double* pt,
+                      double* jacp /* 3*nv */, double* jacr /* 3*nv or NULL */) {
+  int nv = m->nv;
+  memset(jacp, 0, sizeof(double) * 3 * nv);
+  if (jacr) memset(jacr, 0, sizeof(double) * 3 * nv);
+  if (body == 0) return;
+  const double* off = d->subtree_com + 3 * m->body_rootid[body];
+  double rel[3];
+  v3_sub(rel, pt, off);
+  for (int i = 0; i < nv; i++) {
+    if (!((m->dof_bodymask[i] >> body) & 1ull)) continue;
+    const double* c = d->cdof + 6 * i;
+    double t[3];
+    v3_cross(t, c, rel);
+    for (int k = 0; k < 3; k++) {
+      jacp[k * nv + i] = c[3 + k] + t[k];
+      if (jacr) jacr[k * nv + i] = c[k];
+    }
+  }
+}
+
+static double impedance(const double* si, double pos, double margin) {
+  double dmin = fmin(MAXIMP, fmax(MINIMP, si[0])), dmax = fmin(MAXIMP, fmax(MINIMP, si[1]));
+  double width = fmax(0, si[2]), mid = fmin(1, fmax(MINIMP, si[3])), power = fmax(1, si[4]);
+  if (dmin == dmax || width <= MINVAL) return 0.5 * (dmin + dmax);
+  double x = fabs(pos - margin) / width;
+  if (x >= 1 || x <= 0) return x >= 1 ? dmax : dmin;
+  double y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = pow(x, power) / pow(mid, power - 1);
+  else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+static int add_row(const mjxModelDesc* m, orcData* d, int type, int id, const double* J,
+                   double pos, double margin, double diag, const double* solref,
+                   const double* solimp) {
+  if (d->nefc >= d->njmax) { d->overflow |= 2; return -1; }
+  int r = d->nefc++, nv = m->nv;
+  memcpy(d->efc_J + (size_t)r * nv, J, sizeof(double) * nv);
+  d->efc_type[r] = type; d->efc_id[r] = id;
+  d->efc_pos[r] = pos; d->efc_margin[r] = margin; d->efc_diagApprox[r] = diag;
+  double imp = impedance(solimp, pos, margin);
+  double R = fmax(MINVAL, (1 - imp) * diag / imp);
+  d->efc_R[r] = R;
+  d->efc_D[r] = 1.0 / R;
+  double dmax = fmin(MAXIMP, fmax(MINIMP, solimp[1]));
+  double K, B;
+  if (solref[0] > 0) {
+    double tc = fmax(solref[0], 2 * m->timestep), dr = solref[1];
+    K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+    B = 2.0 / (dmax * tc);
+  } else {
+    K = -solref[0] / (dmax * dmax);
+    B = -solref[1] / dmax;
+  }
+  double vel = 0;
+  for (int i = 0; i < nv; i++) vel += J[i] * d->qvel[i];
+  d->efc_vel[r] = vel;
+  d->efc_aref[r] = -B * vel - K * imp * (pos - margin);
+  return r;
+}
+
+static void make_constraint(const mjxModelDesc* m, orcData* d) {
+  int nv = m->nv;
+  d->nefc = 0;
+  double* J = d->work;                       /* nv */
+  double* jp1 = d->work + nv;                /* 3nv */
+  double* jp2 = d->work + 4 * nv;            /* 3nv */
+  double* jdif = d->work + 7 * nv;           /* 3nv */
+  /* joint limits: lower (side -1) then upper (side +1) */
+  for (int k = 0; k < m->njnt; k++) {
+    if (!m->jnt_limited[k]) continue;
+    int t = m->jnt_type[k];
+    if (t != MJX_JNT_HINGE && t != MJX_JNT_SLIDE) continue;
+    double q = d->qpos[m->jnt_qposadr[k]];
+    for (int side = -1; side <= 1; side += 2) {
+      double dist = side * (m->jnt_range[2 * k + (side + 1) / 2] - q);
+      if (dist < m->jnt_margin[k]) {
+        memset(J, 0, sizeof(double) * nv);
+        J[m->jnt_dofadr[k]] = -side;
+        add_row(m, d, EFC_LIMIT, k, J, dist, m->jnt_margin[k], m->dof_invweight0[m->jnt_dofadr[k]],
+                m->jnt_solref + 2 * k, m->jnt_solimp + 5 * k);
+      }
+    }
+  }
+  d->nlimit = d->nefc;
+  /* contacts */
+  for (int c = 0; c < d->ncon; c++) {
+    orcContact* con = d->contact + c;
+    con->efc_address = -1;
+    int b1 = m->geom_bodyid[con->geom1], b2 = m->geom_bodyid[con->geom2];
+    jac_point(m, d, b1, con->pos, jp1, NULL);
+    jac_point(m, d, b2, con->pos, jp2, NULL);
+    for (int i = 0; i < 3 * nv; i++) jdif[i] = jp2[i] - jp1[i];
+    double tran = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
+    const double* fr = con->frame;
+    if (con->dim == 1) {
+      for (int i = 0; i < nv; i++) J[i] = fr[0] * jdif[i] + fr[1] * jdif[nv + i] + fr[2] * jdif[2 * nv + i];
+      int r = add_row(m, d, EFC_FRICTIONLESS, c, J, con->dist, con->includemargin, tran,
+                      con->solref, con->solimp);
+      con->efc_address = r;
+    } else {
+      /* pyramidal cone: rows n +/- mu_k t_k (condim 3: two tangent directions) */
+      double* jnp = d->work + 10 * nv;
+      double* jt1 = d->work + 11 * nv;
+      double* jt2 = d->work + 12 * nv;
+      for (int i = 0; i < nv; i++) {
+        jnp[i] = fr[0] * jdif[i] + fr[1] * jdif[nv + i] + fr[2] * jdif[2 * nv + i];
+        jt1[i] = fr[3] * jdif[i] + fr[4] * jdif[nv + i] + fr[5] * jdif[2 * nv + i];
+        jt2[i] = fr[6] * jdif[i] + fr[7] * jdif[nv + i] + fr[8] * jdif[2 * nv + i];
+      }
+      if (con->dim != 3) d->overflow |= 4; /* torsional/rolling rows not supported */
+      int first = -1;
+      for (int k = 0; k < 2; k++) {
+        double mu = con->friction[k];
+        const double* jt = k == 0 ? jt1 : jt2;
+        double diag = tran + mu * mu * tran;
+        for (int s = 0; s < 2; s++) {
+          double sg = s == 0 ? 1.0 : -1.0;
+          for (int i = 0; i < nv; i++) J[i] = jnp[i] + sg * mu * jt[i];
+          int r = add_row(m, d, EFC_PYRAMIDAL, c, J, con->dist, con->includemargin,
+                          diag / m->impratio, con->solref, con->solimp);
+          if (first < 0) first = r;
+        }
+      }
+      con->efc_address = first;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ velocity stage */
+static void com_vel(const mjxModelDesc* m, orcData* d) {
+  memset(d->cvel, 0, 6 * sizeof(double));
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parentid[b];
+    double v[6];
+    memcpy(v, d->cvel + 6 * p, sizeof(v));
+    for (int k = m->body_jntadr[b]; k < m->body_jntadr[b] + m->body_jntnum[b]; k++) {
+      int dof = m->jnt_dofadr[k];
+      if (m->jnt_type[k] == MJX_JNT_FREE) {
+        for (int i = 0; i < 3; i++) {
+          memset(d->cdof_dot + 6 * (dof + i), 0, 6 * sizeof(double));
+          for (int j = 0; j < 6; j++) v[j] += d->cdof[6 * (dof + i) + j] * d->qvel[dof + i];
+        }
+        for (int i = 3; i < 6; i++) cross_motion(d->cdof_dot + 6 * (dof + i), v, d->cdof + 6 * (dof + i));
+        for (int i = 3; i < 6; i++)
+          for (int j = 0; j < 6; j++) v[j] += d->cdof[6 * (dof + i) + j] * d->qvel[dof + i];
+      } else {
+        cross_motion(d->cdof_dot + 6 * dof, v, d->cdof + 6 * dof);
+        for (int j = 0; j < 6; j++) v[j] += d->cdof[6 * dof + j] * d->qvel[dof];
+      }
+    }
+    memcpy(d->cvel + 6 * b, v, sizeof(v));
+  }
+}
+
+/* RNE: qfrc_bias (flg_acc=0), or cacc only (post-constraint, with qacc) */
+static void rne(const mjxModelDesc* m, orcData* d, int with_qacc, double* cacc, double* out_bias) {
+  int nb = m->nbody;
+  double* cfrc = d->work; /* 6*nb */
+  memset(cacc, 0, 6 * sizeof(double));
+  cacc[3] = -m->gravity[0]; cacc[4] = -m->gravity[1]; cacc[5] = -m->gravity[2];
+  for (int b = 1; b < nb; b++) {
+    int p = m->body_parentid[b];
+    double a[6];
+    memcpy(a, cacc + 6 * p, sizeof(a));
+    for (int i = m->body_dofadr[b]; i >= 0 && i < m->body_dofadr[b] + m->body_dofnum[b]; i++) {
+      for (int j = 0; j < 6; j++) {
+        a[j] += d->cdof_dot[6 * i + j] * d->qvel[i];
+        if (with_qacc) a[j] += d->cdof[6 * i + j] * d->qacc[i];
+      }
+    }
+    memcpy(cacc + 6 * b, a, sizeof(a));
+    if (out_bias) {
+      double f1[6], f2[6], iv[6];
+      inert_mul(f1, d->cinert + 10 * b, a);
+      inert_mul(iv, d->cinert + 10 * b, d->cvel + 6 * b);
+      cross_force(f2, d->cvel + 6 * b, iv);
+      for (int j = 0; j < 6; j++) cfrc[6 * b + j] = f1[j] + f2[j];
+    }
+  }
+  if (!out_bias) return;
+  memset(cfrc, 0, 6 * sizeof(double));
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    for (int j = 0; j < 6; j++) cfrc[6 * p + j] += cfrc[6 * b + j];
+  }
+  for (int i = 0; i < m->nv; i++) out_bias[i] = dot6(d->cdof + 6 * i, cfrc + 6 * m->dof_bodyid[i]);
+}
+
+static void passive(const mjxModelDesc* m, orcData* d) {
+  memset(d->qfrc_passive, 0, sizeof(double) * m->nv);
+  for (int k = 0; k < m->njnt; k++) {
+    int t = m->jnt_type[k];
+    if ((t == MJX_JNT_HINGE || t == MJX_JNT_SLIDE) && m->jnt_stiffness[k] != 0) {
+      int a = m->jnt_qposadr[k];
+      d->qfrc_passive[m->jnt_dofadr[k]] -= m->jnt_stiffness[k] * (d->qpos[a] - m->qpos_spring[a]);
+    }
+  }
+  for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] -= m->dof_damping[i] * d->qvel[i];
+}
+
+static void subtree_vel(const mjxModelDesc* m, orcData* d) {
+  int nb = m->nbody;
+  double* vcom = d->work; /* 3*nb: linear velocity at xipos */
+  for (int b = 0; b < nb; b++) {
+    const double* cv = d->cvel + 6 * b;
+    const double* off = d->subtree_com + 3 * m->body_rootid[b];
+    double rel[3], t[3];
+    v3_sub(rel, d->xipos + 3 * b, off);
+    v3_cross(t, cv, rel);
+    v3_add(vcom + 3 * b, cv + 3, t);
+    v3_scl(d->subtree_linvel + 3 * b, vcom + 3 * b, m->body_mass[b]);
+    /* body angular momentum about its own com: R diag(I) R^T w */
+    double wl[3], hl[3];
+    m3_mulTv(wl, d->ximat + 9 * b, cv);
+    for (int i = 0; i < 3; i++) hl[i] = m->body_inertia[3 * b + i] * wl[i];
+    m3_mulv(d->subtree_angmom + 3 * b, d->ximat + 9 * b, hl);
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    v3_add(d->subtree_linvel + 3 * p, d->subtree_linvel + 3 * p, d->subtree_linvel + 3 * b);
+  }
+  for (int b = 0; b < nb; b++) {
+    double sm = m->body_subtreemass[b];
+    if (sm > MINVAL) v3_scl(d->subtree_linvel + 3 * b, d->subtree_linvel + 3 * b, 1.0 / sm);
+    else v3_copy(d->subtree_linvel + 3 * b, vcom + 3 * b);
+  }
+  /* angular momentum about subtree com, accumulated leaf to root */
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    double dx[3], dv[3], dp[3], t[3];
+    v3_sub(dx, d->xipos + 3 * b, d->subtree_com + 3 * b);
+    v3_sub(dv, vcom + 3 * b, d->subtree_linvel + 3 * b);
+    v3_scl(dp, dv, m->body_mass[b]);
+    v3_cross(t, dx, dp);
+    v3_add(d->subtree_angmom + 3 * b, d->subtree_angmom + 3 * b, t);
+    v3_sub(dx, d->subtree_com + 3 * b, d->subtree_com + 3 * p);
+    v3_sub(dv, d->subtree_linvel + 3 * b, d->subtree_linvel + 3 * p);
+    v3_scl(dp, dv, m->body_subtreemass[b]);
+    v3_cross(t, dx, dp);
+    v3_add(d->subtree_angmom + 3 * p, d->subtree_angmom + 3 * p, d->subtree_angmom + 3 * b);
+    v3_add(d->subtree_angmom + 3 * p, d->subtree_angmom + 3 * p, t);
+  }
+}
+
+/* ------------------------------------------------------------------ actuation */
+static void actuation(const mjxModelDesc* m, orcData* d) {
+  memset(d->qfrc_actuator, 0, sizeof(double) * m->nv);
+  for (int u = 0; u < m->nu; u++) {
+    int j = m->actuator_trnid[u];
+    int dof = m->jnt_dofadr[j], a = m->jnt_qposadr[j];
+    double gear = m->actuator_gear[u];
+    double len = gear * d->qpos[a], vel = gear * d->qvel[dof];
+    double ctrl = d->ctrl[u];
+    if (m->actuator_ctrllimited[u]) {
+      ctrl = fmin(fmax(ctrl, m->actuator_ctrlrange[2 * u]), m->actuator_ctrlrange[2 * u + 1]);
+    }
+    const double* bp = m->actuator_biasprm + 3 * u;
+    double f = m->actuator_gainprm[3 * u] * ctrl + bp[0] + bp[1] * len + bp[2] * vel;
+    if (m->actuator_forcelimited[u])
+      f = fmin(fmax(f, m->actuator_forcerange[2 * u]), m->actuator_forcerange[2 * u + 1]);
+    d->actuator_force[u] = f;
+    d->qfrc_actuator[dof] += gear * f;
+  }
+}
+
+static void xfrc_accumulate(const mjxModelDesc* m, orcData* d, double* qfrc) {
+  int nv = m->nv;
+  double* jp = d->work + 20 * nv;
+  double* jr = d->work + 23 * nv;
+  for (int b = 1; b < m->nbody; b++) {
+    const double* f = d->xfrc_applied + 6 * b;
+    if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+    jac_point(m, d, b, d->xipos + 3 * b, jp, jr);
+    for (int i = 0; i < nv; i++)
+      qfrc[i] += jp[i] * f[0] + jp[nv + i] * f[1] + jp[2 * nv + i] * f[2] + jr[i] * f[3] +
+                 jr[nv + i] * f[4] + jr[2 * nv + i] * f[5];
+  }
+}
+
+/* ------------------------------------------------------------------ Newton solver */
+/* cost of qacc `x`: Gauss term + half-quadratic constraint terms; fills jar and force */
+static double eval_cost(const mjxModelDesc* m, orcData* d, const double* x, const double* Mx,
+                        double* jar) {
+  int nv = m->nv;
+  double gauss = 0;
+  for (int i = 0; i < nv; i++) gauss += 0.5 * (x[i] - d->qacc_smooth[i]) * (Mx[i] - d->qfrc_smooth[i]);
+  double c = 0;
+  for (int r = 0; r < d->nefc; r++) {
+    double v = -d->efc_aref[r];
+    const double* J = d->efc_J + (size_t)r * nv;
+    for (int i = 0; i < nv; i++) v += J[i] * x[i];
+    jar[r] = v;
+    if (v < 0) c += 0.5 * d->efc_D[r] * v * v;
+  }
+  return gauss + c;
+}
+
+static void mulM(const mjxModelDesc* m, const orcData* d, double* r, const double* x) {
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++) {
+    double s = 0;
+    for (int j = 0; j < nv; j++) s += d->qM[i * nv + j] * x[j];
+    r[i] = s;
+  }
+}
+
+/* 1-D derivative data along the search line at alpha */
+static void ls_eval(const orcData* d, double g1, double g2, const double* jar, const double* Js,
+                    double alpha, double* der, double* der2) {
+  double f1 = g1 + alpha * g2, f2 = g2;
+  for (int r = 0; r < d->nefc; r++) {
+    double v = jar[r] + alpha * Js[r];
+    if (v < 0) {
+      f1 += d->efc_D[r] * v * Js[r];
+      f2 += d->efc_D[r] * Js[r] * Js[r];
+    }
+  }
+  *der = f1; *der2 = f2;
+}
+
+/* exact line search on the piecewise-quadratic convex cost: safeguarded Newton on the
+ * piecewise-linear derivative with a shrinking bracket [lo, hi]. */
+static double linesearch(const mjxModelDesc* m, const orcData* d, double g1, double g2,
+                         const double* jar, const double* Js, double gtol) {
+  double d0, dd0;
+  ls_eval(d, g1, g2, jar, Js, 0.0, &d0, &dd0);
+  if (d0 >= 0) return 0.0;
+  /* curvature just right of 0: rows with jar==0 and Js<0 become active */
+  double lo = 0, hi = -1, dlo = d0, alpha;
+  double c0 = g2;
+  for (int r = 0; r < d->nefc; r++)
+    if (jar[r] < 0 || (jar[r] == 0 && Js[r] < 0)) c0 += d->efc_D[r] * Js[r] * Js[r];
+  alpha = -d0 / c0;
+  double best = 0;
+  for (int it = 0; it < m->ls_iterations; it++) {
+    double der, der2;
+    ls_eval(d, g1, g2, jar, Js, alpha, &der, &der2);
+    if (fabs(der) <= gtol) return alpha;
+    if (der < 0) { lo = alpha; dlo = der; best = alpha; }
+    else { hi = alpha; }
+    double next = der2 > 0 ? alpha - der / der2 : alpha * 2;
+    if (hi >= 0 && !(next > lo && next < hi)) next = 0.5 * (lo + hi);
+    if (hi < 0 && next <= lo) next = lo + (lo > 0 ? lo : 1.0);
+    alpha = next;
+  }
+  (void)dlo;
+  /* out of iterations: the point with negative derivative closest to the root */
+  return best > 0 ? best : alpha;
+}
+
+static void solve_newton(const mjxModelDesc* m, orcData* d) {
+  int nv = m->nv, nefc = d->nefc;
+  double* w = d->work;
+  double* x = w;              w += nv;
+  double* Mx = w;             w += nv;
+  double* grad = w;           w += nv;
+  double* srch = w;           w += nv;
+  double* Ms = w;             w += nv;
+  double* H = w;              w += nv * nv;
+  double* jar = w;            w += nefc > 0 ? nefc : 1;
+  double* Js = w;             w += nefc > 0 ? nefc : 1;
+  double* xs = w;             w += nv;
+
+  d->niter = 0;
+  if (nefc == 0) {
+    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+    return;
+  }
+  /* warmstart: pick qacc_warmstart if its total cost beats qacc_smooth */
+  memcpy(x, d->qacc_warmstart, sizeof(double) * nv);
+  mulM(m, d, Mx, x);
+  double cost_ws = eval_cost(m, d, x, Mx, jar);
+  memcpy(xs, d->qacc_smooth, sizeof(double) * nv);
+  double* Mxs = Ms;
+  memcpy(Mxs, d->qfrc_smooth, sizeof(double) * nv);
+  double cost_sm = eval_cost(m, d, xs, Mxs, jar);
+  if (cost_sm < cost_ws) {
+    memcpy(x, xs, sizeof(double) * nv);
+    memcpy(Mx, d->qfrc_smooth, sizeof(double) * nv);
+  }
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  double cost = eval_cost(m, d, x, Mx, jar);
+  for (int iter = 0; iter < m->iterations; iter++) {
+    /* gradient and Hessian at x */
+    for (int i = 0; i < nv; i++) grad[i] = Mx[i] - d->qfrc_smooth[i];
+    memcpy(H, d->qM, sizeof(double) * nv * nv);
+    for (int r = 0; r < nefc; r++) {
+      if (jar[r] >= 0) continue;
+      const double* J = d->efc_J + (size_t)r * nv;
+      double Dr = d->efc_D[r];
+      for (int i = 0; i < nv; i++) {
+        if (J[i] == 0) continue;
+        grad[i] += J[i] * Dr * jar[r];
+        for (int j = 0; j <= i; j++) H[i * nv + j] += J[i] * Dr * J[j];
+      }
+    }
+    for (int i = 0; i < nv; i++)
+      for (int j = i + 1; j < nv; j++) H[i * nv + j] = H[j * nv + i];
+    double gnorm = 0;
+    for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
+    gnorm = sqrt(gnorm);
+    if (iter > 0 && scale * gnorm < m->tolerance) break;
+    chol(H, nv);
+    for (int i = 0; i < nv; i++) srch[i] = -grad[i];
+    chol_solve(H, nv, srch);
+    /* line search */
+    mulM(m, d, Ms, srch);
+    double g1 = 0, g2 = 0, snorm = 0;
+    for (int i = 0; i < nv; i++) {
+      g1 += srch[i] * (Mx[i] - d->qfrc_smooth[i]);
+      g2 += srch[i] * Ms[i];
+      snorm += srch[i] * srch[i];
+    }
+    snorm = sqrt(snorm);
+    for (int r = 0; r < nefc; r++) {
+      const double* J = d->efc_J + (size_t)r * nv;
+      double s = 0;
+      for (int i = 0; i < nv; i++) s += J[i] * srch[i];
+      Js[r] = s;
+    }
+    double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
+    double alpha = linesearch(m, d, g1, g2, jar, Js, gtol);
+    d->niter = iter + 1;
+    if (alpha == 0) break;
+    for (int i = 0; i < nv; i++) { x[i] += alpha * srch[i]; Mx[i] += alpha * Ms[i]; }
+    double old = cost;
+    cost = eval_cost(m, d, x, Mx, jar);
+    if (scale * (old - cost) < m->tolerance) break;
+  }
+  memcpy(d->qacc, x, sizeof(double) * nv);
+  /* constraint forces */
+  memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+  for (int r = 0; r < nefc; r++) {
+    const double* J = d->efc_J + (size_t)r * nv;
+    double v = -d->efc_aref[r];
+    for (int i = 0; i < nv; i++) v += J[i] * x[i];
+    d->efc_force[r] = v < 0 ? -d->efc_D[r] * v : 0;
+    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += J[i] * d->efc_force[r];
+  }
+}
+
+/* ------------------------------------------------------------------ sensors */
+static void contact_force(const orcData* d, const orcContact* c, double* f /* 6 */) {
+  memset(f, 0, 6 * sizeof(double));
+  if (c->efc_address < 0) return;
+  const double* ef = d->efc_force + c->efc_address;
+  if (c->dim == 1) { f[0] = ef[0]; return; }
+  for (int k = 0; k < 2 * (c->dim - 1); k++) f[0] += ef[k];
+  for (int k = 0; k < c->dim - 1; k++) f[1 + k] = (ef[2 * k] - ef[2 * k + 1]) * c->friction[k];
+}
+
+static int in_mask(const uint32_t* mk, int g) { return (mk[g >> 5] >> (g & 31)) & 1u; }
+
+static void sensors(const mjxModelDesc* m, orcData* d) {
+  for (int s = 0; s < m->nsensor; s++) {
+    double* out = d->sensordata + m->sensor_adr[s];
+    int obj = m->sensor_objid[s];
+    switch (m->sensor_type[s]) {
+      case MJX_SENS_GYRO: {
+        int b = m->site_bodyid[obj];
+        m3_mulTv(out, d->site_xmat + 9 * obj, d->cvel + 6 * b);
+      } break;
+      case MJX_SENS_VELOCIMETER: {
+        int b = m->site_bodyid[obj];
+        double rel[3], t[3], v[3];
+        v3_sub(rel, d->site_xpos + 3 * obj, d->subtree_com + 3 * m->body_rootid[b]);
+        v3_cross(t, d->cvel + 6 * b, rel);
+        v3_add(v, d->cvel + 6 * b + 3, t);
+        m3_mulTv(out, d->site_xmat + 9 * obj, v);
+      } break;
+      case MJX_SENS_ACCELEROMETER: {
+        int b = m->site_bodyid[obj];
+        const double* cv = d->cvel + 6 * b;
+        const double* ca = d->cacc + 6 * b;
+        double rel[3], t[3], v[3], a[3];
+        v3_sub(rel, d->site_xpos + 3 * obj, d->subtree_com + 3 * m->body_rootid[b]);
+        v3_cross(t, cv, rel); v3_add(v, cv + 3, t);
+        v3_cross(t, ca, rel); v3_add(a, ca + 3, t);
+        v3_cross(t, cv, v); v3_add(a, a, t);
+        m3_mulTv(out, d->site_xmat + 9 * obj, a);
+      } break;
+      case MJX_SENS_SUBTREEANGMOM:
+        v3_copy(out, d->subtree_angmom + 3 * obj);
+        break;
+      case MJX_SENS_FRAMEPOS:
+        if (m->sensor_objtype[s] == MJX_OBJ_SITE) v3_copy(out, d->site_xpos + 3 * obj);
+        else v3_copy(out, d->xpos + 3 * obj);
+        break;
+      case MJX_SENS_JOINTPOS: out[0] = d->qpos[m->jnt_qposadr[obj]]; break;
+      case MJX_SENS_JOINTVEL: out[0] = d->qvel[m->jnt_dofadr[obj]]; break;
+      case MJX_SENS_CONTACT: {
+        const int* ip = m->sensor_intprm + 3 * s;
+        int bits = ip[0], reduce = ip[1], nslot = ip[2];
+        const uint32_t* mk1 = m->sensor_geommask1 + MJX_MASK_WORDS * s;
+        const uint32_t* mk2 = m->sensor_geommask2 + MJX_MASK_WORDS * s;
+        int fdim = (bits & 1) || (bits & 8) ? 1 : 3;
+        memset(out, 0, sizeof(double) * m->sensor_dim[s]);
+        int found = 0;
+        double net[3] = {0, 0, 0};
+        /* slot selection for none/mindist/maxforce */
+        int sel[16]; double key[16]; int nsel = 0;
+        for (int c = 0; c < d->ncon; c++) {
+          const orcContact* con = d->contact + c;
+          int a1 = in_mask(mk1, con->geom1) && in_mask(mk2, con->geom2);
+          int a2 = in_mask(mk1, con->geom2) && in_mask(mk2, con->geom1);
+          if (!a1 && !a2) continue;
+          found++;
+          double sg = a1 ? 1.0 : -1.0;
+          double f[6], fg[3];
+          contact_force(d, con, f);
+          m3_mulTv(fg, con->frame, f);
+          for (int i = 0; i < 3; i++) net[i] += sg * fg[i];
+          double k = reduce == MJX_REDUCE_MINDIST ? con->dist
+                   : reduce == MJX_REDUCE_MAXFORCE ? -v3_norm(f) : (double)nsel;
+          /* insertion into top-nslot by key (ascending) */
+          if (nsel < nslot || k < key[nsel - 1]) {
+            int pos = nsel < nslot ? nsel++ : nslot - 1;
+            while (pos > 0 && key[pos - 1] > k) { key[pos] = key[pos - 1]; sel[pos] = sel[pos - 1]; pos--; }
+            key[pos] = k; sel[pos] = c * 2 + (a1 ? 0 : 1);
+          }
+        }
+        if (reduce == MJX_REDUCE_NETFORCE) {
+          if (bits & 1) out[0] = found;
+          else if (bits & 2) v3_copy(out, net);
+          break;
+        }
+        for (int k = 0; k < nsel; k++) {
+          const orcContact* con = d->contact + (sel[k] >> 1);
+          double sg = (sel[k] & 1) ? -1.0 : 1.0;
+          double* o = out + k * fdim;
+          double f[6];
+          contact_force(d, con, f);
+          if (bits & 1) o[0] = found;
+          else if (bits & 2) v3_copy(o, f);
+          else if (bits & 4) v3_copy(o, f + 3);
+          else if (bits & 8) o[0] = con->dist;
+          else if (bits & 16) v3_copy(o, con->pos);
+          else if (bits & 32) v3_scl(o, con->frame, sg);
+          else if (bits & 64) v3_scl(o, con->frame + 3, sg);
+        }
+        if ((bits & 1) && nsel == 0) out[0] = 0;
+      } break;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ pipeline */
+void orc_forward(const mjxModelDesc* m, orcData* d) {
+  int nv = m->nv;
+  d->overflow = 0;
+  kinematics(m, d);
+  com_pos(m, d);
+  crb(m, d);
+  collision(m, d);
+  make_constraint(m, d);
+  com_vel(m, d);
+  passive(m, d);
+  rne(m, d, 0, d->cacc, d->qfrc_bias);
+  subtree_vel(m, d);
+  actuation(m, d);
+  for (int i = 0; i < nv; i++)
+    d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_applied[i] + d->qfrc_actuator[i];
+  xfrc_accumulate(m, d, d->qfrc_smooth);
+  /* qacc_smooth = M^-1 qfrc_smooth */
+  double* Lm = (double*)malloc(sizeof(double) * nv * nv);
+  memcpy(Lm, d->qM, sizeof(double) * nv * nv);
+  chol(Lm, nv);
+  memcpy(d->qacc_smooth, d->qfrc_smooth, sizeof(double) * nv);
+  chol_solve(Lm, nv, d->qacc_smooth);
+  free(Lm);
+  solve_newton(m, d);
+  rne(m, d, 1, d->cacc, NULL);
+  sensors(m, d);
+}
+
+void orc_step(const mjxModelDesc* m, orcData* d) {
+  int nv = m->nv;
+  orc_forward(m, d);
+  double h = m->timestep;
+  double* A = (double*)malloc(sizeof(double) * (nv * nv + nv));
+  double* f = A + nv * nv;
+  memcpy(A, d->qM, sizeof(double) * nv * nv);
+  int need = 0;
+  if (m->integrator == MJX_INT_IMPLICITFAST) {
+    for (int i = 0; i < nv; i++) if (m->dof_damping[i] > 0) { A[i * nv + i] += h * m->dof_damping[i]; need = 1; }
+    for (int u = 0; u < m->nu; u++) {
+      if (m->actuator_forcelimited[u]) {
+        double fo = d->actuator_force[u];
+        if (fo <= m->actuator_forcerange[2 * u] || fo >= m->actuator_forcerange[2 * u + 1]) continue;
+      }
+      double bv = m->actuator_biasprm[3 * u + 2];
+      if (bv == 0) continue;
+      int dof = m->jnt_dofadr[m->actuator_trnid[u]];
+      double g = m->actuator_gear[u];
+      A[dof * nv + dof] -= h * g * g * bv;
+      need = 1;
+    }
+  } else {
+    for (int i = 0; i < nv; i++) if (m->dof_damping[i] > 0) { A[i * nv + i] += h * m->dof_damping[i]; need = 1; }
+  }
+  double* qacc_int = d->qacc;
+  double* tmp = NULL;
+  if (need) {
+    for (int i = 0; i < nv; i++) f[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
+    chol(A, nv);
+    chol_solve(A, nv, f);
+    tmp = f;
+    qacc_int = tmp;
+  }
+  for (int i = 0; i < nv; i++) d->qvel[i] += h * qacc_int[i];
+  /* integrate positions */
+  for (int k = 0; k < m->njnt; k++) {
+    int a = m->jnt_qposadr[k], dof = m->jnt_dofadr[k];
+    switch (m->jnt_type[k]) {
+      case MJX_JNT_FREE: {
+        for (int i = 0; i < 3; i++) d->qpos[a + i] += h * d->qvel[dof + i];
+        double* q = d->qpos + a + 3;
+        double w[3] = {d->qvel[dof + 3], d->qvel[dof + 4], d->qvel[dof + 5]};
+        double ang = h * v3_normalize(w), qr[4];
+        q_axisangle(qr, w, ang);
+        q_normalize(q);
+        q_mul(q, q, qr);
+      } break;
+      case MJX_JNT_HINGE:
+      case MJX_JNT_SLIDE:
+        d->qpos[a] += h * d->qvel[dof];
+        break;
+    }
+  }
+  d->time += h;
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * nv);
+  free(A);
+}
+
+/* ------------------------------------------------------------------ batch helpers */
+int orc_rollout(const mjxModelDesc* m, int nworld, int nstep, int nconmax, int njmax,
+                double* qpos, double* qvel, double* qacc_warmstart, double* ctrl,
+                double* time, double* qacc_out, double* sensordata_out, double* xpos_out,
+                double* cvel_out, double* subtree_com_out, double* actuator_force_out,
+                int* ncon_out, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+  {
+    orcData* d = orc_data_new(m, nconmax, njmax);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+    for (int w = 0; w < nworld; w++) {
+      memcpy(d->qpos, qpos + (size_t)w * m->nq, sizeof(double) * m->nq);
+      memcpy(d->qvel, qvel + (size_t)w * m->nv, sizeof(double) * m->nv);
+      memcpy(d->qacc_warmstart, qacc_warmstart + (size_t)w * m->nv, sizeof(double) * m->nv);
+      memcpy(d->ctrl, ctrl + (size_t)w * m->nu, sizeof(double) * m->nu);
+      memset(d->xfrc_applied, 0, sizeof(double) * 6 * m->nbody);
+      memset(d->qfrc_applied, 0, sizeof(double) * m->nv);
+      d->time = time[w];
+      for (int s = 0; s < nstep; s++) orc_step(m, d);
+      memcpy(qpos + (size_t)w * m->nq, d->qpos, sizeof(double) * m->nq);
+      memcpy(qvel + (size_t)w * m->nv, d->qvel, sizeof(double) * m->nv);
+      memcpy(qacc_warmstart + (size_t)w * m->nv, d->qacc_warmstart, sizeof(double) * m->nv);
+      time[w] = d->time;
+      if (qacc_out) memcpy(qacc_out + (size_t)w * m->nv, d->qacc, sizeof(double) * m->nv);
+      if (sensordata_out)
+        memcpy(sensordata_out + (size_t)w * m->nsensordata, d->sensordata, sizeof(double) * m->nsensordata);
+      if (xpos_out) memcpy(xpos_out + (size_t)w * 3 * m->nbody, d->xpos, sizeof(double) * 3 * m->nbody);
+      if (cvel_out) memcpy(cvel_out + (size_t)w * 6 * m->nbody, d->cvel, sizeof(double) * 6 * m->nbody);
+      if (subtree_com_out)
+        memcpy(subtree_com_out + (size_t)w * 3 * m->nbody, d->subtree_com, sizeof(double) * 3 * m->nbody);
+      if (actuator_force_out)
+        memcpy(actuator_force_out + (size_t)w * m->nu, d->actuator_force, sizeof(double) * m->nu);
+      if (ncon_out) ncon_out[w] = d->ncon;
+    }
+    orc_data_free(d);
+  }
+  return 0;
+}
+
+int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                     const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                     double time, int do_step, double* out_qpos, double* out_qvel,
+                     double* out_qacc, double* out_qacc_smooth, double* out_sensordata,
+                     double* out_xpos, double* out_xquat, double* out_cvel,
+                     double* out_subtree_com, double* out_qfrc_bias, double* out_qM,
+                     double* out_actuator_force, double* out_cacc, int* out_ncon,
+                     int* out_nefc, double* out_contact, double* out_efc_force, int* out_niter) {
+  orcData* d = orc_data_new(m, nconmax, njmax);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_warmstart, sizeof(double) * m->nv);
+  memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+  d->time = time;
+  if (do_step) orc_step(m, d); else orc_forward(m, d);
+  int nv = m->nv, nb = m->nbody;
+  if (out_qpos) memcpy(out_qpos, d->qpos, sizeof(double) * m->nq);
+  if (out_qvel) memcpy(out_qvel, d->qvel, sizeof(double) * nv);
+  if (out_qacc) memcpy(out_qacc, d->qacc, sizeof(double) * nv);
+  if (out_qacc_smooth) memcpy(out_qacc_smooth, d->qacc_smooth, sizeof(double) * nv);
+  if (out_sensordata) memcpy(out_sensordata, d->sensordata, sizeof(double) * m->nsensordata);
+  if (out_xpos) memcpy(out_xpos, d->xpos, sizeof(double) * 3 * nb);
+  if (out_xquat) memcpy(out_xquat, d->xquat, sizeof(double) * 4 * nb);
+  if (out_cvel) memcpy(out_cvel, d->cvel, sizeof(double) * 6 * nb);
+  if (out_subtree_com) memcpy(out_subtree_com, d->subtree_com, sizeof(double) * 3 * nb);
+  if (out_qfrc_bias) memcpy(out_qfrc_bias, d->qfrc_bias, sizeof(double) * nv);
+  if (out_qM) memcpy(out_qM, d->qM, sizeof(double) * nv * nv);
+  if (out_actuator_force) memcpy(out_actuator_force, d->actuator_force, sizeof(double) * m->nu);
+  if (out_cacc) memcpy(out_cacc, d->cacc, sizeof(double) * 6 * nb);
+  if (out_ncon) *out_ncon = d->ncon;
+  if (out_nefc) *out_nefc = d->nefc;
+  if (out_contact)
+    for (int c = 0; c < d->ncon; c++) {
+      double* o = out_contact + 9 * c;
+      o[0] = d->contact[c].geom1; o[1] = d->contact[c].geom2; o[2] = d->contact[c].dist;
+      v3_copy(o + 3, d->contact[c].pos); v3_copy(o + 6, d->contact[c].frame);
+    }
+  if (out_efc_force) memcpy(out_efc_force, d->efc_force, sizeof(double) * d->nefc);
+  if (out_niter) *out_niter = d->niter;
+  int ov = d->overflow;
+  orc_data_free(d);
+  return ov;
+}
+
+size_t orc_model_desc_size(void) { return sizeof(mjxModelDesc); }

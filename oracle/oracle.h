@@ -1,0 +1,86 @@
+/* oracle.h — CPU (fp64) restatement of the mj_step pipeline subset on the hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the reported CPU
+ * baseline.  The product path (mjlab-1_amd) never links or calls it.
+ *
+ * Parity status: the reference's physics lives in un-vendored mujoco_warp (git
+ * f2f7957) / MuJoCo 3.4.1.dev and neither is importable here,
+ * so this restatement is pinned by (a) the reference's own known-answer tests
+ * (tests/test_spec_utils.py:26-102 actuator law, tests/test_sim.py:89-110 reset,
+ * tests/test_entity_data.py:44-158 velocity round trips) re-expressed in tests/,
+ * and (b) analytic answers (free fall, pendulum, box-on-plane m*g).  Trajectory
+ * parity with MuJoCo-C itself is UNPINNED (no MuJoCo in the container).
+ */
+#ifndef MJX_ORACLE_H_
+#define MJX_ORACLE_H_
+
+#include "../include/mjx355.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int geom1, geom2, dim;
+  double dist, includemargin;
+  double pos[3], frame[9];
+  double friction[5], solref[2], solimp[5];
+  int efc_address;
+} orcContact;
+
+typedef struct {
+  int nconmax, njmax;
+  /* state (in) */
+  double time;
+  double *qpos, *qvel, *qacc_warmstart, *ctrl, *qfrc_applied, *xfrc_applied;
+  /* position stage */
+  double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis;
+  double *geom_xpos, *geom_xmat, *site_xpos, *site_xmat;
+  double *subtree_com, *cinert, *cdof, *crb, *qM;
+  /* velocity stage */
+  double *cvel, *cdof_dot, *qfrc_bias, *qfrc_passive, *subtree_linvel, *subtree_angmom;
+  /* actuation / acceleration */
+  double *actuator_force, *qfrc_actuator, *qfrc_smooth, *qacc_smooth;
+  double *qacc, *qfrc_constraint, *cacc, *sensordata;
+  /* contacts + constraints */
+  int ncon, nefc, niter, nlimit;
+  orcContact* contact;
+  int *efc_type, *efc_id;
+  double *efc_J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_vel, *efc_force,
+      *efc_diagApprox, *efc_frame_mu;
+  int overflow; /* bit0: contacts dropped, bit1: rows dropped, bit2: unsupported pair */
+  /* scratch */
+  double* work;
+} orcData;
+
+orcData* orc_data_new(const mjxModelDesc* m, int nconmax, int njmax);
+void orc_data_free(orcData* d);
+void orc_reset(const mjxModelDesc* m, orcData* d);      /* mj_resetData */
+void orc_forward(const mjxModelDesc* m, orcData* d);    /* mj_forward */
+void orc_step(const mjxModelDesc* m, orcData* d);       /* mj_step (implicitfast/euler) */
+
+/* Batched helpers for the Python tests / CPU baseline: worlds are independent; the
+ * state arrays are [nworld][n] contiguous.  Runs `nstep` steps per world, copying the
+ * selected outputs back.  nthreads<=0: all cores (OpenMP). */
+int orc_rollout(const mjxModelDesc* m, int nworld, int nstep, int nconmax, int njmax,
+                double* qpos, double* qvel, double* qacc_warmstart, double* ctrl,
+                double* time, double* qacc_out, double* sensordata_out,
+                double* xpos_out, double* cvel_out, double* subtree_com_out,
+                double* actuator_force_out, int* ncon_out, int nthreads);
+
+/* Single-world full data dump for parity tests (all pointers may be NULL). */
+int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                     const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                     double time, int do_step, double* out_qpos, double* out_qvel,
+                     double* out_qacc, double* out_qacc_smooth, double* out_sensordata,
+                     double* out_xpos, double* out_xquat, double* out_cvel,
+                     double* out_subtree_com, double* out_qfrc_bias, double* out_qM,
+                     double* out_actuator_force, double* out_cacc, int* out_ncon,
+                     int* out_nefc, double* out_contact /* ncon*(2+1+3+3) */,
+                     double* out_efc_force, int* out_niter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
