@@ -1,0 +1,396 @@
+"""ManagerBasedRlEnv, task configs and the task registry.
+
+`ManagerBasedRlEnv.step()` / `reset()` follow `src/mjlab/envs/manager_based_rl_env.py:
+254-416` step for step (decimation loop, counters, terminations, rewards, resets with
+write_data_to_sim + forward, commands, interval events, observations).  Task factories
+restate `tasks/velocity/velocity_env_cfg.py:33-354` and
+`tasks/velocity/config/{g1,go1}/env_cfgs.py`.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+import torch
+
+from . import asset_zoo as az
+from . import mdp
+from .managers import (ActionManager, CommandManager, CurriculumManager, CurriculumTermCfg,
+                       EventManager, EventTermCfg, NullCommandManager, NullCurriculumManager,
+                       ObservationGroupCfg, ObservationManager, ObservationTermCfg,
+                       RewardManager, RewardTermCfg, SceneEntityCfg, TerminationManager,
+                       TerminationTermCfg, UniformNoiseCfg)
+from .scene import Scene
+from .scenes import load_scene
+from .sim import MujocoCfg, Simulation, SimulationCfg
+
+
+@dataclass
+class SceneCfg:
+  scene_name: str = "g1_velocity"
+  num_envs: int = 1
+  env_spacing: float = 2.0
+  entities: dict = field(default_factory=lambda: {"robot": {"soft_joint_pos_limit_factor": 0.9}})
+  contact_sensors: dict = field(default_factory=dict)
+
+
+@dataclass(kw_only=True)
+class ManagerBasedRlEnvCfg:
+  decimation: int
+  scene: SceneCfg
+  observations: dict[str, ObservationGroupCfg] = field(default_factory=dict)
+  actions: dict = field(default_factory=dict)
+  events: dict = field(default_factory=dict)
+  seed: int | None = None
+  sim: SimulationCfg = field(default_factory=SimulationCfg)
+  rewards: dict = field(default_factory=dict)
+  terminations: dict = field(default_factory=dict)
+  commands: dict | None = None
+  curriculum: dict | None = None
+  episode_length_s: float = 0.0
+  is_finite_horizon: bool = False
+
+
+def seed_rng(seed: int) -> None:
+  import random
+  random.seed(seed)
+  np.random.seed(seed)
+  torch.manual_seed(seed)
+
+
+class ManagerBasedRlEnv:
+  """Manager-based RL environment on the MI355X engine."""
+
+  is_vector_env = True
+
+  def __init__(self, cfg: ManagerBasedRlEnvCfg, device: str, render_mode: str | None = None,
+               **kwargs):
+    self.cfg = cfg
+    if cfg.seed is not None:
+      self.cfg.seed = self.seed(cfg.seed)
+    self._sim_step_counter = 0
+    self.extras: dict[str, Any] = {}
+    self.obs_buf = {}
+    model = load_scene(cfg.scene.scene_name)
+    self.scene = Scene(model, cfg.scene.num_envs, device, cfg.scene.entities,
+                       cfg.scene.contact_sensors, cfg.scene.env_spacing)
+    self.sim = Simulation(num_envs=cfg.scene.num_envs, cfg=cfg.sim, model=model, device=device)
+    self.scene.initialize(self.sim.mj_model, self.sim.model, self.sim.data)
+    self.common_step_counter = 0
+    self.episode_length_buf = torch.zeros(cfg.scene.num_envs, device=device, dtype=torch.long)
+    self.render_mode = render_mode
+    self.load_managers()
+
+  @property
+  def num_envs(self) -> int:
+    return self.scene.num_envs
+
+  @property
+  def physics_dt(self) -> float:
+    return self.cfg.sim.mujoco.timestep
+
+  @property
+  def step_dt(self) -> float:
+    return self.cfg.sim.mujoco.timestep * self.cfg.decimation
+
+  @property
+  def device(self) -> str:
+    return self.sim.device
+
+  @property
+  def max_episode_length_s(self) -> float:
+    return self.cfg.episode_length_s
+
+  @property
+  def max_episode_length(self) -> int:
+    return math.ceil(self.max_episode_length_s / self.step_dt)
+
+  @property
+  def unwrapped(self):
+    return self
+
+  def load_managers(self) -> None:
+    self.extras["log"] = {}
+    self.event_manager = EventManager(self.cfg.events, self)
+    self.sim.expand_model_fields(self.event_manager.domain_randomization_fields)
+    self.command_manager = (CommandManager(self.cfg.commands, self) if self.cfg.commands
+                            else NullCommandManager())
+    self.action_manager = ActionManager(self.cfg.actions, self)
+    self.observation_manager = ObservationManager(self.cfg.observations, self)
+    self.termination_manager = TerminationManager(self.cfg.terminations, self)
+    self.reward_manager = RewardManager(self.cfg.rewards, self)
+    self.curriculum_manager = (CurriculumManager(self.cfg.curriculum, self) if self.cfg.curriculum
+                               else NullCurriculumManager())
+    self._configure_spaces()
+    if "startup" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="startup")
+
+  def _configure_spaces(self):
+    self.single_action_dim = sum(self.action_manager.action_term_dim)
+    self.observation_dims = dict(self.observation_manager.group_obs_dim)
+
+  @staticmethod
+  def seed(seed: int = -1) -> int:
+    if seed == -1:
+      seed = np.random.randint(0, 10_000)
+    seed_rng(seed)
+    return seed
+
+  def reset(self, *, seed: int | None = None, env_ids: torch.Tensor | None = None,
+            options: dict | None = None):
+    if env_ids is None:
+      env_ids = torch.arange(self.num_envs, dtype=torch.int64, device=self.device)
+    if seed is not None:
+      self.seed(seed)
+    self._reset_idx(env_ids)
+    self.scene.write_data_to_sim()
+    self.sim.forward()
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    return self.obs_buf, self.extras
+
+  def step(self, action: torch.Tensor):
+    self.action_manager.process_action(action.to(self.device))
+    for _ in range(self.cfg.decimation):
+      self._sim_step_counter += 1
+      self.action_manager.apply_action()
+      self.scene.write_data_to_sim()
+      self.sim.step()
+      self.scene.update(dt=self.physics_dt)
+    self.episode_length_buf += 1
+    self.common_step_counter += 1
+    self.reset_buf = self.termination_manager.compute()
+    self.reset_terminated = self.termination_manager.terminated
+    self.reset_time_outs = self.termination_manager.time_outs
+    self.reward_buf = self.reward_manager.compute(dt=self.step_dt)
+    reset_env_ids = self.reset_buf.nonzero(as_tuple=False).squeeze(-1)
+    if len(reset_env_ids) > 0:
+      self._reset_idx(reset_env_ids)
+      self.scene.write_data_to_sim()
+      self.sim.forward()
+    self.command_manager.compute(dt=self.step_dt)
+    if "interval" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="interval", dt=self.step_dt)
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    return self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
+
+  def _reset_idx(self, env_ids: torch.Tensor) -> None:
+    self.curriculum_manager.compute(env_ids=env_ids)
+    self.sim.reset(env_ids)
+    self.scene.reset(env_ids)
+    if "reset" in self.event_manager.available_modes:
+      self.event_manager.apply(mode="reset", env_ids=env_ids,
+                               global_env_step_count=self._sim_step_counter // self.cfg.decimation)
+    self.extras["log"] = {}
+    for mgr in (self.observation_manager, self.action_manager, self.reward_manager,
+                self.curriculum_manager, self.command_manager, self.event_manager,
+                self.termination_manager):
+      self.extras["log"].update(mgr.reset(env_ids))
+    self.episode_length_buf[env_ids] = 0
+
+  def packed_episode_stats(self) -> torch.Tensor:
+    """Episode statistics of the last reset, packed into one fp32 vector (for the
+    cross-rank all-gather)."""
+    vals = []
+    for v in self.extras.get("log", {}).values():
+      vals.append(torch.as_tensor(v, dtype=torch.float32, device=self.device).reshape(-1)[:1])
+    if not vals:
+      return torch.zeros(1, device=self.device)
+    return torch.cat(vals)
+
+  def close(self) -> None:
+    pass
+
+
+# =========================================================================== task configs
+def make_velocity_env_cfg(scene_name: str) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/velocity_env_cfg.py:33-354` (flat terrain variant)."""
+  policy = {
+    "base_lin_vel": ObservationTermCfg(func=mdp.builtin_sensor, params={"sensor_name": "robot/imu_lin_vel"},
+                                       noise=UniformNoiseCfg(n_min=-0.5, n_max=0.5)),
+    "base_ang_vel": ObservationTermCfg(func=mdp.builtin_sensor, params={"sensor_name": "robot/imu_ang_vel"},
+                                       noise=UniformNoiseCfg(n_min=-0.2, n_max=0.2)),
+    "projected_gravity": ObservationTermCfg(func=mdp.projected_gravity,
+                                            noise=UniformNoiseCfg(n_min=-0.05, n_max=0.05)),
+    "joint_pos": ObservationTermCfg(func=mdp.joint_pos_rel, noise=UniformNoiseCfg(n_min=-0.01, n_max=0.01)),
+    "joint_vel": ObservationTermCfg(func=mdp.joint_vel_rel, noise=UniformNoiseCfg(n_min=-1.5, n_max=1.5)),
+    "actions": ObservationTermCfg(func=mdp.last_action),
+    "command": ObservationTermCfg(func=mdp.generated_commands, params={"command_name": "twist"}),
+  }
+  import copy
+  critic = {k: copy.deepcopy(v) for k, v in policy.items()}
+  critic.update({
+    "foot_height": ObservationTermCfg(func=mdp.foot_height, params={"asset_cfg": SceneEntityCfg("robot", site_names=())}),
+    "foot_air_time": ObservationTermCfg(func=mdp.foot_air_time, params={"sensor_name": "feet_ground_contact"}),
+    "foot_contact": ObservationTermCfg(func=mdp.foot_contact, params={"sensor_name": "feet_ground_contact"}),
+    "foot_contact_forces": ObservationTermCfg(func=mdp.foot_contact_forces, params={"sensor_name": "feet_ground_contact"}),
+  })
+  observations = {
+    "policy": ObservationGroupCfg(terms=policy, concatenate_terms=True, enable_corruption=True),
+    "critic": ObservationGroupCfg(terms=critic, concatenate_terms=True, enable_corruption=False),
+  }
+  actions = {"joint_pos": mdp.JointPositionActionCfg(asset_name="robot", actuator_names=(".*",),
+                                                    scale=0.5, use_default_offset=True)}
+  commands = {"twist": mdp.UniformVelocityCommandCfg(
+    asset_name="robot", resampling_time_range=(3.0, 8.0), rel_standing_envs=0.1,
+    rel_heading_envs=0.3, heading_command=True, heading_control_stiffness=0.5,
+    ranges=mdp.UniformVelocityCommandCfg.Ranges(lin_vel_x=(-1.0, 1.0), lin_vel_y=(-1.0, 1.0),
+                                                ang_vel_z=(-0.5, 0.5), heading=(-math.pi, math.pi)))}
+  events = {
+    "reset_base": EventTermCfg(func=mdp.reset_root_state_uniform, mode="reset", params={
+      "pose_range": {"x": (-0.5, 0.5), "y": (-0.5, 0.5), "yaw": (-3.14, 3.14)}, "velocity_range": {}}),
+    "reset_robot_joints": EventTermCfg(func=mdp.reset_joints_by_offset, mode="reset", params={
+      "position_range": (0.0, 0.0), "velocity_range": (0.0, 0.0),
+      "asset_cfg": SceneEntityCfg("robot", joint_names=(".*",))}),
+    "push_robot": EventTermCfg(func=mdp.push_by_setting_velocity, mode="interval",
+                               interval_range_s=(1.0, 3.0),
+                               params={"velocity_range": {"x": (-0.5, 0.5), "y": (-0.5, 0.5)}}),
+    "foot_friction": EventTermCfg(mode="startup", func=mdp.randomize_field, domain_randomization=True,
+                                  params={"asset_cfg": SceneEntityCfg("robot", geom_names=()),
+                                          "operation": "abs", "field": "geom_friction",
+                                          "ranges": (0.3, 1.2)}),
+  }
+  rewards = {
+    "track_linear_velocity": RewardTermCfg(func=mdp.track_linear_velocity, weight=2.0,
+                                           params={"command_name": "twist", "std": math.sqrt(0.25)}),
+    "track_angular_velocity": RewardTermCfg(func=mdp.track_angular_velocity, weight=2.0,
+                                            params={"command_name": "twist", "std": math.sqrt(0.5)}),
+    "upright": RewardTermCfg(func=mdp.flat_orientation, weight=1.0,
+                             params={"std": math.sqrt(0.2), "asset_cfg": SceneEntityCfg("robot", body_names=())}),
+    "pose": RewardTermCfg(func=mdp.variable_posture, weight=1.0, params={
+      "asset_cfg": SceneEntityCfg("robot", joint_names=(".*",)), "command_name": "twist",
+      "std_standing": {}, "std_walking": {}, "std_running": {}, "walking_threshold": 0.05,
+      "running_threshold": 1.5}),
+    "body_ang_vel": RewardTermCfg(func=mdp.body_angular_velocity_penalty, weight=0.0,
+                                  params={"asset_cfg": SceneEntityCfg("robot", body_names=())}),
+    "angular_momentum": RewardTermCfg(func=mdp.angular_momentum_penalty, weight=0.0,
+                                      params={"sensor_name": "robot/root_angmom"}),
+    "dof_pos_limits": RewardTermCfg(func=mdp.joint_pos_limits, weight=-1.0),
+    "action_rate_l2": RewardTermCfg(func=mdp.action_rate_l2, weight=-0.1),
+    "air_time": RewardTermCfg(func=mdp.feet_air_time, weight=0.0, params={
+      "sensor_name": "feet_ground_contact", "threshold_min": 0.05, "threshold_max": 0.5,
+      "command_name": "twist", "command_threshold": 0.5}),
+    "foot_clearance": RewardTermCfg(func=mdp.feet_clearance, weight=-2.0, params={
+      "target_height": 0.1, "command_name": "twist", "command_threshold": 0.05,
+      "asset_cfg": SceneEntityCfg("robot", site_names=())}),
+    "foot_swing_height": RewardTermCfg(func=mdp.feet_swing_height, weight=-0.25, params={
+      "sensor_name": "feet_ground_contact", "target_height": 0.1, "command_name": "twist",
+      "command_threshold": 0.05, "asset_cfg": SceneEntityCfg("robot", site_names=())}),
+    "foot_slip": RewardTermCfg(func=mdp.feet_slip, weight=-0.1, params={
+      "sensor_name": "feet_ground_contact", "command_name": "twist", "command_threshold": 0.05,
+      "asset_cfg": SceneEntityCfg("robot", site_names=())}),
+    "soft_landing": RewardTermCfg(func=mdp.soft_landing, weight=-1e-5, params={
+      "sensor_name": "feet_ground_contact", "command_name": "twist", "command_threshold": 0.05}),
+  }
+  terminations = {
+    "time_out": TerminationTermCfg(func=mdp.time_out, time_out=True),
+    "fell_over": TerminationTermCfg(func=mdp.bad_orientation, params={"limit_angle": math.radians(70.0)}),
+  }
+  curriculum = {"command_vel": CurriculumTermCfg(func=mdp.commands_vel, params={
+    "command_name": "twist", "velocity_stages": [
+      {"step": 0, "lin_vel_x": (-1.0, 1.0), "ang_vel_z": (-0.5, 0.5)},
+      {"step": 5000 * 24, "lin_vel_x": (-1.5, 2.0), "ang_vel_z": (-0.7, 0.7)},
+      {"step": 10000 * 24, "lin_vel_x": (-2.0, 3.0)}]})}
+  return ManagerBasedRlEnvCfg(
+    scene=SceneCfg(scene_name=scene_name, num_envs=1), observations=observations,
+    actions=actions, commands=commands, events=events, rewards=rewards,
+    terminations=terminations, curriculum=curriculum,
+    sim=SimulationCfg(nconmax=35, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10,
+                                                               ls_iterations=20)),
+    decimation=4, episode_length_s=20.0)
+
+
+def unitree_g1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/config/g1/env_cfgs.py:20-175` (flat)."""
+  cfg = make_velocity_env_cfg("g1_velocity")
+  cfg.scene.contact_sensors = {
+    "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
+    "self_collision": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
+  }
+  sites = ("left_foot", "right_foot")
+  geoms = tuple(f"{s}_foot{i}_collision" for s in ("left", "right") for i in range(1, 8))
+  cfg.actions["joint_pos"].scale = az.action_scale(az.g1_actuators())
+  cfg.observations["critic"].terms["foot_height"].params["asset_cfg"].site_names = sites
+  cfg.events["foot_friction"].params["asset_cfg"].geom_names = geoms
+  p = cfg.rewards["pose"].params
+  p["std_standing"] = {".*": 0.05}
+  p["std_walking"] = {r".*hip_pitch.*": 0.3, r".*hip_roll.*": 0.15, r".*hip_yaw.*": 0.15,
+                      r".*knee.*": 0.35, r".*ankle_pitch.*": 0.25, r".*ankle_roll.*": 0.1,
+                      r".*waist_yaw.*": 0.2, r".*waist_roll.*": 0.08, r".*waist_pitch.*": 0.1,
+                      r".*shoulder_pitch.*": 0.15, r".*shoulder_roll.*": 0.15,
+                      r".*shoulder_yaw.*": 0.1, r".*elbow.*": 0.15, r".*wrist.*": 0.3}
+  p["std_running"] = {r".*hip_pitch.*": 0.5, r".*hip_roll.*": 0.2, r".*hip_yaw.*": 0.2,
+                      r".*knee.*": 0.6, r".*ankle_pitch.*": 0.35, r".*ankle_roll.*": 0.15,
+                      r".*waist_yaw.*": 0.3, r".*waist_roll.*": 0.08, r".*waist_pitch.*": 0.2,
+                      r".*shoulder_pitch.*": 0.5, r".*shoulder_roll.*": 0.2,
+                      r".*shoulder_yaw.*": 0.15, r".*elbow.*": 0.35, r".*wrist.*": 0.3}
+  cfg.rewards["upright"].params["asset_cfg"].body_names = ("torso_link",)
+  cfg.rewards["body_ang_vel"].params["asset_cfg"].body_names = ("torso_link",)
+  for r in ("foot_clearance", "foot_swing_height", "foot_slip"):
+    cfg.rewards[r].params["asset_cfg"].site_names = sites
+  cfg.rewards["body_ang_vel"].weight = -0.05
+  cfg.rewards["angular_momentum"].weight = -0.02
+  cfg.rewards["air_time"].weight = 0.0
+  cfg.rewards["self_collisions"] = RewardTermCfg(func=mdp.self_collision_cost, weight=-1.0,
+                                                 params={"sensor_name": "self_collision"})
+  if play:
+    cfg.episode_length_s = int(1e9)
+    cfg.observations["policy"].enable_corruption = False
+    cfg.events.pop("push_robot", None)
+    t = cfg.commands["twist"]
+    t.ranges.lin_vel_x = (-1.5, 2.0)
+    t.ranges.ang_vel_z = (-0.7, 0.7)
+  return cfg
+
+
+def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/config/go1/env_cfgs.py:15-127` (flat)."""
+  cfg = make_velocity_env_cfg("go1_velocity")
+  cfg.scene.contact_sensors = {
+    "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
+    "nonfoot_ground_touch": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
+  }
+  names = ("FR", "FL", "RR", "RL")
+  geoms = tuple(f"{n}_foot_collision" for n in names)
+  cfg.actions["joint_pos"].scale = az.action_scale(az.go1_actuators())
+  cfg.observations["critic"].terms["foot_height"].params["asset_cfg"].site_names = names
+  cfg.events["foot_friction"].params["asset_cfg"].geom_names = geoms
+  p = cfg.rewards["pose"].params
+  p["std_standing"] = {r".*(FR|FL|RR|RL)_(hip|thigh)_joint.*": 0.05, r".*(FR|FL|RR|RL)_calf_joint.*": 0.1}
+  p["std_walking"] = {r".*(FR|FL|RR|RL)_(hip|thigh)_joint.*": 0.3, r".*(FR|FL|RR|RL)_calf_joint.*": 0.6}
+  p["std_running"] = {r".*(FR|FL|RR|RL)_(hip|thigh)_joint.*": 0.3, r".*(FR|FL|RR|RL)_calf_joint.*": 0.6}
+  cfg.rewards["upright"].params["asset_cfg"].body_names = ("trunk",)
+  cfg.rewards["body_ang_vel"].params["asset_cfg"].body_names = ("trunk",)
+  for r in ("foot_clearance", "foot_swing_height", "foot_slip"):
+    cfg.rewards[r].params["asset_cfg"].site_names = names
+  cfg.rewards["body_ang_vel"].weight = 0.0
+  cfg.rewards["angular_momentum"].weight = 0.0
+  cfg.rewards["air_time"].weight = 0.0
+  cfg.terminations["illegal_contact"] = TerminationTermCfg(
+    func=mdp.illegal_contact, params={"sensor_name": "nonfoot_ground_touch"})
+  if play:
+    cfg.episode_length_s = int(1e9)
+    cfg.observations["policy"].enable_corruption = False
+    cfg.events.pop("push_robot", None)
+  return cfg
+
+
+TASKS = {
+  "Mjlab-Velocity-Flat-Unitree-G1": unitree_g1_flat_env_cfg,
+  "Mjlab-Velocity-Flat-Unitree-Go1": unitree_go1_flat_env_cfg,
+}
+
+
+def load_env_cfg(task: str, play: bool = False) -> ManagerBasedRlEnvCfg:
+  if task not in TASKS:
+    raise KeyError(f"unknown task {task}; available: {sorted(TASKS)}")
+  return TASKS[task](play=play)
+
+
+def make_env(task: str, num_envs: int, device: str, seed: int = 42, play: bool = False):
+  cfg = load_env_cfg(task, play)
+  cfg.scene.num_envs = num_envs
+  cfg.seed = seed
+  return ManagerBasedRlEnv(cfg, device=device)

@@ -1,0 +1,92 @@
+"""Batched quaternion / sampling helpers (wxyz convention) used by entity views and terms.
+
+Same conventions and semantics as the torch helpers the reference takes from Isaac Lab
+(`src/mjlab/utils/lab_api/math.py:102,166,275,318,527,629,651,1360`).
+"""
+
+from __future__ import annotations
+
+import torch
+
+
+def quat_mul(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  w1, x1, y1, z1 = q1.unbind(-1)
+  w2, x2, y2, z2 = q2.unbind(-1)
+  return torch.stack([
+    w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
+    w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+    w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+    w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], dim=-1)
+
+
+def quat_apply(quat: torch.Tensor, vec: torch.Tensor) -> torch.Tensor:
+  """Rotate `vec` by `quat` (v' = q v q*)."""
+  vec = vec.expand(quat.shape[:-1] + (3,)) if vec.dim() < quat.dim() else vec
+  w = quat[..., :1]
+  xyz = quat[..., 1:]
+  t = 2.0 * torch.cross(xyz, vec, dim=-1)
+  return vec + w * t + torch.cross(xyz, t, dim=-1)
+
+
+def quat_apply_inverse(quat: torch.Tensor, vec: torch.Tensor) -> torch.Tensor:
+  """Rotate `vec` by the inverse of `quat`."""
+  vec = vec.expand(quat.shape[:-1] + (3,)) if vec.dim() < quat.dim() else vec
+  w = quat[..., :1]
+  xyz = quat[..., 1:]
+  t = 2.0 * torch.cross(xyz, vec, dim=-1)
+  return vec - w * t + torch.cross(xyz, t, dim=-1)
+
+
+def quat_from_euler_xyz(roll: torch.Tensor, pitch: torch.Tensor, yaw: torch.Tensor):
+  cr, sr = torch.cos(roll * 0.5), torch.sin(roll * 0.5)
+  cp, sp = torch.cos(pitch * 0.5), torch.sin(pitch * 0.5)
+  cy, sy = torch.cos(yaw * 0.5), torch.sin(yaw * 0.5)
+  return torch.stack([cy * cr * cp + sy * sr * sp,
+                      cy * sr * cp - sy * cr * sp,
+                      cy * cr * sp + sy * sr * cp,
+                      sy * cr * cp - cy * sr * sp], dim=-1)
+
+
+def quat_from_matrix(m: torch.Tensor) -> torch.Tensor:
+  """Rotation matrix (..., 9) or (..., 3, 3) -> quaternion with w >= 0."""
+  if m.shape[-1] == 9:
+    m = m.reshape(m.shape[:-1] + (3, 3))
+  m00, m11, m22 = m[..., 0, 0], m[..., 1, 1], m[..., 2, 2]
+  w = torch.sqrt(torch.clamp(1 + m00 + m11 + m22, min=0)) * 0.5
+  x = torch.sqrt(torch.clamp(1 + m00 - m11 - m22, min=0)) * 0.5
+  y = torch.sqrt(torch.clamp(1 - m00 + m11 - m22, min=0)) * 0.5
+  z = torch.sqrt(torch.clamp(1 - m00 - m11 + m22, min=0)) * 0.5
+  x = torch.copysign(x, m[..., 2, 1] - m[..., 1, 2])
+  y = torch.copysign(y, m[..., 0, 2] - m[..., 2, 0])
+  z = torch.copysign(z, m[..., 1, 0] - m[..., 0, 1])
+  q = torch.stack([w, x, y, z], dim=-1)
+  return q / torch.linalg.norm(q, dim=-1, keepdim=True).clamp(min=1e-12)
+
+
+def matrix_from_quat(q: torch.Tensor) -> torch.Tensor:
+  w, x, y, z = q.unbind(-1)
+  return torch.stack([
+    1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+    2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+    2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=-1
+  ).reshape(q.shape[:-1] + (3, 3))
+
+
+def wrap_to_pi(angles: torch.Tensor) -> torch.Tensor:
+  wrapped = torch.remainder(angles, 2 * torch.pi)
+  return torch.where(wrapped > torch.pi, wrapped - 2 * torch.pi, wrapped)
+
+
+def sample_uniform(lower, upper, size, device, generator=None) -> torch.Tensor:
+  if isinstance(size, int):
+    size = (size,)
+  return torch.rand(*size, device=device, generator=generator) * (upper - lower) + lower
+
+
+def yaw_quat(quat: torch.Tensor) -> torch.Tensor:
+  w, x, y, z = quat.unbind(-1)
+  yaw = torch.atan2(2 * (w * z + x * y), 1 - 2 * (y * y + z * z))
+  out = torch.zeros_like(quat)
+  out[..., 0] = torch.cos(yaw / 2)
+  out[..., 3] = torch.sin(yaw / 2)
+  return out

@@ -1,0 +1,497 @@
+"""MDP term library used by the velocity / tracking / jump tasks.
+
+Generic terms restate `src/mjlab/envs/mdp/{observations,rewards,terminations,events}.py`
+and the joint-position action (`envs/mdp/actions/joint_actions.py:18-129`); velocity-task
+terms restate `src/mjlab/tasks/velocity/mdp/{rewards,observations,velocity_command,
+curriculums}.py`.  Same names, parameters and math.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from .managers import (ActionTerm, ActionTermCfg, CommandTerm, CommandTermCfg, SceneEntityCfg,
+                       resolve_matching_names_values)
+from .math_utils import quat_apply, quat_apply_inverse, quat_from_euler_xyz, quat_mul, \
+  sample_uniform, wrap_to_pi
+
+_ROBOT = SceneEntityCfg("robot")
+
+
+# =========================================================================== actions
+@dataclass(kw_only=True)
+class JointPositionActionCfg(ActionTermCfg):
+  actuator_names: tuple[str, ...] = (".*",)
+  scale: float | dict[str, float] = 1.0
+  offset: float | dict[str, float] = 0.0
+  use_default_offset: bool = True
+
+  def __post_init__(self):
+    self.class_type = JointPositionAction
+
+
+class JointPositionAction(ActionTerm):
+  """target = a * scale + offset - encoder_bias -> joint_pos_target (joint_actions.py)."""
+
+  def __init__(self, cfg: JointPositionActionCfg, env):
+    super().__init__(cfg, env)
+    self._asset = env.scene[cfg.asset_name]
+    ids, names = self._asset.find_joints_by_actuator_names(cfg.actuator_names)
+    self._joint_ids = torch.tensor(ids, device=self.device, dtype=torch.long)
+    self._joint_names = names
+    n = len(ids)
+    self._raw = torch.zeros(self.num_envs, n, device=self.device)
+    self._processed = torch.zeros_like(self._raw)
+    if isinstance(cfg.scale, (int, float)):
+      self._scale = float(cfg.scale)
+    else:
+      self._scale = torch.ones(self.num_envs, n, device=self.device)
+      idx, _, val = resolve_matching_names_values(cfg.scale, names)
+      self._scale[:, idx] = torch.tensor(val, device=self.device)
+    if isinstance(cfg.offset, (int, float)):
+      self._offset = float(cfg.offset)
+    else:
+      self._offset = torch.zeros_like(self._raw)
+      idx, _, val = resolve_matching_names_values(cfg.offset, names)
+      self._offset[:, idx] = torch.tensor(val, device=self.device)
+    if cfg.use_default_offset:
+      self._offset = self._asset.data.default_joint_pos[:, self._joint_ids].clone()
+
+  @property
+  def action_dim(self):
+    return len(self._joint_names)
+
+  @property
+  def raw_action(self):
+    return self._raw
+
+  @property
+  def scale(self):
+    return self._scale
+
+  @property
+  def offset(self):
+    return self._offset
+
+  def process_actions(self, actions):
+    self._raw[:] = actions
+    self._processed = self._raw * self._scale + self._offset
+
+  def apply_actions(self):
+    bias = self._asset.data.encoder_bias[:, self._joint_ids]
+    self._asset.set_joint_position_target(self._processed - bias, joint_ids=self._joint_ids)
+
+  def reset(self, env_ids=None):
+    self._raw[slice(None) if env_ids is None else env_ids] = 0.0
+
+
+# =========================================================================== observations
+def base_lin_vel(env, asset_cfg=_ROBOT):
+  return env.scene[asset_cfg.name].data.root_link_lin_vel_b
+
+
+def base_ang_vel(env, asset_cfg=_ROBOT):
+  return env.scene[asset_cfg.name].data.root_link_ang_vel_b
+
+
+def projected_gravity(env, asset_cfg=_ROBOT):
+  return env.scene[asset_cfg.name].data.projected_gravity_b
+
+
+def joint_pos_rel(env, biased: bool = False, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  jp = a.data.joint_pos_biased if biased else a.data.joint_pos
+  return jp[:, asset_cfg.joint_ids] - a.data.default_joint_pos[:, asset_cfg.joint_ids]
+
+
+def joint_vel_rel(env, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  return a.data.joint_vel[:, asset_cfg.joint_ids] - a.data.default_joint_vel[:, asset_cfg.joint_ids]
+
+
+def last_action(env, action_name: str | None = None):
+  if action_name is None:
+    return env.action_manager.action
+  return env.action_manager.get_term(action_name).raw_action
+
+
+def generated_commands(env, command_name: str):
+  return env.command_manager.get_command(command_name)
+
+
+def builtin_sensor(env, sensor_name: str):
+  return env.scene[sensor_name].data
+
+
+def foot_height(env, asset_cfg=_ROBOT):
+  return env.scene[asset_cfg.name].data.site_pos_w[:, asset_cfg.site_ids, 2]
+
+
+def foot_air_time(env, sensor_name: str):
+  return env.scene[sensor_name].data.current_air_time
+
+
+def foot_contact(env, sensor_name: str):
+  return (env.scene[sensor_name].data.found > 0).float()
+
+
+def foot_contact_forces(env, sensor_name: str):
+  f = env.scene[sensor_name].data.force.flatten(start_dim=1)
+  return torch.sign(f) * torch.log1p(torch.abs(f))
+
+
+# =========================================================================== terminations
+def time_out(env):
+  return env.episode_length_buf >= env.max_episode_length
+
+
+def bad_orientation(env, limit_angle: float, asset_cfg=_ROBOT):
+  g = env.scene[asset_cfg.name].data.projected_gravity_b
+  return torch.acos(-g[:, 2]).abs() > limit_angle
+
+
+def root_height_below_minimum(env, minimum_height: float, asset_cfg=_ROBOT):
+  return env.scene[asset_cfg.name].data.root_link_pos_w[:, 2] < minimum_height
+
+
+def nan_detection(env):
+  d = env.sim.data
+  return torch.isnan(d.qpos).any(-1) | torch.isnan(d.qvel).any(-1)
+
+
+def illegal_contact(env, sensor_name: str):
+  return torch.any(env.scene[sensor_name].data.found > 0, dim=-1)
+
+
+# =========================================================================== rewards
+def _command_active(env, command_name, threshold):
+  c = env.command_manager.get_command(command_name)
+  total = torch.norm(c[:, :2], dim=1) + torch.abs(c[:, 2])
+  return (total > threshold).float()
+
+
+def track_linear_velocity(env, std: float, command_name: str, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  c = env.command_manager.get_command(command_name)
+  v = a.data.root_link_lin_vel_b
+  err = torch.sum(torch.square(c[:, :2] - v[:, :2]), dim=1) + torch.square(v[:, 2])
+  return torch.exp(-err / std ** 2)
+
+
+def track_angular_velocity(env, std: float, command_name: str, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  c = env.command_manager.get_command(command_name)
+  w = a.data.root_link_ang_vel_b
+  err = torch.square(c[:, 2] - w[:, 2]) + torch.sum(torch.square(w[:, :2]), dim=1)
+  return torch.exp(-err / std ** 2)
+
+
+def flat_orientation(env, std: float, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  if isinstance(asset_cfg.body_ids, list) and asset_cfg.body_ids:
+    q = a.data.body_link_quat_w[:, asset_cfg.body_ids, :].squeeze(1)
+    g = quat_apply_inverse(q, a.data.gravity_vec_w)
+  else:
+    g = a.data.projected_gravity_b
+  return torch.exp(-torch.sum(torch.square(g[:, :2]), dim=1) / std ** 2)
+
+
+def self_collision_cost(env, sensor_name: str):
+  return env.scene[sensor_name].data.found.squeeze(-1)
+
+
+def body_angular_velocity_penalty(env, asset_cfg=_ROBOT):
+  w = env.scene[asset_cfg.name].data.body_link_ang_vel_w[:, asset_cfg.body_ids, :].squeeze(1)
+  return torch.sum(torch.square(w[:, :2]), dim=1)
+
+
+def angular_momentum_penalty(env, sensor_name: str):
+  h = env.scene[sensor_name].data
+  sq = torch.sum(torch.square(h), dim=-1)
+  env.extras["log"]["Metrics/angular_momentum_mean"] = torch.mean(torch.sqrt(sq))
+  return sq
+
+
+def joint_pos_limits(env, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  lim = a.data.soft_joint_pos_limits
+  q = a.data.joint_pos[:, asset_cfg.joint_ids]
+  out = -(q - lim[:, asset_cfg.joint_ids, 0]).clip(max=0.0)
+  out += (q - lim[:, asset_cfg.joint_ids, 1]).clip(min=0.0)
+  return torch.sum(out, dim=1)
+
+
+def action_rate_l2(env):
+  return torch.sum(torch.square(env.action_manager.action - env.action_manager.prev_action), dim=1)
+
+
+def feet_air_time(env, sensor_name: str, threshold_min: float = 0.05, threshold_max: float = 0.5,
+                  command_name: str | None = None, command_threshold: float = 0.5):
+  t = env.scene[sensor_name].data.current_air_time
+  reward = torch.sum(((t > threshold_min) & (t < threshold_max)).float(), dim=1)
+  in_air = (t > 0).float()
+  env.extras["log"]["Metrics/air_time_mean"] = torch.sum(t * in_air) / torch.clamp(in_air.sum(), min=1)
+  if command_name is not None:
+    reward = reward * _command_active(env, command_name, command_threshold)
+  return reward
+
+
+def feet_clearance(env, target_height: float, command_name: str | None = None,
+                   command_threshold: float = 0.01, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  z = a.data.site_pos_w[:, asset_cfg.site_ids, 2]
+  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_ids, :2], dim=-1)
+  cost = torch.sum(torch.abs(z - target_height) * v, dim=1)
+  if command_name is not None:
+    cost = cost * _command_active(env, command_name, command_threshold)
+  return cost
+
+
+class feet_swing_height:
+  """Stateful: peak height per foot while airborne, cost at landing."""
+
+  def __init__(self, cfg, env):
+    self.peak_heights = torch.zeros(env.num_envs, len(cfg.params["asset_cfg"].site_names),
+                                    device=env.device)
+    self.step_dt = env.step_dt
+
+  def reset(self, env_ids=None):
+    pass
+
+  def __call__(self, env, sensor_name, target_height, command_name, command_threshold, asset_cfg):
+    a = env.scene[asset_cfg.name]
+    s = env.scene[sensor_name]
+    h = a.data.site_pos_w[:, asset_cfg.site_ids, 2]
+    in_air = s.data.found == 0
+    self.peak_heights = torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights)
+    first = s.compute_first_contact(dt=self.step_dt)
+    active = _command_active(env, command_name, command_threshold)
+    err = self.peak_heights / target_height - 1.0
+    cost = torch.sum(torch.square(err) * first.float(), dim=1) * active
+    nland = torch.sum(first.float())
+    env.extras["log"]["Metrics/peak_height_mean"] = (
+      torch.sum(self.peak_heights * first.float()) / torch.clamp(nland, min=1))
+    self.peak_heights = torch.where(first, torch.zeros_like(self.peak_heights), self.peak_heights)
+    return cost
+
+
+def feet_slip(env, sensor_name: str, command_name: str, command_threshold: float = 0.01,
+              asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  s = env.scene[sensor_name]
+  active = _command_active(env, command_name, command_threshold)
+  inc = (s.data.found > 0).float()
+  v = torch.norm(a.data.site_lin_vel_w[:, asset_cfg.site_ids, :2], dim=-1)
+  cost = torch.sum(torch.square(v) * inc, dim=1) * active
+  env.extras["log"]["Metrics/slip_velocity_mean"] = torch.sum(v * inc) / torch.clamp(inc.sum(), min=1)
+  return cost
+
+
+def soft_landing(env, sensor_name: str, command_name: str | None = None,
+                 command_threshold: float = 0.05):
+  s = env.scene[sensor_name]
+  fm = torch.norm(s.data.force, dim=-1)
+  first = s.compute_first_contact(dt=env.step_dt)
+  impact = fm * first.float()
+  cost = torch.sum(impact, dim=1)
+  env.extras["log"]["Metrics/landing_force_mean"] = torch.sum(impact) / torch.clamp(first.float().sum(), min=1)
+  if command_name is not None:
+    cost = cost * _command_active(env, command_name, command_threshold)
+  return cost
+
+
+class variable_posture:
+  """exp(-mean((q-q0)^2/std^2)) with std chosen by command speed band."""
+
+  def __init__(self, cfg, env):
+    p = cfg.params
+    a = env.scene[p["asset_cfg"].name]
+    self.default_joint_pos = a.data.default_joint_pos
+    _, names = a.find_joints(p["asset_cfg"].joint_names)
+    mk = lambda d: torch.tensor(resolve_matching_names_values(d, names)[2], device=env.device,
+                                dtype=torch.float32)
+    self.std_standing = mk(p["std_standing"])
+    self.std_walking = mk(p["std_walking"])
+    self.std_running = mk(p["std_running"])
+
+  def reset(self, env_ids=None):
+    pass
+
+  def __call__(self, env, std_standing, std_walking, std_running, asset_cfg, command_name,
+               walking_threshold=0.5, running_threshold=1.5):
+    a = env.scene[asset_cfg.name]
+    c = env.command_manager.get_command(command_name)
+    sp = torch.norm(c[:, :2], dim=1) + torch.abs(c[:, 2])
+    st = (sp < walking_threshold).float().unsqueeze(1)
+    wk = ((sp >= walking_threshold) & (sp < running_threshold)).float().unsqueeze(1)
+    rn = (sp >= running_threshold).float().unsqueeze(1)
+    std = self.std_standing * st + self.std_walking * wk + self.std_running * rn
+    err = torch.square(a.data.joint_pos[:, asset_cfg.joint_ids] -
+                       self.default_joint_pos[:, asset_cfg.joint_ids])
+    return torch.exp(-torch.mean(err / std ** 2, dim=1))
+
+
+# =========================================================================== events
+def reset_root_state_uniform(env, env_ids, pose_range: dict, velocity_range: dict | None = None,
+                             asset_cfg=_ROBOT):
+  if env_ids is None:
+    env_ids = torch.arange(env.num_envs, device=env.device)
+  a = env.scene[asset_cfg.name]
+  keys = ["x", "y", "z", "roll", "pitch", "yaw"]
+  r = torch.tensor([pose_range.get(k, (0.0, 0.0)) for k in keys], device=env.device)
+  ps = sample_uniform(r[:, 0], r[:, 1], (len(env_ids), 6), env.device)
+  rs = a.data.default_root_state[env_ids].clone()
+  pos = rs[:, 0:3] + ps[:, 0:3] + env.scene.env_origins[env_ids]
+  quat = quat_mul(rs[:, 3:7], quat_from_euler_xyz(ps[:, 3], ps[:, 4], ps[:, 5]))
+  vr = torch.tensor([(velocity_range or {}).get(k, (0.0, 0.0)) for k in keys], device=env.device)
+  vel = rs[:, 7:13] + sample_uniform(vr[:, 0], vr[:, 1], (len(env_ids), 6), env.device)
+  a.write_root_link_pose_to_sim(torch.cat([pos, quat], dim=-1), env_ids=env_ids)
+  a.write_root_link_velocity_to_sim(vel, env_ids=env_ids)
+
+
+def reset_joints_by_offset(env, env_ids, position_range, velocity_range, asset_cfg=_ROBOT):
+  if env_ids is None:
+    env_ids = torch.arange(env.num_envs, device=env.device)
+  a = env.scene[asset_cfg.name]
+  jp = a.data.default_joint_pos[env_ids][:, asset_cfg.joint_ids].clone()
+  jp += sample_uniform(*position_range, jp.shape, env.device)
+  lim = a.data.soft_joint_pos_limits[env_ids][:, asset_cfg.joint_ids]
+  jp = jp.clamp_(lim[..., 0], lim[..., 1])
+  jv = a.data.default_joint_vel[env_ids][:, asset_cfg.joint_ids].clone()
+  jv += sample_uniform(*velocity_range, jv.shape, env.device)
+  jid = asset_cfg.joint_ids
+  if isinstance(jid, list):
+    jid = torch.tensor(jid, device=env.device)
+  a.write_joint_state_to_sim(jp.view(len(env_ids), -1), jv.view(len(env_ids), -1),
+                             env_ids=env_ids, joint_ids=jid)
+
+
+def push_by_setting_velocity(env, env_ids, velocity_range: dict, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  vel = a.data.root_link_vel_w[env_ids]
+  keys = ["x", "y", "z", "roll", "pitch", "yaw"]
+  r = torch.tensor([velocity_range.get(k, (0.0, 0.0)) for k in keys], device=env.device)
+  vel += sample_uniform(r[:, 0], r[:, 1], vel.shape, env.device)
+  a.write_root_link_velocity_to_sim(vel, env_ids=env_ids)
+
+
+def randomize_field(env, env_ids, field: str, ranges, operation: str = "abs",
+                    distribution: str = "uniform", asset_cfg=_ROBOT, axes=None):
+  """Domain randomization of one model field over the entity's elements
+  (`envs/mdp/events.py:264-289,519-706`); the field must have been expanded."""
+  a = env.scene[asset_cfg.name]
+  if env_ids is None:
+    env_ids = torch.arange(env.num_envs, device=env.device)
+  t = getattr(env.sim.model, field)
+  if field.startswith("geom_"):
+    ids = a.indexing.geom_ids if asset_cfg.geom_ids == slice(None) else a.indexing.geom_ids[asset_cfg.geom_ids]
+  elif field.startswith("body_"):
+    ids = a.indexing.body_ids if asset_cfg.body_ids == slice(None) else a.indexing.body_ids[asset_cfg.body_ids]
+  elif field.startswith("dof_"):
+    ids = a.indexing.joint_v_adr if asset_cfg.joint_ids == slice(None) else a.indexing.joint_v_adr[asset_cfg.joint_ids]
+  else:
+    raise NotImplementedError(field)
+  if axes is None:
+    axes = [0] if t.dim() == 3 else None
+  lo, hi = ranges if isinstance(ranges, tuple) else tuple(ranges)
+  shape = (len(env_ids), len(ids)) + ((len(axes),) if axes is not None else ())
+  if distribution == "uniform":
+    vals = sample_uniform(lo, hi, shape, env.device)
+  else:
+    vals = torch.exp(sample_uniform(math.log(lo), math.log(hi), shape, env.device))
+  e = env_ids[:, None]
+  if axes is None:
+    base = env.sim.get_default_field(field)[ids]
+    cur = vals if operation == "abs" else (base * vals if operation == "scale" else base + vals)
+    t[e, ids] = cur
+  else:
+    ax = torch.tensor(axes, device=env.device)
+    base = env.sim.get_default_field(field)[ids][:, ax]
+    cur = vals if operation == "abs" else (base * vals if operation == "scale" else base + vals)
+    t[e[..., None], ids[None, :, None], ax[None, None, :]] = cur
+
+
+# =========================================================================== commands
+@dataclass(kw_only=True)
+class UniformVelocityCommandCfg(CommandTermCfg):
+  asset_name: str = "robot"
+  heading_command: bool = False
+  heading_control_stiffness: float = 1.0
+  rel_standing_envs: float = 0.0
+  rel_heading_envs: float = 1.0
+  init_velocity_prob: float = 0.0
+
+  @dataclass
+  class Ranges:
+    lin_vel_x: tuple[float, float] = (-1.0, 1.0)
+    lin_vel_y: tuple[float, float] = (-1.0, 1.0)
+    ang_vel_z: tuple[float, float] = (-1.0, 1.0)
+    heading: tuple[float, float] | None = None
+
+  ranges: "UniformVelocityCommandCfg.Ranges" = field(default_factory=lambda: UniformVelocityCommandCfg.Ranges())
+
+  def __post_init__(self):
+    self.class_type = UniformVelocityCommand
+
+
+class UniformVelocityCommand(CommandTerm):
+  """`tasks/velocity/mdp/velocity_command.py:25-101`."""
+
+  def __init__(self, cfg: UniformVelocityCommandCfg, env):
+    super().__init__(cfg, env)
+    self.robot = env.scene[cfg.asset_name]
+    n = self.num_envs
+    self.vel_command_b = torch.zeros(n, 3, device=self.device)
+    self.heading_target = torch.zeros(n, device=self.device)
+    self.heading_error = torch.zeros(n, device=self.device)
+    self.is_heading_env = torch.zeros(n, dtype=torch.bool, device=self.device)
+    self.is_standing_env = torch.zeros_like(self.is_heading_env)
+    self.metrics["error_vel_xy"] = torch.zeros(n, device=self.device)
+    self.metrics["error_vel_yaw"] = torch.zeros(n, device=self.device)
+
+  @property
+  def command(self):
+    return self.vel_command_b
+
+  def _update_metrics(self):
+    steps = self.cfg.resampling_time_range[1] / self._env.step_dt
+    v = self.robot.data.root_link_lin_vel_b
+    w = self.robot.data.root_link_ang_vel_b
+    self.metrics["error_vel_xy"] += torch.norm(self.vel_command_b[:, :2] - v[:, :2], dim=-1) / steps
+    self.metrics["error_vel_yaw"] += torch.abs(self.vel_command_b[:, 2] - w[:, 2]) / steps
+
+  def _resample_command(self, env_ids):
+    r = torch.empty(len(env_ids), device=self.device)
+    rg = self.cfg.ranges
+    self.vel_command_b[env_ids, 0] = r.uniform_(*rg.lin_vel_x)
+    self.vel_command_b[env_ids, 1] = r.uniform_(*rg.lin_vel_y)
+    self.vel_command_b[env_ids, 2] = r.uniform_(*rg.ang_vel_z)
+    if self.cfg.heading_command:
+      self.heading_target[env_ids] = r.uniform_(*rg.heading)
+      self.is_heading_env[env_ids] = r.uniform_(0.0, 1.0) <= self.cfg.rel_heading_envs
+    self.is_standing_env[env_ids] = r.uniform_(0.0, 1.0) <= self.cfg.rel_standing_envs
+
+  def _update_command(self):
+    if self.cfg.heading_command:
+      self.heading_error = wrap_to_pi(self.heading_target - self.robot.data.heading_w)
+      lo, hi = self.cfg.ranges.ang_vel_z
+      hc = torch.clip(self.cfg.heading_control_stiffness * self.heading_error, min=lo, max=hi)
+      self.vel_command_b[:, 2] = torch.where(self.is_heading_env, hc, self.vel_command_b[:, 2])
+    self.vel_command_b.masked_fill_(self.is_standing_env.unsqueeze(1), 0.0)
+
+
+# =========================================================================== curriculum
+def commands_vel(env, env_ids, command_name: str, velocity_stages: list):
+  cfg = env.command_manager.get_term(command_name).cfg
+  for st in velocity_stages:
+    if env.common_step_counter > st["step"]:
+      for k in ("lin_vel_x", "lin_vel_y", "ang_vel_z"):
+        if st.get(k) is not None:
+          setattr(cfg.ranges, k, st[k])
+  r = cfg.ranges
+  return {"lin_vel_x_min": r.lin_vel_x[0], "lin_vel_x_max": r.lin_vel_x[1],
+          "lin_vel_y_min": r.lin_vel_y[0], "lin_vel_y_max": r.lin_vel_y[1],
+          "ang_vel_z_min": r.ang_vel_z[0], "ang_vel_z_max": r.ang_vel_z[1]}

@@ -91,6 +91,11 @@ def save_model(m: Model, path: str) -> None:
   meta["gravity"] = list(map(float, m.gravity))
   meta["names"] = m.names
   payload["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+  if os.path.exists(path):  # keep the file (and its zip timestamps) when nothing changed
+    with np.load(path, allow_pickle=False) as z:
+      if set(z.files) == set(payload) and all(
+          z[k].shape == np.asarray(v).shape and np.array_equal(z[k], v) for k, v in payload.items()):
+        return
   np.savez_compressed(path, **payload)
 
 

@@ -135,6 +135,7 @@ class Simulation:
     self._model_bridge = DeviceBridge(self, "model.", self.num_envs)
     self._reset_mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self._torch_device)
     self.nan_guard = NanGuard(cfg.nan_guard, self.num_envs, self._mj_model)
+    self._timing = None
     self.create_graph()
 
   def __del__(self):
@@ -205,7 +206,28 @@ class Simulation:
   def step(self, nsubstep: int = 1) -> None:
     """One mj_step for every world (or `nsubstep` steps fused in one launch)."""
     with self.nan_guard.watch(self.data):
-      check(lib().mjx_step(self._sim, int(nsubstep), _stream_handle(self._torch_device)))
+      if self._timing is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        check(lib().mjx_step(self._sim, int(nsubstep), _stream_handle(self._torch_device)))
+        ev1.record()
+        self._timing.append((ev0, ev1))
+      else:
+        check(lib().mjx_step(self._sim, int(nsubstep), _stream_handle(self._torch_device)))
+
+  # Launch timing (HIP events on the launch stream) for the benchmark's roofline.
+  def timing_begin(self) -> None:
+    self._timing = []
+
+  def timing_end(self) -> float:
+    """Mean step-kernel launch duration in ms since timing_begin (synchronises)."""
+    ev = self._timing or []
+    self._timing = None
+    if not ev:
+      return 0.0
+    torch.cuda.synchronize(self._torch_device)
+    return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
   def reset(self, env_ids: torch.Tensor | None = None) -> None:
     stream = _stream_handle(self._torch_device)
