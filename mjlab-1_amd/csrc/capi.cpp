@@ -221,6 +221,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_FLT
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
+  reserve("__prof", sizeof(unsigned long long) * 16);
   hipError_t e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }
   e = hipMemset(s->arena, 0, off);
@@ -240,6 +241,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_FLT
 #undef X_INT
   s->dd.stats = (int32_t*)(base + offs[k++].second);
+  s->dd.prof = (unsigned long long*)(base + offs[k++].second);
   s->stats = s->dd.stats;
   // model fields visible as "model.<name>"
   for (auto& kv : model->float_dims) {
@@ -384,6 +386,13 @@ int mjx_expand_field(mjxSim* s, const char* cname, void* stream) {
   MJX_MODEL_FLOAT_FIELDS(X_FLT)
 #undef X_FLT
   return sync_params(s, stream);
+}
+
+int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
+  if (!s || !out) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(out, s->dd.prof, sizeof(uint64_t) * 16, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
 }
 
 int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {

@@ -49,6 +49,7 @@ struct DData {
 #undef X_FLT
 #undef X_INT
   int32_t* stats;  // [8] global counters (atomics)
+  unsigned long long* prof;  // [16] stage cycle sums (diagnostic -DMJX_STAMPS build)
 };
 
 // Per-world LDS carve (offsets in 4-byte words).
@@ -62,8 +63,8 @@ struct Lds {
       qfrc_con, vtmp, act_force, act_len, act_vel;
   int con_g1, con_g2, con_key, con_dist, con_pos, con_frame, con_mu, con_solref,
       con_solimp, con_imargin, con_dim, con_efc;
-  int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_type;
-  int red;      // 2*kWave scratch for reductions
+  int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_type, efc_act, hdiag;
+  int red;      // 5*kWave scratch (J^T w partial sums)
   int ints;     // small int block: [0]=ncon [1]=nefc [2]=nlimit [3]=overflow
   int total;
 };

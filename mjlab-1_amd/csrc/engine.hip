@@ -41,7 +41,7 @@ Lds make_lds(const Dims& d) {
   Lds L{};
   int o = 0;
   auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };  // 16-B aligned carve
-  const int nb = d.nbody, nv = d.nv, C = d.nconmax, R = d.njmax;
+  const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
   L.qpos = take(d.nq); L.qvel = take(nv); L.ctrl = take(d.nu); L.qacc_ws = take(nv);
   L.qfrc_applied = take(nv); L.xfrc = take(6 * nb);
   L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
@@ -63,7 +63,8 @@ Lds make_lds(const Dims& d) {
   L.con_dim = take(C); L.con_efc = take(C);
   L.efc_J = take(R * nv); L.efc_aref = take(R); L.efc_D = take(R); L.efc_jar = take(R);
   L.efc_Js = take(R); L.efc_force = take(R); L.efc_cid = take(R); L.efc_type = take(R);
-  L.red = take(2 * kWave);
+  L.efc_act = take(R); L.hdiag = take(nv);
+  L.red = take(5 * kWave);
   L.ints = take(8);
   L.total = o;
   return L;
@@ -167,47 +168,259 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
 
 #define MF(f) (m.f + (size_t)w * m.f##_ws)
 
-// Dense Cholesky of the nv x nv SPD matrix A (row-major, lower used) in place.
-// Right-looking; the trailing update is spread over lanes by lower-triangle element.
-__device__ void chol_lds(float* A, int n, int lane) {
-  for (int k = 0; k < n; k++) {
-    float piv = A[k * n + k];
-    piv = sqrtf(fmaxf(piv, MINVAL));
-    float inv = 1.0f / piv;
+// Diagnostic build only (-DMJX_STAMPS): per-stage s_memtime deltas summed over worlds.
+#ifdef MJX_STAMPS
+#define STAMP(k)                                                                 \
+  do {                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+    if (lane == 0) atomicAdd((unsigned long long*)&D.prof[k], t_ - stamp_prev);   \
+    stamp_prev = t_;                                                             \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
+// --------------------------------------------------------------------------- tiled SPD algebra
+// The nv x nv SPD systems (mass matrix, Newton Hessian, implicit-integration matrix) are
+// padded to NVP = 4*ceil(nv/4) and split into 4x4 tiles of the lower triangle; lane l owns
+// tiles l and l+64 (at most 2, so NVP <= 60).  Tiles live in registers through assembly
+// and factorization; the Cholesky factor is published to LDS (row stride NVP) for the
+// triangular solves.  Padding rows/cols are identity, so padded unknowns solve to 0.
+struct Tiles {
+  int nb, ntile;
+  int bi[2], bj[2];
+  bool own[2];
+};
+__device__ __forceinline__ Tiles make_tiles(int nvp, int lane) {
+  Tiles t;
+  t.nb = nvp >> 2;
+  t.ntile = t.nb * (t.nb + 1) / 2;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    int idx = lane + kWave * s;
+    t.own[s] = idx < t.ntile;
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= idx) bi++;
+    t.bi[s] = bi;
+    t.bj[s] = idx - bi * (bi + 1) / 2;
+  }
+  return t;
+}
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4v(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ void tiles_load(float (&A)[2][16], const Tiles& T, const float* Mm, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float4 v = ld4(Mm + (4 * T.bi[s] + r) * nvp + 4 * T.bj[s]);
+      A[s][4 * r + 0] = v.x; A[s][4 * r + 1] = v.y; A[s][4 * r + 2] = v.z; A[s][4 * r + 3] = v.w;
+    }
+  }
+}
+// A += sum_k D[act[k]] * J[act[k], iblock]^T J[act[k], jblock]
+__device__ __forceinline__ void tiles_add_jtdj(float (&A)[2][16], const Tiles& T, const float* J,
+                                               const float* Dv, const int* act, int nact, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+    const int oi = 4 * T.bi[s], oj = 4 * T.bj[s];
+    int k = 0;
+    for (; k + 1 < nact; k += 2) {
+      int r0 = act[k], r1 = act[k + 1];
+      float4 a0 = ld4(J + r0 * nvp + oi), b0 = ld4(J + r0 * nvp + oj);
+      float4 a1 = ld4(J + r1 * nvp + oi), b1 = ld4(J + r1 * nvp + oj);
+      float d0 = Dv[r0], d1 = Dv[r1];
+      float ai0[4] = {a0.x, a0.y, a0.z, a0.w}, bj0[4] = {b0.x * d0, b0.y * d0, b0.z * d0, b0.w * d0};
+      float ai1[4] = {a1.x, a1.y, a1.z, a1.w}, bj1[4] = {b1.x * d1, b1.y * d1, b1.z * d1, b1.w * d1};
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) A[s][4 * r + c] += ai0[r] * bj0[c] + ai1[r] * bj1[c];
+    }
+    if (k < nact) {
+      int r0 = act[k];
+      float4 a0 = ld4(J + r0 * nvp + oi), b0 = ld4(J + r0 * nvp + oj);
+      float d0 = Dv[r0];
+      float ai0[4] = {a0.x, a0.y, a0.z, a0.w}, bj0[4] = {b0.x * d0, b0.y * d0, b0.z * d0, b0.w * d0};
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) A[s][4 * r + c] += ai0[r] * bj0[c];
+    }
+  }
+}
+// Right-looking blocked Cholesky; L written to Lm (row stride nvp, lower tiles).
+__device__ void tiles_chol(float (&A)[2][16], const Tiles& T, float* Lm, int nvp) {
+  for (int p = 0; p < T.nb; p++) {
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      if (!(T.own[s] && T.bi[s] == p && T.bj[s] == p)) continue;
+      float* a = A[s];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        float d = a[5 * c];
+#pragma unroll
+        for (int k = 0; k < c; k++) d -= a[4 * c + k] * a[4 * c + k];
+        d = sqrtf(fmaxf(d, MINVAL));
+        a[5 * c] = d;
+        float inv = 1.0f / d;
+#pragma unroll
+        for (int r = c + 1; r < 4; r++) {
+          float v = a[4 * r + c];
+#pragma unroll
+          for (int k = 0; k < c; k++) v -= a[4 * r + k] * a[4 * c + k];
+          a[4 * r + c] = v * inv;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        st4v(Lm + (4 * p + r) * nvp + 4 * p,
+             make_float4(a[4 * r], r >= 1 ? a[4 * r + 1] : 0.f, r >= 2 ? a[4 * r + 2] : 0.f,
+                         r >= 3 ? a[4 * r + 3] : 0.f));
+    }
     sync();
-    if (lane == 0) A[k * n + k] = piv;
-    for (int i = k + 1 + lane; i < n; i += kWave) A[i * n + k] *= inv;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      if (!(T.own[s] && T.bj[s] == p && T.bi[s] > p)) continue;
+      float Lp[16];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float4 v = ld4(Lm + (4 * p + r) * nvp + 4 * p);
+        Lp[4 * r] = v.x; Lp[4 * r + 1] = v.y; Lp[4 * r + 2] = v.z; Lp[4 * r + 3] = v.w;
+      }
+      float* a = A[s];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          float v = a[4 * r + c];
+#pragma unroll
+          for (int k = 0; k < c; k++) v -= a[4 * r + k] * Lp[4 * c + k];
+          a[4 * r + c] = v / Lp[5 * c];
+        }
+        st4v(Lm + (4 * T.bi[s] + r) * nvp + 4 * p,
+             make_float4(a[4 * r], a[4 * r + 1], a[4 * r + 2], a[4 * r + 3]));
+      }
+    }
     sync();
-    int m = n - k - 1;  // trailing size
-    int cnt = m * (m + 1) / 2;
-    for (int e = lane; e < cnt; e += kWave) {
-      // e -> (i, j), i >= j, over the trailing block
-      int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
-      while ((i + 1) * (i + 2) / 2 <= e) i++;
-      while (i * (i + 1) / 2 > e) i--;
-      int j = e - i * (i + 1) / 2;
-      i += k + 1; j += k + 1;
-      A[i * n + j] -= A[i * n + k] * A[j * n + k];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      if (!(T.own[s] && T.bj[s] > p)) continue;
+      float Li[16], Lj[16];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float4 v = ld4(Lm + (4 * T.bi[s] + r) * nvp + 4 * p);
+        Li[4 * r] = v.x; Li[4 * r + 1] = v.y; Li[4 * r + 2] = v.z; Li[4 * r + 3] = v.w;
+        float4 u = ld4(Lm + (4 * T.bj[s] + r) * nvp + 4 * p);
+        Lj[4 * r] = u.x; Lj[4 * r + 1] = u.y; Lj[4 * r + 2] = u.z; Lj[4 * r + 3] = u.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+          for (int k = 0; k < 4; k++) A[s][4 * r + c] -= Li[4 * r + k] * Lj[4 * c + k];
+    }
+  }
+}
+// Solve (L L^T) x = b in place; x in LDS (length nvp, padded entries 0).
+__device__ void tiles_solve(const float* Lm, float* x, int nb, int nvp, int lane) {
+  for (int p = 0; p < nb; p++) {
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = x[4 * p + r];
+        for (int c = 0; c < r; c++) v -= Lm[(4 * p + r) * nvp + 4 * p + c] * x[4 * p + c];
+        x[4 * p + r] = v / Lm[(4 * p + r) * nvp + 4 * p + r];
+      }
+    }
+    sync();
+    float4 xp = ld4(x + 4 * p);
+    for (int i = 4 * (p + 1) + lane; i < nvp; i += kWave) {
+      float4 l = ld4(Lm + i * nvp + 4 * p);
+      x[i] -= l.x * xp.x + l.y * xp.y + l.z * xp.z + l.w * xp.w;
+    }
+    sync();
+  }
+  for (int p = nb - 1; p >= 0; p--) {
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 3; r >= 0; r--) {
+        float v = x[4 * p + r];
+        for (int c = r + 1; c < 4; c++) v -= Lm[(4 * p + c) * nvp + 4 * p + r] * x[4 * p + c];
+        x[4 * p + r] = v / Lm[(4 * p + r) * nvp + 4 * p + r];
+      }
+    }
+    sync();
+    float4 xp = ld4(x + 4 * p);
+    for (int i = lane; i < 4 * p; i += kWave) {
+      x[i] -= Lm[(4 * p) * nvp + i] * xp.x + Lm[(4 * p + 1) * nvp + i] * xp.y +
+              Lm[(4 * p + 2) * nvp + i] * xp.z + Lm[(4 * p + 3) * nvp + i] * xp.w;
     }
     sync();
   }
 }
-// Solve L L^T x = b in place (b in LDS vector).
-__device__ void chol_solve_lds(const float* L, int n, float* x, int lane) {
-  for (int k = 0; k < n; k++) {
-    float xk = x[k] / L[k * n + k];
-    sync();
-    if (lane == 0) x[k] = xk;
-    for (int i = k + 1 + lane; i < n; i += kWave) x[i] -= L[i * n + k] * xk;
-    sync();
+// out[i] = Mm[i,:] . v for i < nrow (row stride nvp), v broadcast-read as float4.
+__device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const float* v, int nrow,
+                                            int nvp, int lane) {
+  const int nb = nvp >> 2;
+  for (int i = lane; i < nrow; i += kWave) {
+    const float* row = Mm + i * nvp;
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    for (; k + 1 < nb; k += 2) {
+      float4 a = ld4(row + 4 * k), b = ld4(v + 4 * k);
+      float4 c = ld4(row + 4 * k + 4), e = ld4(v + 4 * k + 4);
+      s0 += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+      s1 += c.x * e.x + c.y * e.y + c.z * e.z + c.w * e.w;
+    }
+    if (k < nb) {
+      float4 a = ld4(row + 4 * k), b = ld4(v + 4 * k);
+      s0 += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    }
+    out[i] = s0 + s1;
   }
-  for (int k = n - 1; k >= 0; k--) {
-    float xk = x[k] / L[k * n + k];
-    sync();
-    if (lane == 0) x[k] = xk;
-    for (int i = lane; i < k; i += kWave) x[i] -= L[k * n + i] * xk;
-    sync();
+}
+// out[c] = sum_k J[act[k], c] * wv[act[k]] (c < nvp).  Lanes split (column block, row
+// group); partial sums reduced through `part` (>= 64*4 floats).  Ends with a sync.
+__device__ void jt_mul(float* out, const float* J, const float* wv, const int* act, int nact,
+                       int nvp, float* part, int lane) {
+  const int nb = nvp >> 2;
+  const int ng = kWave / nb;
+  const int cb = lane % nb, g = lane / nb;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < ng) {
+    for (int k = g; k < nact; k += ng) {
+      int r = act[k];
+      float4 j = ld4(J + r * nvp + 4 * cb);
+      float wr = wv[r];
+      acc.x += j.x * wr; acc.y += j.y * wr; acc.z += j.z * wr; acc.w += j.w * wr;
+    }
+    st4v(part + g * nvp + 4 * cb, acc);
   }
+  sync();
+  for (int c = lane; c < nvp; c += kWave) {
+    float s = 0.f;
+    for (int gg = 0; gg < ng; gg++) s += part[gg * nvp + c];
+    out[c] = s;
+  }
+  sync();
+}
+// Compact the rows with jar < 0 into act[]; returns the count (wave-uniform).
+__device__ __forceinline__ int build_active(int* act, const float* jar, int nefc, int lane) {
+  int base = 0;
+  for (int r0 = 0; r0 < nefc; r0 += kWave) {
+    int r = r0 + lane;
+    bool f = r < nefc && jar[r] < 0.f;
+    unsigned long long bal = __ballot(f);
+    if (f) act[base + __popcll(bal & ((1ull << lane) - 1ull))] = r;
+    base += __popcll(bal);
+  }
+  return base;
 }
 
 // --------------------------------------------------------------------------- collision
@@ -298,7 +511,18 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
   int* Si = reinterpret_cast<int*>(S);
   int* ints = Si + L.ints;
   const int nv = d.nv, nb = d.nbody, nq = d.nq, nu = d.nu;
+  const int nvp = (nv + 3) & ~3;
+  const Tiles T = make_tiles(nvp, lane);
   const float h = o.timestep;
+  // zero every nvp-padded vector once (stages write only [0, nv))
+  for (int i = lane; i < nvp; i += kWave) {
+    S[L.qvel + i] = 0.f; S[L.qacc_ws + i] = 0.f; S[L.qfrc_applied + i] = 0.f;
+    S[L.qfrc_bias + i] = 0.f; S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f;
+    S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
+    S[L.grad + i] = 0.f; S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
+    S[L.vtmp + i] = 0.f;
+  }
+  sync();
 
   // ------------------------------------------------------------- load state (coalesced)
   for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
@@ -314,6 +538,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
   for (int i = lane; i < 6 * nb; i += kWave) any_xfrc |= (D.xfrc_applied[(size_t)w * 6 * nb + i] != 0.f);
   any_xfrc = __any(any_xfrc);
   sync();
+#ifdef MJX_STAMPS
+  unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
 
   const float* body_pos = MF(body_pos);
   const float* body_quat = MF(body_quat);
@@ -409,6 +636,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         mat3mul(S + L.sxmat + 9 * s, R, Rs);
       }
     }
+    STAMP(0);
     // =========================================================== com / cinert / cdof
     for (int b = lane; b < nb; b += kWave) {
       float ms = body_mass[b];
@@ -493,6 +721,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
     }
     sync();
+    STAMP(1);
     // =========================================================== CRB + mass matrix
     for (int i = lane; i < 10 * nb; i += kWave) S[L.crb + i] = S[L.cinert + i];
     sync();
@@ -510,8 +739,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       sync();
     }
-    for (int i = lane; i < nv * nv; i += kWave) S[L.M + i] = 0;
+    for (int i = lane; i < nvp * nvp; i += kWave) S[L.M + i] = 0;
     sync();
+    for (int i = nv + lane; i < nvp; i += kWave) S[L.M + i * nvp + i] = 1.f;  // identity padding
     {
       const float* arm = MF(dof_armature);
       for (int i = lane; i < nv; i += kWave) {
@@ -519,12 +749,13 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         inert_mul(f, S + L.crb + 10 * m.dof_bodyid[i], S + L.cdof + 6 * i);
         for (int j = i; j >= 0; j = m.dof_parentid[j]) {
           float v = dot6(S + L.cdof + 6 * j, f);
-          S[L.M + i * nv + j] = v;
-          S[L.M + j * nv + i] = v;
+          S[L.M + i * nvp + j] = v;
+          S[L.M + j * nvp + i] = v;
         }
-        S[L.M + i * nv + i] += arm[i];
+        S[L.M + i * nvp + i] += arm[i];
       }
     }
+    STAMP(2);
     if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
     sync();
     // =========================================================== collision
@@ -592,6 +823,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
     }
     sync();
+    STAMP(3);
     // deterministic order: bitonic sort of (key, slot) over 64 lanes, then permute
     int ncon = min(ints[0], d.nconmax);
     {
@@ -676,6 +908,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       sync();
     }
+    STAMP(4);
     // =========================================================== constraints
     {
       // row counts: limits (lane per joint) then contacts (lane per contact)
@@ -739,11 +972,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       sync();
       // Jacobian rows: lane per dof
-      for (int i = lane; i < nv; i += kWave) {
+      for (int i = lane; i < nvp; i += kWave) {
         // limits
         for (int r = 0; r < lim_total && r < nefc; r++) {
           int j = -1 - Si[L.efc_cid + r];
-          S[L.efc_J + r * nv + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
+          S[L.efc_J + r * nvp + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
+        }
+        if (i >= nv) {  // zero padding columns of the contact rows
+          for (int r = lim_total; r < nefc; r++) S[L.efc_J + r * nvp + i] = 0.f;
+          continue;
         }
         uint64_t bm = m.dof_bodymask[i];
         const float* cd = S + L.cdof + 6 * i;
@@ -760,15 +997,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
           float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
           int r0 = Si[L.con_efc + c];
           if (Si[L.con_dim + c] == 1) {
-            S[L.efc_J + r0 * nv + i] = jn;
+            S[L.efc_J + r0 * nvp + i] = jn;
           } else {
             float jt1 = fr[3] * jd.x + fr[4] * jd.y + fr[5] * jd.z;
             float jt2 = fr[6] * jd.x + fr[7] * jd.y + fr[8] * jd.z;
             float mu0 = S[L.con_mu + 2 * c], mu1 = S[L.con_mu + 2 * c + 1];
-            S[L.efc_J + (r0 + 0) * nv + i] = jn + mu0 * jt1;
-            S[L.efc_J + (r0 + 1) * nv + i] = jn - mu0 * jt1;
-            S[L.efc_J + (r0 + 2) * nv + i] = jn + mu1 * jt2;
-            S[L.efc_J + (r0 + 3) * nv + i] = jn - mu1 * jt2;
+            S[L.efc_J + (r0 + 0) * nvp + i] = jn + mu0 * jt1;
+            S[L.efc_J + (r0 + 1) * nvp + i] = jn - mu0 * jt1;
+            S[L.efc_J + (r0 + 2) * nvp + i] = jn + mu1 * jt2;
+            S[L.efc_J + (r0 + 3) * nvp + i] = jn - mu1 * jt2;
           }
         }
       }
@@ -813,7 +1050,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
           B = -sref[1] / dmax;
         }
         float vel = 0;
-        const float* J = S + L.efc_J + r * nv;
+        const float* J = S + L.efc_J + r * nvp;
         for (int i = 0; i < nv; i++) vel += J[i] * S[L.qvel + i];
         S[L.efc_D + r] = 1.0f / Rr;
         S[L.efc_aref + r] = -B * vel - K * imp * (pos - margin);
@@ -823,6 +1060,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
     }
     const int nefc = ints[1];
     ncon = ints[4];
+    STAMP(5);
     // =========================================================== velocity stage
     if (lane < 6) S[L.cvel + lane] = 0;
     sync();
@@ -959,11 +1197,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       // stash body com velocity in cacc? no: recompute when needed
     }
     sync();
+    STAMP(6);
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
-    for (int i = lane; i < nv * nv; i += kWave) S[L.H + i] = S[L.M + i];
-    sync();
-    chol_lds(S + L.H, nv, lane);
-    chol_solve_lds(S + L.H, nv, S + L.qacc_smooth, lane);
+    {
+      float A[2][16];
+      tiles_load(A, T, S + L.M, nvp);
+      tiles_chol(A, T, S + L.H, nvp);
+    }
+    tiles_solve(S + L.H, S + L.qacc_smooth, T.nb, nvp, lane);
+    STAMP(7);
     // linear momentum of subtrees -> velocity of subtree com
     for (int lv = d.nlevel - 2; lv >= 0; lv--) {
       int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
@@ -1010,119 +1252,110 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       sync();
     }
+    STAMP(8);
     // =========================================================== Newton solver
     int niter = 0;
     if (nefc == 0) {
-      for (int i = lane; i < nv; i += kWave) {
+      for (int i = lane; i < nvp; i += kWave) {
         S[L.x + i] = S[L.qacc_smooth + i];
         S[L.qfrc_con + i] = 0.f;
       }
       sync();
     } else {
+      float* jar = S + L.efc_jar;
+      float* Js = S + L.efc_Js;
+      float* wv = S + L.efc_force;
+      const float* Dv = S + L.efc_D;
+      const float* J = S + L.efc_J;
+      int* act = Si + L.efc_act;
+      float* Lm = S + L.H;
       const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
-      // cost(x) helper over rows; Mx must be valid.  Returns total cost (wave-uniform).
-      auto eval_cost = [&](const float* xv, const float* Mxv) -> float {
+      // jar = J x - aref for every row (lane per row)
+      auto set_jar = [&](const float* xv) {
+        matvec_rows(jar, J, xv, nefc, nvp, lane);
+        for (int r = lane; r < nefc; r += kWave) jar[r] -= S[L.efc_aref + r];
+      };
+      // total cost at (x, Mx, jar): Gauss term + active half-quadratics (wave-uniform)
+      auto cost_of = [&](const float* xv, const float* Mxv) -> float {
         float g = 0.f;
         for (int i = lane; i < nv; i += kWave)
           g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
-        float c = 0.f;
         for (int r = lane; r < nefc; r += kWave) {
-          const float* J = S + L.efc_J + r * nv;
-          float v = -S[L.efc_aref + r];
-          for (int i = 0; i < nv; i++) v += J[i] * xv[i];
-          S[L.efc_jar + r] = v;
-          if (v < 0) c += 0.5f * S[L.efc_D + r] * v * v;
+          float v = jar[r];
+          if (v < 0.f) g += 0.5f * Dv[r] * v * v;
         }
-        return wave_sum(g + c);
+        return wave_sum(g);
       };
-      auto mulM = [&](float* out, const float* xv) {
-        for (int i = lane; i < nv; i += kWave) {
-          float s = 0.f;
-          const float* Mr = S + L.M + i * nv;
-          for (int j = 0; j < nv; j++) s += Mr[j] * xv[j];
-          out[i] = s;
-        }
-      };
-      // warmstart choice
-      for (int i = lane; i < nv; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
+      // warmstart: keep qacc_warmstart if its cost beats qacc_smooth
+      for (int i = lane; i < nvp; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
       sync();
-      mulM(S + L.Mx, S + L.x);
+      matvec_rows(S + L.Mx, S + L.M, S + L.x, nvp, nvp, lane);
+      set_jar(S + L.x);
       sync();
-      float cost_ws = eval_cost(S + L.x, S + L.Mx);
+      const float cost_ws = cost_of(S + L.x, S + L.Mx);
       sync();
-      float cost_sm = eval_cost(S + L.qacc_smooth, S + L.qfrc_smooth);
+      set_jar(S + L.qacc_smooth);
       sync();
+      const float cost_sm = cost_of(S + L.qacc_smooth, S + L.qfrc_smooth);
+      sync();
+      float cost;
       if (cost_sm < cost_ws) {
-        for (int i = lane; i < nv; i += kWave) {
+        for (int i = lane; i < nvp; i += kWave) {
           S[L.x + i] = S[L.qacc_smooth + i];
           S[L.Mx + i] = S[L.qfrc_smooth + i];
         }
+        cost = cost_sm;
+      } else {
+        set_jar(S + L.x);
+        cost = cost_ws;
       }
       sync();
-      float cost = eval_cost(S + L.x, S + L.Mx);
-      sync();
       for (int iter = 0; iter < o.iterations; iter++) {
-        // gradient
-        for (int i = lane; i < nv; i += kWave) {
-          float g = S[L.Mx + i] - S[L.qfrc_smooth + i];
-          for (int r = 0; r < nefc; r++) {
-            float jar = S[L.efc_jar + r];
-            if (jar < 0) g += S[L.efc_J + r * nv + i] * S[L.efc_D + r] * jar;
-          }
-          S[L.grad + i] = g;
-        }
-        // Hessian H = M + J^T D J over active rows (lower triangle by element)
-        {
-          int cnt = nv * (nv + 1) / 2;
-          for (int e = lane; e < cnt; e += kWave) {
-            int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
-            while ((i + 1) * (i + 2) / 2 <= e) i++;
-            while (i * (i + 1) / 2 > e) i--;
-            int j = e - i * (i + 1) / 2;
-            float hsum = S[L.M + i * nv + j];
-            for (int r = 0; r < nefc; r++) {
-              float jar = S[L.efc_jar + r];
-              if (jar < 0) hsum += S[L.efc_J + r * nv + i] * S[L.efc_D + r] * S[L.efc_J + r * nv + j];
-            }
-            S[L.H + i * nv + j] = hsum;
-          }
-        }
+        // gradient = M x - qfrc_smooth + J_act^T (D jar)
+        const int nact = build_active(act, jar, nefc, lane);
+        for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
         sync();
+        jt_mul(S + L.grad, J, wv, act, nact, nvp, S + L.red, lane);
         float gn = 0.f;
-        for (int i = lane; i < nv; i += kWave) gn += S[L.grad + i] * S[L.grad + i];
+        for (int i = lane; i < nvp; i += kWave) {
+          float g = S[L.grad + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];
+          S[L.grad + i] = g;
+          S[L.srch + i] = -g;
+          gn += g * g;
+        }
         gn = sqrtf(wave_sum(gn));
         if (iter > 0 && scale * gn < o.tolerance) break;
-        chol_lds(S + L.H, nv, lane);
-        for (int i = lane; i < nv; i += kWave) S[L.srch + i] = -S[L.grad + i];
-        sync();
-        chol_solve_lds(S + L.H, nv, S + L.srch, lane);
-        mulM(S + L.Ms, S + L.srch);
-        float g1 = 0.f, g2 = 0.f, sn = 0.f;
+        // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
+        {
+          float A[2][16];
+          tiles_load(A, T, S + L.M, nvp);
+          tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
+          tiles_chol(A, T, Lm, nvp);
+        }
+        tiles_solve(Lm, S + L.srch, T.nb, nvp, lane);
+        matvec_rows(S + L.Ms, S + L.M, S + L.srch, nvp, nvp, lane);
+        matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
+        float g1 = 0.f, sn = 0.f;
         for (int i = lane; i < nv; i += kWave) {
-          float s = S[L.srch + i];
-          g1 += s * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
-          sn += s * s;
-        }
-        for (int r = lane; r < nefc; r += kWave) {
-          const float* J = S + L.efc_J + r * nv;
-          float js = 0.f;
-          for (int i = 0; i < nv; i++) js += J[i] * S[L.srch + i];
-          S[L.efc_Js + r] = js;
+          float sv = S[L.srch + i];
+          g1 += sv * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
+          sn += sv * sv;
         }
         sync();
+        float g2 = 0.f;
         for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
         g1 = wave_sum(g1);
         g2 = wave_sum(g2);
         sn = sqrtf(wave_sum(sn));
         const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
-        // line search (same algorithm as the oracle): derivative at alpha
+        // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
         auto ls_eval = [&](float alpha, float* der, float* der2) {
           float f1 = 0.f, f2 = 0.f;
           for (int r = lane; r < nefc; r += kWave) {
-            float js = S[L.efc_Js + r];
-            float v = S[L.efc_jar + r] + alpha * js;
+            float js = Js[r];
+            float v = jar[r] + alpha * js;
             if (v < 0) {
-              float Dr = S[L.efc_D + r];
+              float Dr = Dv[r];
               f1 += Dr * v * js;
               f2 += Dr * js * js;
             }
@@ -1136,8 +1369,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         if (d0 < 0) {
           float c0 = 0.f;
           for (int r = lane; r < nefc; r += kWave) {
-            float jar = S[L.efc_jar + r], js = S[L.efc_Js + r];
-            if (jar < 0 || (jar == 0 && js < 0)) c0 += S[L.efc_D + r] * js * js;
+            float ja = jar[r], js = Js[r];
+            if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
           }
           c0 = g2 + wave_sum(c0);
           float lo = 0.f, hi = -1.f, best = 0.f;
@@ -1157,29 +1390,27 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         }
         niter = iter + 1;
         if (alpha == 0.f) break;
-        for (int i = lane; i < nv; i += kWave) {
+        for (int i = lane; i < nvp; i += kWave) {
           S[L.x + i] += alpha * S[L.srch + i];
           S[L.Mx + i] += alpha * S[L.Ms + i];
         }
+        for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
         sync();
         float old = cost;
-        cost = eval_cost(S + L.x, S + L.Mx);
-        sync();
+        cost = cost_of(S + L.x, S + L.Mx);
         if (scale * (old - cost) < o.tolerance) break;
       }
-      // constraint forces and qfrc_constraint = J^T f
+      // constraint forces and qfrc_constraint = J^T f over the active rows
+      sync();
       for (int r = lane; r < nefc; r += kWave) {
-        float jar = S[L.efc_jar + r];
-        S[L.efc_force + r] = jar < 0 ? -S[L.efc_D + r] * jar : 0.f;
+        float ja = jar[r];
+        wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
       }
+      const int nact = build_active(act, jar, nefc, lane);
       sync();
-      for (int i = lane; i < nv; i += kWave) {
-        float f = 0.f;
-        for (int r = 0; r < nefc; r++) f += S[L.efc_J + r * nv + i] * S[L.efc_force + r];
-        S[L.qfrc_con + i] = f;
-      }
-      sync();
+      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, S + L.red, lane);
     }
+    STAMP(9);
     niter_last = niter;
     // =========================================================== post-constraint acc
     if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
@@ -1199,6 +1430,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       sync();
     }
+    STAMP(10);
     // =========================================================== sensors
     for (int s = lane; s < d.nsensor; s += kWave) {
       float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
@@ -1300,6 +1532,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         }
       }
     }
+    STAMP(11);
     // =========================================================== write kinematics outputs
     const bool last = (sub == nsubstep - 1);
     if (last) {
@@ -1376,19 +1609,18 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         atomicMax(&D.stats[5], niter_last);
       }
     }
+    STAMP(12);
     if (!integrate) break;
     // =========================================================== implicitfast / Euler
     sync();
     {
-      for (int i = lane; i < nv * nv; i += kWave) S[L.H + i] = S[L.M + i];
-      sync();
       const float* damping = MF(dof_damping);
-      for (int i = lane; i < nv; i += kWave) S[L.H + i * nv + i] += h * damping[i];
+      for (int i = lane; i < nvp; i += kWave) S[L.hdiag + i] = i < nv ? h * damping[i] : 0.f;
+      sync();
       if (o.integrator == 1) {
         const float* gear = MF(actuator_gear);
         const float* bias = MF(actuator_biasprm);
         const float* frange = MF(actuator_forcerange);
-        sync();
         for (int u = lane; u < nu; u += kWave) {
           if (m.actuator_forcelimited[u]) {
             float fo = S[L.act_force + u];
@@ -1398,13 +1630,23 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
           if (bv == 0.f) continue;
           int dof = m.jnt_dofadr[m.actuator_trnid[u]];
           float g = gear[u];
-          atomicAdd(S + L.H + dof * nv + dof, -h * g * g * bv);
+          atomicAdd(S + L.hdiag + dof, -h * g * g * bv);
         }
       }
-      for (int i = lane; i < nv; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
+      for (int i = lane; i < nvp; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
       sync();
-      chol_lds(S + L.H, nv, lane);
-      chol_solve_lds(S + L.H, nv, S + L.vtmp, lane);
+      {
+        float A[2][16];
+        tiles_load(A, T, S + L.M, nvp);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+          if (!(T.own[s2] && T.bi[s2] == T.bj[s2])) continue;
+#pragma unroll
+          for (int r = 0; r < 4; r++) A[s2][5 * r] += S[L.hdiag + 4 * T.bi[s2] + r];
+        }
+        tiles_chol(A, T, S + L.H, nvp);
+      }
+      tiles_solve(S + L.H, S + L.vtmp, T.nb, nvp, lane);
       for (int i = lane; i < nv; i += kWave) S[L.qvel + i] += h * S[L.vtmp + i];
       sync();
       for (int k = lane; k < d.njnt; k += kWave) {
@@ -1427,6 +1669,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       sync();
     }
   }
+  STAMP(13);
   // ------------------------------------------------------------- store state
   if (integrate) {
     for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];

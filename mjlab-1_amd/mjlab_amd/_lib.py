@@ -12,13 +12,13 @@ import os
 from ._capi import ModelDesc
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmjx355.so")
+LIB_PATH = os.environ.get("MJX355_LIB", os.path.join(_HERE, "libmjx355.so"))
 
 # Symbols declared in include/mjx355.h (kept in sync by tests/test_capi.py).
 EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_model_create",
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
-           "mjx_field_is_expanded", "mjx_sim_stats")
+           "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile")
 
 _lib = None
 
@@ -53,6 +53,7 @@ def lib() -> ctypes.CDLL:
   L.mjx_expand_field.argtypes = [vp, ctypes.c_char_p, vp]
   L.mjx_field_is_expanded.argtypes = [vp, ctypes.c_char_p]
   L.mjx_sim_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp]
+  L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
   for name in EXPORTS:
     if name not in ("mjx_last_error", "mjx_field_name", "mjx_model_desc_size"):
       getattr(L, name).restype = ci

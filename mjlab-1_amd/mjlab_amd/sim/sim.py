@@ -245,5 +245,11 @@ class Simulation:
     return dict(max_ncon=out[0], max_nefc=out[1], con_overflow=out[2], row_overflow=out[3],
                 unsupported=out[4], max_niter=out[5])
 
+  def profile(self) -> list[int]:
+    """Per-stage cycle sums (diagnostic MJX_STAMPS build only)."""
+    out = (ctypes.c_uint64 * 16)()
+    check(lib().mjx_sim_profile(self._sim, out, _stream_handle(self._torch_device)))
+    return list(out)
+
   def field(self, name: str) -> torch.Tensor:
     return field_tensor(self._sim, name)

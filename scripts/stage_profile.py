@@ -1,0 +1,27 @@
+"""Per-stage cycle breakdown of the step kernel (diagnostic -DMJX_STAMPS build)."""
+import os, sys
+os.environ["MJX355_LIB"] = os.path.join(os.path.dirname(__file__), "..", "mjlab-1_amd", "mjlab_amd", "libmjx355_stamps.so")
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mjlab-1_amd"))
+import torch
+from mjlab_amd.envs import make_env
+NAMES = ["kinematics", "com/cinert/cdof", "crb+M", "collision", "contact sort+params",
+         "constraints", "velocity+rne+act", "smooth solve", "subtree mom", "newton",
+         "post acc", "sensors", "outputs", "integrate"]
+for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
+  N = 4096
+  env = make_env(task, N, "cuda:0", seed=42)
+  env.reset()
+  g = torch.Generator(device="cuda:0"); g.manual_seed(0)
+  for i in range(40):
+    env.step(2 * torch.rand(N, env.action_manager.total_action_dim, device="cuda:0", generator=g) - 1)
+  p0 = env.sim.profile()
+  for i in range(20):
+    env.step(2 * torch.rand(N, env.action_manager.total_action_dim, device="cuda:0", generator=g) - 1)
+  p1 = env.sim.profile()
+  d = [b - a for a, b in zip(p0, p1)]
+  tot = sum(d)
+  nsub = 20 * env.cfg.decimation * N
+  print(f"== {task}: {tot / nsub:.0f} cycles per world-substep (s_memtime ticks)")
+  for i, n in enumerate(NAMES):
+    print(f"  {n:22s} {d[i] / nsub:10.0f}  {100 * d[i] / max(tot, 1):5.1f}%")
+  print("  stats", env.sim.stats())
