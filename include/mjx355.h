@@ -124,6 +124,9 @@ int mjx_sim_destroy(mjxSim* sim);
 int mjx_step(mjxSim* sim, int nsubstep, void* stream);
 /* mj_forward without integration (kinematics/sensors/acc for the current state). */
 int mjx_forward(mjxSim* sim, void* stream);
+/* mj_forward only on worlds where mask[w] != 0 (mask: device uint8[nworld]; NULL = all).
+ * Lets a sync-free (graph-captured) env step refresh just the worlds it reset. */
+int mjx_forward_masked(mjxSim* sim, const uint8_t* mask, void* stream);
 /* mj_resetData on worlds where mask[w] != 0 (mask: device uint8[nworld]; NULL = all). */
 int mjx_reset(mjxSim* sim, const uint8_t* mask, void* stream);
 

@@ -257,6 +257,8 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   e = hipMalloc((void**)&s->dparams, sizeof(mjx::Params));
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc params: ") + hipGetErrorString(e)); }
   if (sync_params(s, nullptr)) { delete s; return -1; }
+  e = mjx::prepare_step(host_params(s));
+  if (e != hipSuccess) { delete s; return fail(std::string("prepare: ") + hipGetErrorString(e)); }
   // initial state: mj_resetData
   if (mjx::launch_reset(d, s->dm, s->dd, nullptr, nworld, nullptr) != hipSuccess) {
     delete s;
@@ -280,15 +282,17 @@ int mjx_sim_destroy(mjxSim* s) {
 int mjx_step(mjxSim* s, int nsubstep, void* stream) {
   if (!s) return fail("null sim");
   if (nsubstep < 1) return fail("nsubstep must be >= 1");
-  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, nsubstep, 1,
+  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, nsubstep, 1, nullptr,
                                   (hipStream_t)stream);
   if (e != hipSuccess) return fail(std::string("step launch: ") + hipGetErrorString(e));
   return 0;
 }
 
-int mjx_forward(mjxSim* s, void* stream) {
+int mjx_forward(mjxSim* s, void* stream) { return mjx_forward_masked(s, nullptr, stream); }
+
+int mjx_forward_masked(mjxSim* s, const uint8_t* mask, void* stream) {
   if (!s) return fail("null sim");
-  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, 1, 0,
+  hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, 1, 0, mask,
                                   (hipStream_t)stream);
   if (e != hipSuccess) return fail(std::string("forward launch: ") + hipGetErrorString(e));
   return 0;

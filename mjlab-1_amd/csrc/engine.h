@@ -83,8 +83,9 @@ struct Params {
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.
+hipError_t prepare_step(const Params& host);  // one-time kernel attributes (not capturable)
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
-                       int integrate, hipStream_t stream);
+                       int integrate, const uint8_t* mask, hipStream_t stream);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
                         int nworld, hipStream_t stream);
 

@@ -498,7 +498,8 @@ __device__ float impedance(const float* si, float pos, float margin) {
 
 // --------------------------------------------------------------------------- kernel
 __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ P, int nworld,
-                                                     int nsubstep, int integrate) {
+                                                     int nsubstep, int integrate,
+                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
   const Dims& d = P->d;
   const Opt& o = P->o;
@@ -507,6 +508,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
   const Lds& L = P->L;
   const int w = blockIdx.x;
   if (w >= nworld) return;
+  if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   const int lane = threadIdx.x;
   int* Si = reinterpret_cast<int*>(S);
   int* ints = Si + L.ints;
@@ -1710,17 +1712,20 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
   if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
 }
 
+hipError_t prepare_step(const Params& host) {
+  size_t shmem = (size_t)host.L.total * 4;
+  if (shmem > 64 * 1024)
+    return hipFuncSetAttribute((const void*)step_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+  return hipSuccess;
+}
+
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
-                       int integrate, hipStream_t stream) {
+                       int integrate, const uint8_t* mask, hipStream_t stream) {
   if (nworld <= 0) return hipSuccess;
   size_t shmem = (size_t)host.L.total * 4;
-  if (shmem > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)step_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-    if (e != hipSuccess) return e;
-  }
   hipLaunchKernelGGL(step_kernel, dim3(nworld), dim3(kWave), shmem, stream, dev, nworld,
-                     nsubstep, integrate);
+                     nsubstep, integrate, mask);
   return hipGetLastError();
 }
 

@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("MJX355_LIB", os.path.join(_HERE, "libmjx355.so"))
 EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_model_create",
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
-           "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile")
+           "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile",
+           "mjx_forward_masked")
 
 _lib = None
 
@@ -45,6 +46,7 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_destroy.argtypes = [vp]
   L.mjx_step.argtypes = [vp, ci, vp]
   L.mjx_forward.argtypes = [vp, vp]
+  L.mjx_forward_masked.argtypes = [vp, vp, vp]
   L.mjx_reset.argtypes = [vp, vp, vp]
   L.mjx_field.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
   L.mjx_field_count.argtypes = [vp]

@@ -82,6 +82,8 @@ class ManagerBasedRlEnv:
     self.common_step_counter = 0
     self.episode_length_buf = torch.zeros(cfg.scene.num_envs, device=device, dtype=torch.long)
     self.render_mode = render_mode
+    self.sync_free = False
+    self._use_graph = False
     self.load_managers()
 
   @property
@@ -151,7 +153,87 @@ class ManagerBasedRlEnv:
     self.obs_buf = self.observation_manager.compute(update_history=True)
     return self.obs_buf, self.extras
 
+  # ------------------------------------------------------------------ sync-free + graph
+  def _step_sync_free(self, action: torch.Tensor):
+    """Same stages as step(), with every data-dependent branch turned into masks so the
+    whole env step is host-sync-free and can be captured in one HIP graph."""
+    self.action_manager.process_action(action)
+    for _ in range(self.cfg.decimation):
+      self.action_manager.apply_action()
+      self.scene.write_data_to_sim()
+      self.sim.step()
+      self.scene.update(dt=self.physics_dt)
+    self.episode_length_buf += 1
+    self.reset_buf = self.termination_manager.compute()
+    self.reset_terminated = self.termination_manager.terminated
+    self.reset_time_outs = self.termination_manager.time_outs
+    self.reward_buf = self.reward_manager.compute(dt=self.step_dt)
+    self._reset_masked(self.reset_buf)
+    self.scene.write_data_to_sim()
+    self.sim.forward(mask=self.reset_buf)
+    self.command_manager.compute(dt=self.step_dt)
+    if "interval" in self.event_manager.available_modes:
+      self.event_manager.apply_masked(mode="interval", dt=self.step_dt)
+    self.obs_buf = self.observation_manager.compute(update_history=True)
+    return self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs
+
+  def _reset_masked(self, mask: torch.Tensor) -> None:
+    self.sim.reset_masked(mask)
+    self.scene.reset_masked(mask)
+    if "reset" in self.event_manager.available_modes:
+      self.event_manager.apply_masked(mode="reset", mask=mask)
+    log = self.extras.setdefault("log", {})
+    for mgr in (self.action_manager, self.reward_manager, self.command_manager,
+                self.event_manager, self.termination_manager):
+      log.update(mgr.reset_masked(mask))
+    self.observation_manager.reset(None)
+    self.episode_length_buf.masked_fill_(mask, 0)
+
+  def _graph_key(self):
+    if not self.cfg.commands:
+      return ()
+    return tuple(repr(getattr(t.cfg, "ranges", None)) for t in self.command_manager._terms.values())
+
+  def enable_graph(self, capture: bool = True) -> None:
+    """Switch to the sync-free step; with capture=True record it into a HIP graph
+    (replayed per step; re-recorded when a curriculum changes command ranges)."""
+    self.sync_free = True
+    self._use_graph = capture
+    self._graph = None
+    self._static_action = torch.zeros(self.num_envs, self.action_manager.total_action_dim,
+                                      device=self.device)
+
+  def _capture(self) -> None:
+    s = torch.cuda.Stream(device=self.device)
+    s.wait_stream(torch.cuda.current_stream(self.device))
+    with torch.cuda.stream(s):
+      for _ in range(2):  # warm up allocator + lazy tensors outside the capture
+        self._step_sync_free(self._static_action)
+    torch.cuda.current_stream(self.device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      self._graph_out = self._step_sync_free(self._static_action)
+    self._graph = g
+    self._graph_key_captured = self._graph_key()
+
   def step(self, action: torch.Tensor):
+    if getattr(self, "sync_free", False):
+      self.curriculum_manager.compute(env_ids=None)
+      self._sim_step_counter += self.cfg.decimation
+      self.common_step_counter += 1
+      if not self._use_graph:
+        out = self._step_sync_free(action.to(self.device))
+        return (*out, self.extras)
+      if self._graph is None or self._graph_key() != self._graph_key_captured:
+        self._static_action.copy_(action)
+        self._capture()
+      self._static_action.copy_(action)
+      self._graph.replay()
+      self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs = self._graph_out
+      return (*self._graph_out, self.extras)
+    return self._step_eager(action)
+
+  def _step_eager(self, action: torch.Tensor):
     self.action_manager.process_action(action.to(self.device))
     for _ in range(self.cfg.decimation):
       self._sim_step_counter += 1

@@ -189,7 +189,9 @@ class SceneEntityCfg:
       if ids == list(range(total)) and not self.preserve_order:
         setattr(self, f"{kind}_ids", slice(None))
       else:
-        setattr(self, f"{kind}_ids", ids)
+        # device index tensor: indexing with it needs no host->device copy, so terms stay
+        # capturable in a HIP graph (a Python list index would upload every call)
+        setattr(self, f"{kind}_ids", torch.tensor(ids, dtype=torch.long, device=scene.device))
 
 
 # --------------------------------------------------------------------------- base
@@ -305,6 +307,15 @@ class ActionManager(ManagerBase):
     self._action[env_ids] = 0.0
     for t in self._terms.values():
       t.reset(env_ids=env_ids)
+    return {}
+
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    m = mask.unsqueeze(1)
+    for buf in (self._prev_prev_action, self._prev_action, self._action):
+      buf.masked_fill_(m, 0.0)
+    for t in self._terms.values():
+      if hasattr(t, "reset_masked"):
+        t.reset_masked(mask)
     return {}
 
   def process_action(self, action: torch.Tensor) -> None:
@@ -447,6 +458,17 @@ class RewardManager(ManagerBase):
       c.func.reset(env_ids=env_ids)
     return extras
 
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    extras = {}
+    cnt = torch.clamp(mask.sum(), min=1).float()
+    for k, v in self._episode_sums.items():
+      extras["Episode_Reward/" + k] = (v * mask).sum() / cnt / self._env.max_episode_length_s
+      v.masked_fill_(mask, 0.0)
+    for c in _class_terms(self._term_cfgs):
+      if hasattr(c.func, "reset_masked"):
+        c.func.reset_masked(mask)
+    return extras
+
   def compute(self, dt: float) -> torch.Tensor:
     self._reward_buf.zero_()
     for i, (name, c) in enumerate(zip(self._term_names, self._term_cfgs)):
@@ -508,6 +530,9 @@ class TerminationManager(ManagerBase):
       c.func.reset(env_ids=env_ids)
     return extras
 
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    return {"Episode_Termination/" + k: (v & mask).sum() for k, v in self._term_dones.items()}
+
   def compute(self) -> torch.Tensor:
     self._truncated_buf.zero_()
     self._terminated_buf.zero_()
@@ -549,10 +574,30 @@ class CommandTerm(ManagerTermBase):
   def compute(self, dt: float) -> None:
     self._update_metrics()
     self.time_left -= dt
-    ids = (self.time_left <= 0.0).nonzero().flatten()
-    if len(ids) > 0:
-      self._resample(ids)
+    if getattr(self._env, "sync_free", False):
+      self._resample_masked(self.time_left <= 0.0)
+    else:
+      ids = (self.time_left <= 0.0).nonzero().flatten()
+      if len(ids) > 0:
+        self._resample(ids)
     self._update_command()
+
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    cnt = torch.clamp(mask.sum(), min=1).float()
+    extras = {}
+    for k, v in self.metrics.items():
+      extras[k] = (v * mask).sum() / cnt
+      v.masked_fill_(mask, 0.0)
+    self.command_counter.masked_fill_(mask, 0)
+    self._resample_masked(mask)
+    return extras
+
+  def _resample_masked(self, mask: torch.Tensor) -> None:
+    lo, hi = self.cfg.resampling_time_range
+    fresh = torch.rand(self.num_envs, device=self.device) * (hi - lo) + lo
+    self.time_left.copy_(torch.where(mask, fresh, self.time_left))
+    self._resample_command_masked(mask)
+    self.command_counter += mask.long()
 
   def _resample(self, env_ids: torch.Tensor) -> None:
     if len(env_ids) != 0:
@@ -587,6 +632,13 @@ class CommandManager(ManagerBase):
         extras[f"Metrics/{name}/{k}"] = v
     return extras
 
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    extras = {}
+    for name, t in self._terms.items():
+      for k, v in t.reset_masked(mask).items():
+        extras[f"Metrics/{name}/{k}"] = v
+    return extras
+
   def compute(self, dt: float) -> None:
     for t in self._terms.values():
       t.compute(dt)
@@ -605,6 +657,9 @@ class NullCommandManager:
   active_terms: list = []
 
   def reset(self, env_ids=None):
+    return {}
+
+  def reset_masked(self, mask):
     return {}
 
   def compute(self, dt):
@@ -667,6 +722,36 @@ class EventManager(ManagerBase):
           ids = env_ids if isinstance(env_ids, torch.Tensor) else torch.arange(self.num_envs, device=self.device)
           self._interval_time_left[i][ids] = torch.rand(len(ids), device=self.device) * (hi - lo) + lo
     return {}
+
+  def reset_masked(self, mask: torch.Tensor) -> dict:
+    for i, c in enumerate(self._mode_term_cfgs.get("interval", [])):
+      if not c.is_global_time:
+        lo, hi = c.interval_range_s
+        fresh = torch.rand(self.num_envs, device=self.device) * (hi - lo) + lo
+        self._interval_time_left[i].copy_(torch.where(mask, fresh, self._interval_time_left[i]))
+    return {}
+
+  def apply_masked(self, mode: str, mask: torch.Tensor | None = None, dt: float | None = None) -> None:
+    """Sync-free variant for 'reset' (given a mask) and 'interval' (computes its own mask):
+    every term must provide a `.masked` implementation (graph-capturable)."""
+    for i, c in enumerate(self._mode_term_cfgs.get(mode, [])):
+      fn = getattr(c.func, "masked", None)
+      if fn is None:
+        raise NotImplementedError(f"event term {c.func} has no masked variant")
+      if mode == "interval":
+        if c.is_global_time:
+          raise NotImplementedError("global-time interval events are not graph-capturable")
+        tl = self._interval_time_left[i]
+        tl -= dt
+        m = tl < 1e-6
+        lo, hi = c.interval_range_s
+        fresh = torch.rand(self.num_envs, device=self.device) * (hi - lo) + lo
+        tl.copy_(torch.where(m, fresh, tl))
+        fn(self._env, m, **c.params)
+      else:
+        if c.min_step_count_between_reset != 0:
+          raise NotImplementedError("min_step_count_between_reset requires the eager path")
+        fn(self._env, mask, **c.params)
 
   def apply(self, mode: str, env_ids=None, dt: float | None = None,
             global_env_step_count: int | None = None) -> None:
@@ -738,6 +823,9 @@ class CurriculumManager(ManagerBase):
       c.func.reset(env_ids=env_ids)
     return extras
 
+  def reset_masked(self, mask) -> dict:
+    return self.reset(None)
+
   def compute(self, env_ids=None) -> None:
     if env_ids is None:
       env_ids = slice(None)
@@ -749,6 +837,9 @@ class NullCurriculumManager:
   active_terms: list = []
 
   def reset(self, env_ids=None):
+    return {}
+
+  def reset_masked(self, mask):
     return {}
 
   def compute(self, env_ids=None):

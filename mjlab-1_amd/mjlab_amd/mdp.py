@@ -191,7 +191,7 @@ def track_angular_velocity(env, std: float, command_name: str, asset_cfg=_ROBOT)
 
 def flat_orientation(env, std: float, asset_cfg=_ROBOT):
   a = env.scene[asset_cfg.name]
-  if isinstance(asset_cfg.body_ids, list) and asset_cfg.body_ids:
+  if not isinstance(asset_cfg.body_ids, slice) and len(asset_cfg.body_ids) > 0:
     q = a.data.body_link_quat_w[:, asset_cfg.body_ids, :].squeeze(1)
     g = quat_apply_inverse(q, a.data.gravity_vec_w)
   else:
@@ -266,7 +266,7 @@ class feet_swing_height:
     s = env.scene[sensor_name]
     h = a.data.site_pos_w[:, asset_cfg.site_ids, 2]
     in_air = s.data.found == 0
-    self.peak_heights = torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights)
+    self.peak_heights.copy_(torch.where(in_air, torch.maximum(self.peak_heights, h), self.peak_heights))
     first = s.compute_first_contact(dt=self.step_dt)
     active = _command_active(env, command_name, command_threshold)
     err = self.peak_heights / target_height - 1.0
@@ -274,7 +274,7 @@ class feet_swing_height:
     nland = torch.sum(first.float())
     env.extras["log"]["Metrics/peak_height_mean"] = (
       torch.sum(self.peak_heights * first.float()) / torch.clamp(nland, min=1))
-    self.peak_heights = torch.where(first, torch.zeros_like(self.peak_heights), self.peak_heights)
+    self.peak_heights.masked_fill_(first, 0.0)
     return cost
 
 
@@ -378,6 +378,69 @@ def push_by_setting_velocity(env, env_ids, velocity_range: dict, asset_cfg=_ROBO
   a.write_root_link_velocity_to_sim(vel, env_ids=env_ids)
 
 
+# ---- sync-free (mask) variants used by the graph-captured env step.  They draw randoms
+# for every env and commit them only where `mask` is set (same distributions as the
+# index-based versions above; RNG streams differ, as they do from the reference anyway).
+_CACHE: dict = {}
+
+
+def _range_tensor(spec, device):
+  key = (tuple(sorted(spec.items())) if isinstance(spec, dict) else tuple(spec), str(device))
+  if key not in _CACHE:
+    keys = ["x", "y", "z", "roll", "pitch", "yaw"]
+    vals = [spec.get(k, (0.0, 0.0)) for k in keys] if isinstance(spec, dict) else [spec]
+    _CACHE[key] = torch.tensor(vals, device=device, dtype=torch.float32)
+  return _CACHE[key]
+
+
+def _joint_ids_tensor(ids, device):
+  if isinstance(ids, (slice, torch.Tensor)):
+    return ids
+  key = ("jid", tuple(ids), str(device))
+  if key not in _CACHE:
+    _CACHE[key] = torch.tensor(ids, device=device, dtype=torch.long)
+  return _CACHE[key]
+
+
+def _reset_root_state_uniform_masked(env, mask, pose_range, velocity_range=None, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  n = env.num_envs
+  r = _range_tensor(pose_range, env.device)
+  ps = torch.rand(n, 6, device=env.device) * (r[:, 1] - r[:, 0]) + r[:, 0]
+  rs = a.data.default_root_state
+  pos = rs[:, 0:3] + ps[:, 0:3] + env.scene.env_origins
+  quat = quat_mul(rs[:, 3:7], quat_from_euler_xyz(ps[:, 3], ps[:, 4], ps[:, 5]))
+  vr = _range_tensor(velocity_range or {}, env.device)
+  vel = rs[:, 7:13] + torch.rand(n, 6, device=env.device) * (vr[:, 1] - vr[:, 0]) + vr[:, 0]
+  a.data.write_root_pose_masked(torch.cat([pos, quat], dim=-1), mask)
+  a.data.write_root_velocity_masked(vel, mask)
+
+
+def _reset_joints_by_offset_masked(env, mask, position_range, velocity_range, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  jid = _joint_ids_tensor(asset_cfg.joint_ids, env.device)
+  jp = a.data.default_joint_pos[:, jid]
+  jp = jp + torch.rand_like(jp) * (position_range[1] - position_range[0]) + position_range[0]
+  lim = a.data.soft_joint_pos_limits[:, jid]
+  jp = torch.minimum(torch.maximum(jp, lim[..., 0]), lim[..., 1])
+  jv = a.data.default_joint_vel[:, jid]
+  jv = jv + torch.rand_like(jv) * (velocity_range[1] - velocity_range[0]) + velocity_range[0]
+  a.data.write_joint_state_masked(jp, jv, mask, None if isinstance(jid, slice) else jid)
+
+
+def _push_by_setting_velocity_masked(env, mask, velocity_range, asset_cfg=_ROBOT):
+  a = env.scene[asset_cfg.name]
+  vel = a.data.root_link_vel_w
+  r = _range_tensor(velocity_range, env.device)
+  vel = vel + torch.rand_like(vel) * (r[:, 1] - r[:, 0]) + r[:, 0]
+  a.data.write_root_velocity_masked(vel, mask)
+
+
+reset_root_state_uniform.masked = _reset_root_state_uniform_masked
+reset_joints_by_offset.masked = _reset_joints_by_offset_masked
+push_by_setting_velocity.masked = _push_by_setting_velocity_masked
+
+
 def randomize_field(env, env_ids, field: str, ranges, operation: str = "abs",
                     distribution: str = "uniform", asset_cfg=_ROBOT, axes=None):
   """Domain randomization of one model field over the entity's elements
@@ -387,11 +450,11 @@ def randomize_field(env, env_ids, field: str, ranges, operation: str = "abs",
     env_ids = torch.arange(env.num_envs, device=env.device)
   t = getattr(env.sim.model, field)
   if field.startswith("geom_"):
-    ids = a.indexing.geom_ids if asset_cfg.geom_ids == slice(None) else a.indexing.geom_ids[asset_cfg.geom_ids]
+    ids = a.indexing.geom_ids[asset_cfg.geom_ids]
   elif field.startswith("body_"):
-    ids = a.indexing.body_ids if asset_cfg.body_ids == slice(None) else a.indexing.body_ids[asset_cfg.body_ids]
+    ids = a.indexing.body_ids[asset_cfg.body_ids]
   elif field.startswith("dof_"):
-    ids = a.indexing.joint_v_adr if asset_cfg.joint_ids == slice(None) else a.indexing.joint_v_adr[asset_cfg.joint_ids]
+    ids = a.indexing.joint_v_adr[asset_cfg.joint_ids]
   else:
     raise NotImplementedError(field)
   if axes is None:
@@ -473,6 +536,22 @@ class UniformVelocityCommand(CommandTerm):
       self.heading_target[env_ids] = r.uniform_(*rg.heading)
       self.is_heading_env[env_ids] = r.uniform_(0.0, 1.0) <= self.cfg.rel_heading_envs
     self.is_standing_env[env_ids] = r.uniform_(0.0, 1.0) <= self.cfg.rel_standing_envs
+
+  def _resample_command_masked(self, mask):
+    n = self.num_envs
+    rg = self.cfg.ranges
+    u = torch.rand(n, 6, device=self.device)
+    new = torch.stack([u[:, 0] * (rg.lin_vel_x[1] - rg.lin_vel_x[0]) + rg.lin_vel_x[0],
+                       u[:, 1] * (rg.lin_vel_y[1] - rg.lin_vel_y[0]) + rg.lin_vel_y[0],
+                       u[:, 2] * (rg.ang_vel_z[1] - rg.ang_vel_z[0]) + rg.ang_vel_z[0]], dim=1)
+    self.vel_command_b.copy_(torch.where(mask.unsqueeze(1), new, self.vel_command_b))
+    if self.cfg.heading_command:
+      ht = u[:, 3] * (rg.heading[1] - rg.heading[0]) + rg.heading[0]
+      self.heading_target.copy_(torch.where(mask, ht, self.heading_target))
+      self.is_heading_env.copy_(torch.where(mask, u[:, 4] <= self.cfg.rel_heading_envs,
+                                            self.is_heading_env))
+    self.is_standing_env.copy_(torch.where(mask, u[:, 5] <= self.cfg.rel_standing_envs,
+                                           self.is_standing_env))
 
   def _update_command(self):
     if self.cfg.heading_command:

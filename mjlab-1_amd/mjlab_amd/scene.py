@@ -121,6 +121,33 @@ class EntityData:
     if torque is not None:
       self.data.xfrc_applied[e, b, 3:6] = torque
 
+  # ---------------------------------------------------------------- masked (sync-free) writes
+  def write_root_pose_masked(self, pose, mask):
+    q = self.data.qpos
+    adr = self.indexing.free_joint_q_adr
+    q[:, adr] = torch.where(mask.unsqueeze(1), pose, q[:, adr])
+
+  def write_root_velocity_masked(self, velocity, mask):
+    q = self.data.qpos
+    quat_w = q[:, self.indexing.free_joint_q_adr[3:7]]
+    ang_b = quat_apply_inverse(quat_w, velocity[:, 3:])
+    v = self.data.qvel
+    adr = self.indexing.free_joint_v_adr
+    v[:, adr] = torch.where(mask.unsqueeze(1), torch.cat([velocity[:, :3], ang_b], -1), v[:, adr])
+
+  def write_joint_state_masked(self, position, velocity, mask, joint_ids=None):
+    jid = joint_ids if joint_ids is not None else slice(None)
+    qa = self.indexing.joint_q_adr[jid]
+    va = self.indexing.joint_v_adr[jid]
+    m = mask.unsqueeze(1)
+    self.data.qpos[:, qa] = torch.where(m, position, self.data.qpos[:, qa])
+    self.data.qvel[:, va] = torch.where(m, velocity, self.data.qvel[:, va])
+
+  def clear_state_masked(self, mask):
+    m = mask.unsqueeze(1)
+    for t in (self.joint_pos_target, self.joint_vel_target, self.joint_effort_target):
+      t.masked_fill_(m, 0.0)
+
   def clear_state(self, env_ids=None):
     e = slice(None) if env_ids is None else env_ids
     self.joint_pos_target[e] = 0.0
@@ -395,6 +422,9 @@ class Entity:
   def reset(self, env_ids=None):
     self._data.clear_state(env_ids)
 
+  def reset_masked(self, mask):
+    self._data.clear_state_masked(mask)
+
 
 class BuiltinSensor:
   """View into sensordata for one MJCF sensor (sensor/builtin_sensor.py:327-335)."""
@@ -414,6 +444,9 @@ class BuiltinSensor:
     pass
 
   def reset(self, env_ids=None):
+    pass
+
+  def reset_masked(self, mask):
     pass
 
 
@@ -487,6 +520,14 @@ class ContactSensor:
     for k in ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time"):
       self._air[k][e] = 0.0
     self._air["last_time"][e] = self._data.time[e]
+
+  def reset_masked(self, mask):
+    if self._air is None:
+      return
+    m = mask.unsqueeze(1)
+    for k in ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time"):
+      self._air[k].masked_fill_(m, 0.0)
+    self._air["last_time"].copy_(torch.where(mask, self._data.time, self._air["last_time"]))
 
   def update(self, dt):
     if self._air is None or "found" not in self._fields:
@@ -582,6 +623,12 @@ class Scene:
       e.reset(env_ids)
     for s in self._sensors.values():
       s.reset(env_ids)
+
+  def reset_masked(self, mask):
+    for e in self._entities.values():
+      e.reset_masked(mask)
+    for s in self._sensors.values():
+      s.reset_masked(mask)
 
   def update(self, dt: float):
     for e in self._entities.values():

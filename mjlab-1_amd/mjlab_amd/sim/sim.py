@@ -200,8 +200,26 @@ class Simulation:
         device=self._torch_device).reshape(model_field.shape[1:]).clone()
     return self._default_model_fields[field]
 
-  def forward(self) -> None:
-    check(lib().mjx_forward(self._sim, _stream_handle(self._torch_device)))
+  def forward(self, mask: torch.Tensor | None = None) -> None:
+    """mj_forward for all worlds, or only where the uint8/bool `mask` is set."""
+    stream = _stream_handle(self._torch_device)
+    if mask is None:
+      check(lib().mjx_forward(self._sim, stream))
+      return
+    m = self._as_mask(mask)
+    check(lib().mjx_forward_masked(self._sim, ctypes.c_void_p(m.data_ptr()), stream))
+
+  def _as_mask(self, mask: torch.Tensor) -> torch.Tensor:
+    if mask.dtype == torch.uint8 and mask.is_contiguous():
+      return mask
+    self._reset_mask.copy_(mask.to(torch.uint8))
+    return self._reset_mask
+
+  def reset_masked(self, mask: torch.Tensor) -> None:
+    """mj_resetData on worlds where `mask` is set (sync-free; graph-capturable)."""
+    m = self._as_mask(mask)
+    check(lib().mjx_reset(self._sim, ctypes.c_void_p(m.data_ptr()),
+                          _stream_handle(self._torch_device)))
 
   def step(self, nsubstep: int = 1) -> None:
     """One mj_step for every world (or `nsubstep` steps fused in one launch)."""
