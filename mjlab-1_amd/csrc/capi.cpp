@@ -75,7 +75,9 @@ struct mjxSim_ {
   mjx::Dims d;
   mjx::DModel dm;  // per-sim copy: expanded fields point to per-world buffers
   mjx::DData dd;
-  mjx::Lds lds;
+  mjx::Lds lds;       // full layout (global scratch)
+  mjx::Lds lds_ph[3];  // per-phase LDS carves
+  float* gscr = nullptr;
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
   std::vector<void*> expanded_allocs;
@@ -90,7 +92,9 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.o = s->model->o;
   p.m = s->dm;
   p.D = s->dd;
-  p.L = s->lds;
+  for (int i = 0; i < 3; i++) p.LP[i] = s->lds_ph[i];
+  p.LG = s->lds;
+  p.gscr = s->gscr;
   return p;
 }
 
@@ -201,10 +205,13 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   s->d.nconmax = nconmax;
   s->d.njmax = njmax;
   s->dm = model->dm;
-  s->lds = mjx::make_lds(s->d);
-  if ((size_t)s->lds.total * 4 > 160 * 1024) {
-    delete s;
-    return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
+  s->lds = mjx::make_lds(s->d, -1);
+  for (int i = 0; i < 3; i++) {
+    s->lds_ph[i] = mjx::make_lds(s->d, i);
+    if ((size_t)s->lds_ph[i].total * 4 > 160 * 1024) {
+      delete s;
+      return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
+    }
   }
   const mjx::Dims& d = s->d;
   // data arena: one allocation, 256-B aligned sub-buffers
@@ -221,8 +228,12 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_FLT
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
-  reserve("__prof", sizeof(unsigned long long) * 16);
-  hipError_t e = hipMalloc(&s->arena, off);
+  reserve("__prof", sizeof(unsigned long long) * 32);
+  hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->lds.total);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
+  e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->lds.total);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
+  e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }
   e = hipMemset(s->arena, 0, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
@@ -273,6 +284,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 int mjx_sim_destroy(mjxSim* s) {
   if (!s) return 0;
   if (s->arena) (void)hipFree(s->arena);
+  if (s->gscr) (void)hipFree(s->gscr);
   if (s->dparams) (void)hipFree(s->dparams);
   for (void* p : s->expanded_allocs) (void)hipFree(p);
   delete s;
@@ -394,7 +406,7 @@ int mjx_expand_field(mjxSim* s, const char* cname, void* stream) {
 
 int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
   if (!s || !out) return fail("null argument");
-  HIPCHK(hipMemcpyAsync(out, s->dd.prof, sizeof(uint64_t) * 16, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipMemcpyAsync(out, s->dd.prof, sizeof(uint64_t) * 32, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }

@@ -49,7 +49,7 @@ struct DData {
 #undef X_FLT
 #undef X_INT
   int32_t* stats;  // [8] global counters (atomics)
-  unsigned long long* prof;  // [16] stage cycle sums (diagnostic -DMJX_STAMPS build)
+  unsigned long long* prof;  // [32] stage cycle sums (diagnostic -DMJX_STAMPS build)
 };
 
 // Per-world LDS carve (offsets in 4-byte words).
@@ -69,7 +69,7 @@ struct Lds {
   int total;
 };
 
-Lds make_lds(const Dims& d);
+Lds make_lds(const Dims& d, int phase);  // phase -1: full layout (global scratch)
 
 // Everything a launch needs, resident in device memory (read through the scalar cache
 // instead of occupying ~500 SGPRs of kernarg space).
@@ -78,7 +78,9 @@ struct Params {
   Opt o;
   DModel m;
   DData D;
-  Lds L;
+  Lds LP[3];     // per-phase LDS carves (A, B, C)
+  Lds LG;        // full layout of the per-world global scratch
+  float* gscr;   // nworld * LG.total floats: phase hand-off buffers
 };
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of

@@ -16,6 +16,7 @@
 // Semantics follow the reference's mujoco_warp.step (src/mjlab/sim/sim.py:267-273)
 // stage by stage, restated in oracle/oracle.c (the parity checker).
 #include <float.h>
+#include <stdlib.h>
 #include <math.h>
 
 #include "engine.h"
@@ -37,35 +38,49 @@ enum { OBJ_SITE = 6 };
 enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
 
 // --------------------------------------------------------------------------- host: LDS
-Lds make_lds(const Dims& d) {
+// Phase masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4 (post/integrate).
+// ph < 0 carves the full layout (the per-world global scratch); otherwise only the regions
+// the phase touches, the rest at an offset past the allocation (never accessed).
+Lds make_lds(const Dims& d, int ph) {
   Lds L{};
   int o = 0;
-  auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };  // 16-B aligned carve
+  const int bit = ph < 0 ? 7 : (1 << ph);
+  constexpr int kAbsent = 1 << 24;
+  auto take = [&](int n, int phases) {
+    if (!(phases & bit)) return kAbsent;
+    int r = o;
+    o += (n + 3) & ~3;  // 16-B aligned carve
+    return r;
+  };
   const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
-  L.qpos = take(d.nq); L.qvel = take(nv); L.ctrl = take(d.nu); L.qacc_ws = take(nv);
-  L.qfrc_applied = take(nv); L.xfrc = take(6 * nb);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
-  L.ximat = take(9 * nb); L.xanchor = take(3 * d.njnt); L.xaxis = take(3 * d.njnt);
-  L.stmass = take(nb); L.subtree_com = take(3 * nb); L.cinert = take(10 * nb);
-  L.crb = take(10 * nb); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.stlin = take(3 * nb);
-  L.stang = take(3 * nb);
-  L.cdof = take(6 * nv); L.cdofdot = take(6 * nv);
-  L.gxpos = take(3 * d.ngeom); L.gxmat = take(9 * d.ngeom);
-  L.sxpos = take(3 * d.nsite); L.sxmat = take(9 * d.nsite);
-  L.M = take(nv * nv); L.H = take(nv * nv);
-  L.qfrc_bias = take(nv); L.qfrc_passive = take(nv); L.qfrc_act = take(nv);
-  L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv); L.x = take(nv); L.Mx = take(nv);
-  L.grad = take(nv); L.srch = take(nv); L.Ms = take(nv); L.qfrc_con = take(nv);
-  L.vtmp = take(nv); L.act_force = take(d.nu); L.act_len = take(d.nu); L.act_vel = take(d.nu);
-  L.con_g1 = take(C); L.con_g2 = take(C); L.con_key = take(C); L.con_dist = take(C);
-  L.con_pos = take(3 * C); L.con_frame = take(9 * C); L.con_mu = take(2 * C);
-  L.con_solref = take(2 * C); L.con_solimp = take(5 * C); L.con_imargin = take(C);
-  L.con_dim = take(C); L.con_efc = take(C);
-  L.efc_J = take(R * nv); L.efc_aref = take(R); L.efc_D = take(R); L.efc_jar = take(R);
-  L.efc_Js = take(R); L.efc_force = take(R); L.efc_cid = take(R); L.efc_type = take(R);
-  L.efc_act = take(R); L.hdiag = take(nv);
-  L.red = take(5 * kWave);
-  L.ints = take(8);
+  constexpr int A = 1, B = 2, Cp = 4;
+  L.ints = take(8, A | B | Cp);
+  L.qpos = take(d.nq, A | Cp); L.qvel = take(nv, A | Cp); L.ctrl = take(d.nu, A);
+  L.qacc_ws = take(nv, B | Cp); L.qfrc_applied = take(nv, A); L.xfrc = take(6 * nb, A);
+  L.xpos = take(3 * nb, A); L.xquat = take(4 * nb, A); L.xmat = take(9 * nb, A);
+  L.xipos = take(3 * nb, A); L.ximat = take(9 * nb, A); L.xanchor = take(3 * d.njnt, A);
+  L.xaxis = take(3 * d.njnt, A);
+  L.stmass = take(nb, A); L.subtree_com = take(3 * nb, A | Cp); L.cinert = take(10 * nb, A);
+  L.crb = take(10 * nb, A); L.cvel = take(6 * nb, A | Cp); L.cacc = take(6 * nb, A | Cp);
+  L.stlin = take(3 * nb, A); L.stang = take(3 * nb, A);
+  L.cdof = take(6 * nv, A | Cp); L.cdofdot = take(6 * nv, A | Cp);
+  L.gxpos = take(3 * d.ngeom, A); L.gxmat = take(9 * d.ngeom, A);
+  L.sxpos = take(3 * d.nsite, A | Cp); L.sxmat = take(9 * d.nsite, A | Cp);
+  L.M = take(nv * nv, A | B | Cp); L.H = take(nv * nv, A | B | Cp);
+  L.qfrc_bias = take(nv, A); L.qfrc_passive = take(nv, A); L.qfrc_act = take(nv, A);
+  L.qfrc_smooth = take(nv, A | B | Cp); L.qacc_smooth = take(nv, A | B); L.x = take(nv, B | Cp);
+  L.Mx = take(nv, B); L.grad = take(nv, B); L.srch = take(nv, B); L.Ms = take(nv, B);
+  L.qfrc_con = take(nv, B | Cp); L.vtmp = take(nv, Cp);
+  L.act_force = take(d.nu, A | Cp); L.act_len = take(d.nu, A); L.act_vel = take(d.nu, A);
+  L.con_g1 = take(C, A | Cp); L.con_g2 = take(C, A | Cp); L.con_key = take(C, A);
+  L.con_dist = take(C, A | Cp); L.con_pos = take(3 * C, A | Cp); L.con_frame = take(9 * C, A | Cp);
+  L.con_mu = take(2 * C, A | Cp); L.con_solref = take(2 * C, A); L.con_solimp = take(5 * C, A);
+  L.con_imargin = take(C, A); L.con_dim = take(C, A | Cp); L.con_efc = take(C, A | Cp);
+  L.efc_J = take(R * nv, B);  // phase A writes J rows straight to the global scratch
+  L.efc_aref = take(R, A | B); L.efc_D = take(R, A | B); L.efc_jar = take(R, B);
+  L.efc_Js = take(R, B); L.efc_force = take(R, B | Cp); L.efc_cid = take(R, A);
+  L.efc_type = take(R, A); L.efc_act = take(R, B); L.hdiag = take(nv, Cp);
+  L.red = take(5 * kWave, B);
   L.total = o;
   return L;
 }
@@ -149,10 +164,22 @@ __device__ __forceinline__ float dot6(const float* a, const float* b) {
 }
 
 // --------------------------------------------------------------------------- wave utils
+// Full-wave float sum, result wave-uniform.  DPP within each 16-lane row (quad swaps,
+// half-row and row mirrors), then the four row totals via v_readlane: no LDS crossbar
+// round trips (a __shfl_xor chain costs six ds_swizzle latencies).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
 }
 __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
   int x = v;
@@ -164,7 +191,18 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
   *total = __shfl(x, kWave - 1);
   return x - v;
 }
+// A workgroup is exactly one wavefront and LDS operations of a wavefront execute in
+// issue order, so cross-lane LDS hand-offs need only a compiler barrier (no s_barrier,
+// no lgkmcnt drain).  MJX_SYNCTHREADS=1 restores __syncthreads() for A/B checks.
+#ifndef MJX_SYNCTHREADS
+__device__ __forceinline__ void sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+#else
 __device__ __forceinline__ void sync() { __syncthreads(); }
+#endif
 
 #define MF(f) (m.f + (size_t)w * m.f##_ws)
 
@@ -177,8 +215,17 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
     if (lane == 0) atomicAdd((unsigned long long*)&D.prof[k], t_ - stamp_prev);   \
     stamp_prev = t_;                                                             \
   } while (0)
+// SUBSTAMP(k): nested split of the Newton stage into slots 16+ (does not advance STAMP).
+#define SUBSTAMP(k)                                                              \
+  do {                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+    if (lane == 0) atomicAdd((unsigned long long*)&D.prof[16 + (k)], t_ - sub_prev); \
+    sub_prev = t_;                                                               \
+  } while (0)
 #else
 #define STAMP(k) do {} while (0)
+#define SUBSTAMP(k) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- tiled SPD algebra
@@ -253,117 +300,6 @@ __device__ __forceinline__ void tiles_add_jtdj(float (&A)[2][16], const Tiles& T
     }
   }
 }
-// Right-looking blocked Cholesky; L written to Lm (row stride nvp, lower tiles).
-__device__ void tiles_chol(float (&A)[2][16], const Tiles& T, float* Lm, int nvp) {
-  for (int p = 0; p < T.nb; p++) {
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      if (!(T.own[s] && T.bi[s] == p && T.bj[s] == p)) continue;
-      float* a = A[s];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        float d = a[5 * c];
-#pragma unroll
-        for (int k = 0; k < c; k++) d -= a[4 * c + k] * a[4 * c + k];
-        d = sqrtf(fmaxf(d, MINVAL));
-        a[5 * c] = d;
-        float inv = 1.0f / d;
-#pragma unroll
-        for (int r = c + 1; r < 4; r++) {
-          float v = a[4 * r + c];
-#pragma unroll
-          for (int k = 0; k < c; k++) v -= a[4 * r + k] * a[4 * c + k];
-          a[4 * r + c] = v * inv;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        st4v(Lm + (4 * p + r) * nvp + 4 * p,
-             make_float4(a[4 * r], r >= 1 ? a[4 * r + 1] : 0.f, r >= 2 ? a[4 * r + 2] : 0.f,
-                         r >= 3 ? a[4 * r + 3] : 0.f));
-    }
-    sync();
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      if (!(T.own[s] && T.bj[s] == p && T.bi[s] > p)) continue;
-      float Lp[16];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        float4 v = ld4(Lm + (4 * p + r) * nvp + 4 * p);
-        Lp[4 * r] = v.x; Lp[4 * r + 1] = v.y; Lp[4 * r + 2] = v.z; Lp[4 * r + 3] = v.w;
-      }
-      float* a = A[s];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          float v = a[4 * r + c];
-#pragma unroll
-          for (int k = 0; k < c; k++) v -= a[4 * r + k] * Lp[4 * c + k];
-          a[4 * r + c] = v / Lp[5 * c];
-        }
-        st4v(Lm + (4 * T.bi[s] + r) * nvp + 4 * p,
-             make_float4(a[4 * r], a[4 * r + 1], a[4 * r + 2], a[4 * r + 3]));
-      }
-    }
-    sync();
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      if (!(T.own[s] && T.bj[s] > p)) continue;
-      float Li[16], Lj[16];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        float4 v = ld4(Lm + (4 * T.bi[s] + r) * nvp + 4 * p);
-        Li[4 * r] = v.x; Li[4 * r + 1] = v.y; Li[4 * r + 2] = v.z; Li[4 * r + 3] = v.w;
-        float4 u = ld4(Lm + (4 * T.bj[s] + r) * nvp + 4 * p);
-        Lj[4 * r] = u.x; Lj[4 * r + 1] = u.y; Lj[4 * r + 2] = u.z; Lj[4 * r + 3] = u.w;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-          for (int k = 0; k < 4; k++) A[s][4 * r + c] -= Li[4 * r + k] * Lj[4 * c + k];
-    }
-  }
-}
-// Solve (L L^T) x = b in place; x in LDS (length nvp, padded entries 0).
-__device__ void tiles_solve(const float* Lm, float* x, int nb, int nvp, int lane) {
-  for (int p = 0; p < nb; p++) {
-    if (lane == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        float v = x[4 * p + r];
-        for (int c = 0; c < r; c++) v -= Lm[(4 * p + r) * nvp + 4 * p + c] * x[4 * p + c];
-        x[4 * p + r] = v / Lm[(4 * p + r) * nvp + 4 * p + r];
-      }
-    }
-    sync();
-    float4 xp = ld4(x + 4 * p);
-    for (int i = 4 * (p + 1) + lane; i < nvp; i += kWave) {
-      float4 l = ld4(Lm + i * nvp + 4 * p);
-      x[i] -= l.x * xp.x + l.y * xp.y + l.z * xp.z + l.w * xp.w;
-    }
-    sync();
-  }
-  for (int p = nb - 1; p >= 0; p--) {
-    if (lane == 0) {
-#pragma unroll
-      for (int r = 3; r >= 0; r--) {
-        float v = x[4 * p + r];
-        for (int c = r + 1; c < 4; c++) v -= Lm[(4 * p + c) * nvp + 4 * p + r] * x[4 * p + c];
-        x[4 * p + r] = v / Lm[(4 * p + r) * nvp + 4 * p + r];
-      }
-    }
-    sync();
-    float4 xp = ld4(x + 4 * p);
-    for (int i = lane; i < 4 * p; i += kWave) {
-      x[i] -= Lm[(4 * p) * nvp + i] * xp.x + Lm[(4 * p + 1) * nvp + i] * xp.y +
-              Lm[(4 * p + 2) * nvp + i] * xp.z + Lm[(4 * p + 3) * nvp + i] * xp.w;
-    }
-    sync();
-  }
-}
 // out[i] = Mm[i,:] . v for i < nrow (row stride nvp), v broadcast-read as float4.
 __device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const float* v, int nrow,
                                             int nvp, int lane) {
@@ -387,7 +323,7 @@ __device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const f
 }
 // out[c] = sum_k J[act[k], c] * wv[act[k]] (c < nvp).  Lanes split (column block, row
 // group); partial sums reduced through `part` (>= 64*4 floats).  Ends with a sync.
-__device__ void jt_mul(float* out, const float* J, const float* wv, const int* act, int nact,
+__device__ __forceinline__ void jt_mul(float* out, const float* J, const float* wv, const int* act, int nact,
                        int nvp, float* part, int lane) {
   const int nb = nvp >> 2;
   const int ng = kWave / nb;
@@ -421,6 +357,112 @@ __device__ __forceinline__ int build_active(int* act, const float* jar, int nefc
     base += __popcll(bal);
   }
   return base;
+}
+
+// --------------------------------------------------------------------------- register-row SPD
+// Lane i holds row i of an nvp x nvp SPD matrix in NR registers (NR = compile-time row
+// length >= nvp; rows/cols >= nvp are identity).  Cholesky and both triangular solves run
+// as v_readlane broadcast chains: no LDS round trips and no single-lane sections.
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+template <int NR>
+__device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int nvp, int lane) {
+  const int row = lane < nvp ? lane : 0;
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < nvp) v = ld4(Mm + row * nvp + c);
+    A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
+  }
+  if (lane >= nvp) {
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] = c == lane ? 1.f : 0.f;
+  }
+}
+// In-place right-looking Cholesky of the lower triangle: afterwards A[c] (c <= lane) is
+// L[lane][c] and rdiag = 1/L[lane][lane].  Entries above the diagonal are scratch; they
+// never feed the lower part (every broadcast reads a lower entry).
+template <int NR>
+__device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, int nvp, int lane) {
+  rdiag = 1.f;
+  // Padding rows/cols (>= nvp) are identity/zero, so the full NR sweep is exact there:
+  // no per-step guards (guards get hoisted into spilled SGPR masks).
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
+    A[j] *= r;
+    rdiag = lane == j ? r : rdiag;
+#pragma unroll
+    for (int k = j + 1; k < NR; k++) A[k] = fmaf(-A[j], rl(A[j], k), A[k]);
+  }
+}
+// Publish the strictly-lower part of L (row stride nvp) for the transposed solve.
+template <int NR>
+__device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float* Lm, int nvp, int lane) {
+  if (lane >= nvp) return;
+#pragma unroll
+  for (int c = 0; c < NR; c += 4)
+    if (c < nvp)
+      st4v(Lm + lane * nvp + c, make_float4(c < lane ? A[c] : 0.f, c + 1 < lane ? A[c + 1] : 0.f,
+                                            c + 2 < lane ? A[c + 2] : 0.f, c + 3 < lane ? A[c + 3] : 0.f));
+}
+// x (lane i holds x[i]) <- (L L^T)^-1 x.  Forward from the register rows, backward from
+// columns of the strictly-lower L in Lm (written by rows_store_strict, then synced).
+template <int NR>
+__device__ __forceinline__ float rows_solve(const float (&A)[NR], float rdiag, const float* Lm,
+                                            float x, int nvp, int lane) {
+  float y = x, out = 0.f;
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const float s = rl(y * rdiag, j);
+    out = lane == j ? s : out;
+    y = fmaf(-(lane > j ? A[j] : 0.f), s, y);
+  }
+  float Lc[NR];
+  const int col = lane < nvp ? lane : 0;
+#pragma unroll
+  for (int j = 0; j < NR; j++) Lc[j] = (j < nvp && lane < nvp) ? Lm[j * nvp + col] : 0.f;
+  y = out;
+  out = 0.f;
+#pragma unroll
+  for (int j = NR - 1; j >= 0; j--) {
+    const float s = rl(y * rdiag, j);
+    out = lane == j ? s : out;
+    y = fmaf(-Lc[j], s, y);
+  }
+  return out;
+}
+// Tiles (lower 4x4 blocks) -> LDS matrix (row stride nvp), for rows_load.
+__device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles& T, float* Mm, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      st4v(Mm + (4 * T.bi[s] + r) * nvp + 4 * T.bj[s],
+           make_float4(A[s][4 * r], A[s][4 * r + 1], A[s][4 * r + 2], A[s][4 * r + 3]));
+  }
+}
+// Factor the nvp x nvp SPD matrix in Mm (row stride nvp) and solve for vector v (LDS,
+// length nvp) in place.  Lm (nvp*nvp) receives the strictly-lower factor.  Lm may alias Mm.
+template <int NR>
+__device__ __forceinline__ void spd_factor_solve(const float* Mm, const float* diag_add, float* Lm,
+                                                 float* v, int nvp, int lane) {
+  float A[NR];
+  rows_load<NR>(A, Mm, nvp, lane);
+  if (diag_add && lane < nvp) {
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] += c == lane ? diag_add[lane] : 0.f;
+  }
+  float rd;
+  rows_chol<NR>(A, rd, nvp, lane);
+  rows_store_strict<NR>(A, Lm, nvp, lane);
+  sync();
+  float x = lane < nvp ? v[lane] : 0.f;
+  x = rows_solve<NR>(A, rd, Lm, x, nvp, lane);
+  if (lane < nvp) v[lane] = x;
+  sync();
 }
 
 // --------------------------------------------------------------------------- collision
@@ -464,7 +506,7 @@ __device__ __forceinline__ int sphere_sphere(const ConOut& co, int key, int g1, 
   return 1;
 }
 __device__ __forceinline__ float clamp01(float t) { return t < 0 ? 0 : (t > 1 ? 1 : t); }
-__device__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
+__device__ __forceinline__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
   V3 u = a1 - a0, v = b1 - b0, wv = a0 - b0;
   float a = dot(u, u), b = dot(u, v), c = dot(v, v), dd = dot(u, wv), e = dot(v, wv);
   float den = a * c - b * b, s, t;
@@ -483,7 +525,7 @@ __device__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
 }
 
 // --------------------------------------------------------------------------- impedance
-__device__ float impedance(const float* si, float pos, float margin) {
+__device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
   float dmin = fminf(MAXIMP, fmaxf(MINIMP, si[0])), dmax = fminf(MAXIMP, fmaxf(MINIMP, si[1]));
   float width = fmaxf(0.f, si[2]), mid = fminf(1.f, fmaxf(MINIMP, si[3])), power = fmaxf(1.f, si[4]);
   if (dmin == dmax || width <= MINVAL) return 0.5f * (dmin + dmax);
@@ -496,54 +538,51 @@ __device__ float impedance(const float* si, float pos, float margin) {
   return dmin + y * (dmax - dmin);
 }
 
-// --------------------------------------------------------------------------- kernel
-__global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ P, int nworld,
-                                                     int nsubstep, int integrate,
-                                                     const uint8_t* __restrict__ mask) {
+// --------------------------------------------------------------------------- kernels
+// One substep = three launches, each holding only its own working set in LDS (more
+// resident worlds per CU); hand-off through the per-world global scratch P->gscr, laid out
+// with the full carve P->LG:
+//   PH 0 (A): kinematics, com, CRB/M, velocity/RNE/actuation, smooth solve, subtree
+//             momenta, pos/vel sensors, collision, contact parameters, constraint rows
+//             (J rows written straight to the scratch);
+//   PH 1 (B): Newton solver;
+//   PH 2 (C): post-constraint acceleration, acc-stage sensors, contact forces, integration.
+__device__ __forceinline__ void cp4(float* dst, const float* src, int n, int lane) {
+  for (int i = 4 * lane; i < n; i += 4 * kWave) st4v(dst + i, ld4(src + i));
+}
+__device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DModel& m, int b, V3 p) {
+  if (b <= 0) return {0.f, 0.f, 0.f};
+  const float* cv = S + L.cvel + 6 * b;
+  return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+}
+
+template <int NR, int PH>
+__global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int nworld,
+                                                    int last, int integrate,
+                                                    const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
   const Dims& d = P->d;
   const Opt& o = P->o;
   const DModel& m = P->m;
   const DData& D = P->D;
-  const Lds& L = P->L;
+  const Lds& L = P->LP[PH];
+  const Lds& G = P->LG;
   const int w = blockIdx.x;
   if (w >= nworld) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
+  float* gw = P->gscr + (size_t)w * G.total;
   const int lane = threadIdx.x;
   int* Si = reinterpret_cast<int*>(S);
   int* ints = Si + L.ints;
   const int nv = d.nv, nb = d.nbody, nq = d.nq, nu = d.nu;
   const int nvp = (nv + 3) & ~3;
-  const Tiles T = make_tiles(nvp, lane);
+  const int nvq = (nvp + 3) & ~3;  // copy length of an nvp vector region
   const float h = o.timestep;
-  // zero every nvp-padded vector once (stages write only [0, nv))
-  for (int i = lane; i < nvp; i += kWave) {
-    S[L.qvel + i] = 0.f; S[L.qacc_ws + i] = 0.f; S[L.qfrc_applied + i] = 0.f;
-    S[L.qfrc_bias + i] = 0.f; S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f;
-    S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
-    S[L.grad + i] = 0.f; S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
-    S[L.vtmp + i] = 0.f;
-  }
-  sync();
-
-  // ------------------------------------------------------------- load state (coalesced)
-  for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
-  for (int i = lane; i < nv; i += kWave) {
-    S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
-    S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
-    S[L.qfrc_applied + i] = D.qfrc_applied[(size_t)w * nv + i];
-  }
-  for (int i = lane; i < nu; i += kWave) S[L.ctrl + i] = D.ctrl[(size_t)w * nu + i];
-  for (int i = lane; i < 6 * nb; i += kWave) S[L.xfrc + i] = D.xfrc_applied[(size_t)w * 6 * nb + i];
-  float time = D.time[w];
-  int any_xfrc = 0;
-  for (int i = lane; i < 6 * nb; i += kWave) any_xfrc |= (D.xfrc_applied[(size_t)w * 6 * nb + i] != 0.f);
-  any_xfrc = __any(any_xfrc);
-  sync();
+  (void)nq; (void)nu; (void)h;
 #ifdef MJX_STAMPS
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+  unsigned long long sub_prev = stamp_prev;
 #endif
-
   const float* body_pos = MF(body_pos);
   const float* body_quat = MF(body_quat);
   const float* body_ipos = MF(body_ipos);
@@ -553,9 +592,32 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
   const float* jnt_pos = MF(jnt_pos);
   const float* jnt_axis = MF(jnt_axis);
   const float* qpos0 = MF(qpos0);
+  (void)body_pos; (void)body_quat; (void)body_ipos; (void)body_iquat; (void)body_mass;
+  (void)body_inertia; (void)jnt_pos; (void)jnt_axis; (void)qpos0;
 
-  int niter_last = 0;
-  for (int sub = 0; sub < nsubstep; sub++) {
+  if constexpr (PH == 0) {
+    // ----------------------------------------------------------- phase A
+    for (int i = lane; i < nvp; i += kWave) {
+      S[L.qvel + i] = 0.f; S[L.qfrc_applied + i] = 0.f; S[L.qfrc_bias + i] = 0.f;
+      S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f; S[L.qfrc_smooth + i] = 0.f;
+      S[L.qacc_smooth + i] = 0.f;
+    }
+    sync();
+    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
+    for (int i = lane; i < nv; i += kWave) {
+      S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
+      S[L.qfrc_applied + i] = D.qfrc_applied[(size_t)w * nv + i];
+    }
+    for (int i = lane; i < nu; i += kWave) S[L.ctrl + i] = D.ctrl[(size_t)w * nu + i];
+    int any_xfrc = 0;
+    for (int i = lane; i < 6 * nb; i += kWave) {
+      float v = D.xfrc_applied[(size_t)w * 6 * nb + i];
+      S[L.xfrc + i] = v;
+      any_xfrc |= (v != 0.f);
+    }
+    any_xfrc = __any(any_xfrc);
+    float* Jg = gw + G.efc_J;
+    sync();
     // =========================================================== kinematics (levels)
     if (lane == 0) {
       S[L.xpos + 0] = S[L.xpos + 1] = S[L.xpos + 2] = 0;
@@ -758,6 +820,193 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
     }
     STAMP(2);
+    // =========================================================== velocity stage
+    if (lane < 6) S[L.cvel + lane] = 0;
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float v[6];
+        for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
+        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
+        for (int k = j0; k < j1; k++) {
+          int dof = m.jnt_dofadr[k];
+          if (m.jnt_type[k] == JNT_FREE) {
+            for (int a = 0; a < 3; a++) {
+              for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+            }
+            for (int a = 3; a < 6; a++) cross_motion(S + L.cdofdot + 6 * (dof + a), v, S + L.cdof + 6 * (dof + a));
+            for (int a = 3; a < 6; a++)
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+          } else {
+            cross_motion(S + L.cdofdot + 6 * dof, v, S + L.cdof + 6 * dof);
+            for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * dof + j] * S[L.qvel + dof];
+          }
+        }
+        for (int j = 0; j < 6; j++) S[L.cvel + 6 * b + j] = v[j];
+      }
+      sync();
+    }
+    // RNE (flg_acc = 0): cacc with gravity, body forces into crb scratch (reused as cfrc)
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+        float f1[6], iv[6], f2[6];
+        inert_mul(f1, S + L.cinert + 10 * b, a);
+        inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
+        cross_force(f2, S + L.cvel + 6 * b, iv);
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = f1[j] + f2[j];
+      }
+      sync();
+    }
+    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        float acc[6];
+        for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
+          int ch = m.body_child[k];
+          for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
+        }
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
+      }
+      sync();
+    }
+    {
+      const float* damping = MF(dof_damping);
+      const float* jstiff = MF(jnt_stiffness);
+      const float* qspring = MF(qpos_spring);
+      for (int i = lane; i < nv; i += kWave) {
+        S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * m.dof_bodyid[i]);
+        float pf = -damping[i] * S[L.qvel + i];
+        int j = m.dof_jntid[i];
+        int t = m.jnt_type[j];
+        if ((t == JNT_HINGE || t == JNT_SLIDE) && jstiff[j] != 0.f) {
+          int a = m.jnt_qposadr[j];
+          pf -= jstiff[j] * (S[L.qpos + a] - qspring[a]);
+        }
+        S[L.qfrc_passive + i] = pf;
+        S[L.qfrc_act + i] = 0.f;
+      }
+    }
+    sync();
+    // actuation: position / motor actuators on joints
+    {
+      const float* gear = MF(actuator_gear);
+      const float* gain = MF(actuator_gainprm);
+      const float* bias = MF(actuator_biasprm);
+      const float* frange = MF(actuator_forcerange);
+      const float* crange = MF(actuator_ctrlrange);
+      for (int u = lane; u < nu; u += kWave) {
+        int j = m.actuator_trnid[u];
+        int dof = m.jnt_dofadr[j], a = m.jnt_qposadr[j];
+        float g = gear[u];
+        float len = g * S[L.qpos + a], vel = g * S[L.qvel + dof];
+        float c = S[L.ctrl + u];
+        if (m.actuator_ctrllimited[u]) c = fminf(fmaxf(c, crange[2 * u]), crange[2 * u + 1]);
+        float f = gain[3 * u] * c + bias[3 * u] + bias[3 * u + 1] * len + bias[3 * u + 2] * vel;
+        if (m.actuator_forcelimited[u]) f = fminf(fmaxf(f, frange[2 * u]), frange[2 * u + 1]);
+        S[L.act_force + u] = f;
+        S[L.act_len + u] = len;
+        S[L.act_vel + u] = vel;
+        atomicAdd(S + L.qfrc_act + dof, g * f);
+      }
+    }
+    sync();
+    for (int i = lane; i < nv; i += kWave) {
+      float f = S[L.qfrc_passive + i] - S[L.qfrc_bias + i] + S[L.qfrc_applied + i] + S[L.qfrc_act + i];
+      if (any_xfrc) {
+        uint64_t bm = m.dof_bodymask[i];
+        const float* cd = S + L.cdof + 6 * i;
+        V3 cang = v3(cd), clin = v3(cd + 3);
+        for (int b = 1; b < nb; b++) {
+          if (!((bm >> b) & 1ull)) continue;
+          const float* xf = S + L.xfrc + 6 * b;
+          V3 jp = clin + cross(cang, v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+          f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
+        }
+      }
+      S[L.qfrc_smooth + i] = f;
+      S[L.qacc_smooth + i] = f;
+    }
+    // subtree momenta (for subtreeangmom sensors)
+    for (int b = lane; b < nb; b += kWave) {
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      st3(S + L.stlin + 3 * b, vc * body_mass[b]);
+      const float* Ri = S + L.ximat + 9 * b;
+      V3 wl = mulTv(Ri, v3(cv));
+      V3 hl = {body_inertia[3 * b] * wl.x, body_inertia[3 * b + 1] * wl.y, body_inertia[3 * b + 2] * wl.z};
+      st3(S + L.stang + 3 * b, mulv(Ri, hl));
+      // stash body com velocity in cacc? no: recompute when needed
+    }
+    sync();
+    STAMP(6);
+    // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
+    spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, nvp, lane);
+    STAMP(7);
+    // linear momentum of subtrees -> velocity of subtree com
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        V3 acc = v3(S + L.stlin + 3 * b);
+        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++)
+          acc = acc + v3(S + L.stlin + 3 * m.body_child[k]);
+        st3(S + L.stlin + 3 * b, acc);
+      }
+      sync();
+    }
+    for (int b = lane; b < nb; b += kWave) {
+      float sm = S[L.stmass + b];
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
+      st3(S + L.stlin + 3 * b, lin);
+    }
+    sync();
+    for (int b = lane; b < nb; b += kWave) {
+      if (b == 0) continue;
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
+      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * body_mass[b];
+      st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
+    }
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int p = m.level_body[i];
+        V3 acc = v3(S + L.stang + 3 * p);
+        for (int k = m.body_childadr[p]; k < m.body_childadr[p + 1]; k++) {
+          int b = m.body_child[k];
+          V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
+          V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
+          acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
+        }
+        st3(S + L.stang + 3 * p, acc);
+      }
+      sync();
+    }
+    STAMP(8);
     if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
     sync();
     // =========================================================== collision
@@ -978,10 +1227,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         // limits
         for (int r = 0; r < lim_total && r < nefc; r++) {
           int j = -1 - Si[L.efc_cid + r];
-          S[L.efc_J + r * nvp + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
+          Jg[r * nvp + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
         }
         if (i >= nv) {  // zero padding columns of the contact rows
-          for (int r = lim_total; r < nefc; r++) S[L.efc_J + r * nvp + i] = 0.f;
+          for (int r = lim_total; r < nefc; r++) Jg[r * nvp + i] = 0.f;
           continue;
         }
         uint64_t bm = m.dof_bodymask[i];
@@ -999,15 +1248,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
           float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
           int r0 = Si[L.con_efc + c];
           if (Si[L.con_dim + c] == 1) {
-            S[L.efc_J + r0 * nvp + i] = jn;
+            Jg[r0 * nvp + i] = jn;
           } else {
             float jt1 = fr[3] * jd.x + fr[4] * jd.y + fr[5] * jd.z;
             float jt2 = fr[6] * jd.x + fr[7] * jd.y + fr[8] * jd.z;
             float mu0 = S[L.con_mu + 2 * c], mu1 = S[L.con_mu + 2 * c + 1];
-            S[L.efc_J + (r0 + 0) * nvp + i] = jn + mu0 * jt1;
-            S[L.efc_J + (r0 + 1) * nvp + i] = jn - mu0 * jt1;
-            S[L.efc_J + (r0 + 2) * nvp + i] = jn + mu1 * jt2;
-            S[L.efc_J + (r0 + 3) * nvp + i] = jn - mu1 * jt2;
+            Jg[(r0 + 0) * nvp + i] = jn + mu0 * jt1;
+            Jg[(r0 + 1) * nvp + i] = jn - mu0 * jt1;
+            Jg[(r0 + 2) * nvp + i] = jn + mu1 * jt2;
+            Jg[(r0 + 3) * nvp + i] = jn - mu1 * jt2;
           }
         }
       }
@@ -1051,9 +1300,24 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
           K = -sref[0] / (dmax * dmax);
           B = -sref[1] / dmax;
         }
-        float vel = 0;
-        const float* J = S + L.efc_J + r * nvp;
-        for (int i = 0; i < nv; i++) vel += J[i] * S[L.qvel + i];
+        // efc_vel = J qvel, evaluated from the body velocities (cvel is the same chain sum)
+        float vel;
+        if (type == EFC_LIMIT) {
+          vel = S[L.efc_D + r] * S[L.qvel + m.jnt_dofadr[-1 - Si[L.efc_cid + r]]];
+        } else {
+          int c = Si[L.efc_cid + r];
+          V3 pc = v3(S + L.con_pos + 3 * c);
+          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
+          V3 v = point_vel(S, L, m, b2, pc) - point_vel(S, L, m, b1, pc);
+          const float* fr = S + L.con_frame + 9 * c;
+          vel = fr[0] * v.x + fr[1] * v.y + fr[2] * v.z;
+          if (type != EFC_FRICTIONLESS) {
+            int kr = r - Si[L.con_efc + c];
+            const float* t = fr + 3 * (1 + (kr >> 1));
+            float mu = S[L.con_mu + 2 * c + (kr >> 1)];
+            vel += ((kr & 1) ? -mu : mu) * (t[0] * v.x + t[1] * v.y + t[2] * v.z);
+          }
+        }
         S[L.efc_D + r] = 1.0f / Rr;
         S[L.efc_aref + r] = -B * vel - K * imp * (pos - margin);
       }
@@ -1063,381 +1327,13 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
     const int nefc = ints[1];
     ncon = ints[4];
     STAMP(5);
-    // =========================================================== velocity stage
-    if (lane < 6) S[L.cvel + lane] = 0;
-    sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
-        float v[6];
-        for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
-        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
-        for (int k = j0; k < j1; k++) {
-          int dof = m.jnt_dofadr[k];
-          if (m.jnt_type[k] == JNT_FREE) {
-            for (int a = 0; a < 3; a++) {
-              for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
-              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
-            }
-            for (int a = 3; a < 6; a++) cross_motion(S + L.cdofdot + 6 * (dof + a), v, S + L.cdof + 6 * (dof + a));
-            for (int a = 3; a < 6; a++)
-              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
-          } else {
-            cross_motion(S + L.cdofdot + 6 * dof, v, S + L.cdof + 6 * dof);
-            for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * dof + j] * S[L.qvel + dof];
-          }
-        }
-        for (int j = 0; j < 6; j++) S[L.cvel + 6 * b + j] = v[j];
-      }
-      sync();
-    }
-    // RNE (flg_acc = 0): cacc with gravity, body forces into crb scratch (reused as cfrc)
-    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
-    sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
-        float a[6];
-        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
-        for (int k = d0; k < d1 && d0 >= 0; k++)
-          for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
-        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
-        float f1[6], iv[6], f2[6];
-        inert_mul(f1, S + L.cinert + 10 * b, a);
-        inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
-        cross_force(f2, S + L.cvel + 6 * b, iv);
-        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = f1[j] + f2[j];
-      }
-      sync();
-    }
-    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        float acc[6];
-        for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
-          int ch = m.body_child[k];
-          for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
-        }
-        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
-      }
-      sync();
-    }
-    {
-      const float* damping = MF(dof_damping);
-      const float* jstiff = MF(jnt_stiffness);
-      const float* qspring = MF(qpos_spring);
-      for (int i = lane; i < nv; i += kWave) {
-        S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * m.dof_bodyid[i]);
-        float pf = -damping[i] * S[L.qvel + i];
-        int j = m.dof_jntid[i];
-        int t = m.jnt_type[j];
-        if ((t == JNT_HINGE || t == JNT_SLIDE) && jstiff[j] != 0.f) {
-          int a = m.jnt_qposadr[j];
-          pf -= jstiff[j] * (S[L.qpos + a] - qspring[a]);
-        }
-        S[L.qfrc_passive + i] = pf;
-        S[L.qfrc_act + i] = 0.f;
-      }
-    }
-    sync();
-    // actuation: position / motor actuators on joints
-    {
-      const float* gear = MF(actuator_gear);
-      const float* gain = MF(actuator_gainprm);
-      const float* bias = MF(actuator_biasprm);
-      const float* frange = MF(actuator_forcerange);
-      const float* crange = MF(actuator_ctrlrange);
-      for (int u = lane; u < nu; u += kWave) {
-        int j = m.actuator_trnid[u];
-        int dof = m.jnt_dofadr[j], a = m.jnt_qposadr[j];
-        float g = gear[u];
-        float len = g * S[L.qpos + a], vel = g * S[L.qvel + dof];
-        float c = S[L.ctrl + u];
-        if (m.actuator_ctrllimited[u]) c = fminf(fmaxf(c, crange[2 * u]), crange[2 * u + 1]);
-        float f = gain[3 * u] * c + bias[3 * u] + bias[3 * u + 1] * len + bias[3 * u + 2] * vel;
-        if (m.actuator_forcelimited[u]) f = fminf(fmaxf(f, frange[2 * u]), frange[2 * u + 1]);
-        S[L.act_force + u] = f;
-        S[L.act_len + u] = len;
-        S[L.act_vel + u] = vel;
-        atomicAdd(S + L.qfrc_act + dof, g * f);
-      }
-    }
-    sync();
-    for (int i = lane; i < nv; i += kWave) {
-      float f = S[L.qfrc_passive + i] - S[L.qfrc_bias + i] + S[L.qfrc_applied + i] + S[L.qfrc_act + i];
-      if (any_xfrc) {
-        uint64_t bm = m.dof_bodymask[i];
-        const float* cd = S + L.cdof + 6 * i;
-        V3 cang = v3(cd), clin = v3(cd + 3);
-        for (int b = 1; b < nb; b++) {
-          if (!((bm >> b) & 1ull)) continue;
-          const float* xf = S + L.xfrc + 6 * b;
-          V3 jp = clin + cross(cang, v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
-          f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
-        }
-      }
-      S[L.qfrc_smooth + i] = f;
-      S[L.qacc_smooth + i] = f;
-    }
-    // subtree momenta (for subtreeangmom sensors)
-    for (int b = lane; b < nb; b += kWave) {
-      const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
-      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      st3(S + L.stlin + 3 * b, vc * body_mass[b]);
-      const float* Ri = S + L.ximat + 9 * b;
-      V3 wl = mulTv(Ri, v3(cv));
-      V3 hl = {body_inertia[3 * b] * wl.x, body_inertia[3 * b + 1] * wl.y, body_inertia[3 * b + 2] * wl.z};
-      st3(S + L.stang + 3 * b, mulv(Ri, hl));
-      // stash body com velocity in cacc? no: recompute when needed
-    }
-    sync();
-    STAMP(6);
-    // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
-    {
-      float A[2][16];
-      tiles_load(A, T, S + L.M, nvp);
-      tiles_chol(A, T, S + L.H, nvp);
-    }
-    tiles_solve(S + L.H, S + L.qacc_smooth, T.nb, nvp, lane);
-    STAMP(7);
-    // linear momentum of subtrees -> velocity of subtree com
-    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        V3 acc = v3(S + L.stlin + 3 * b);
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++)
-          acc = acc + v3(S + L.stlin + 3 * m.body_child[k]);
-        st3(S + L.stlin + 3 * b, acc);
-      }
-      sync();
-    }
-    for (int b = lane; b < nb; b += kWave) {
-      float sm = S[L.stmass + b];
-      const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
-      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
-      st3(S + L.stlin + 3 * b, lin);
-    }
-    sync();
-    for (int b = lane; b < nb; b += kWave) {
-      if (b == 0) continue;
-      const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
-      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
-      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * body_mass[b];
-      st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
-    }
-    sync();
-    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int p = m.level_body[i];
-        V3 acc = v3(S + L.stang + 3 * p);
-        for (int k = m.body_childadr[p]; k < m.body_childadr[p + 1]; k++) {
-          int b = m.body_child[k];
-          V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
-          V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
-          acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
-        }
-        st3(S + L.stang + 3 * p, acc);
-      }
-      sync();
-    }
-    STAMP(8);
-    // =========================================================== Newton solver
-    int niter = 0;
-    if (nefc == 0) {
-      for (int i = lane; i < nvp; i += kWave) {
-        S[L.x + i] = S[L.qacc_smooth + i];
-        S[L.qfrc_con + i] = 0.f;
-      }
-      sync();
-    } else {
-      float* jar = S + L.efc_jar;
-      float* Js = S + L.efc_Js;
-      float* wv = S + L.efc_force;
-      const float* Dv = S + L.efc_D;
-      const float* J = S + L.efc_J;
-      int* act = Si + L.efc_act;
-      float* Lm = S + L.H;
-      const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
-      // jar = J x - aref for every row (lane per row)
-      auto set_jar = [&](const float* xv) {
-        matvec_rows(jar, J, xv, nefc, nvp, lane);
-        for (int r = lane; r < nefc; r += kWave) jar[r] -= S[L.efc_aref + r];
-      };
-      // total cost at (x, Mx, jar): Gauss term + active half-quadratics (wave-uniform)
-      auto cost_of = [&](const float* xv, const float* Mxv) -> float {
-        float g = 0.f;
-        for (int i = lane; i < nv; i += kWave)
-          g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
-        for (int r = lane; r < nefc; r += kWave) {
-          float v = jar[r];
-          if (v < 0.f) g += 0.5f * Dv[r] * v * v;
-        }
-        return wave_sum(g);
-      };
-      // warmstart: keep qacc_warmstart if its cost beats qacc_smooth
-      for (int i = lane; i < nvp; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
-      sync();
-      matvec_rows(S + L.Mx, S + L.M, S + L.x, nvp, nvp, lane);
-      set_jar(S + L.x);
-      sync();
-      const float cost_ws = cost_of(S + L.x, S + L.Mx);
-      sync();
-      set_jar(S + L.qacc_smooth);
-      sync();
-      const float cost_sm = cost_of(S + L.qacc_smooth, S + L.qfrc_smooth);
-      sync();
-      float cost;
-      if (cost_sm < cost_ws) {
-        for (int i = lane; i < nvp; i += kWave) {
-          S[L.x + i] = S[L.qacc_smooth + i];
-          S[L.Mx + i] = S[L.qfrc_smooth + i];
-        }
-        cost = cost_sm;
-      } else {
-        set_jar(S + L.x);
-        cost = cost_ws;
-      }
-      sync();
-      for (int iter = 0; iter < o.iterations; iter++) {
-        // gradient = M x - qfrc_smooth + J_act^T (D jar)
-        const int nact = build_active(act, jar, nefc, lane);
-        for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
-        sync();
-        jt_mul(S + L.grad, J, wv, act, nact, nvp, S + L.red, lane);
-        float gn = 0.f;
-        for (int i = lane; i < nvp; i += kWave) {
-          float g = S[L.grad + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];
-          S[L.grad + i] = g;
-          S[L.srch + i] = -g;
-          gn += g * g;
-        }
-        gn = sqrtf(wave_sum(gn));
-        if (iter > 0 && scale * gn < o.tolerance) break;
-        // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
-        {
-          float A[2][16];
-          tiles_load(A, T, S + L.M, nvp);
-          tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
-          tiles_chol(A, T, Lm, nvp);
-        }
-        tiles_solve(Lm, S + L.srch, T.nb, nvp, lane);
-        matvec_rows(S + L.Ms, S + L.M, S + L.srch, nvp, nvp, lane);
-        matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
-        float g1 = 0.f, sn = 0.f;
-        for (int i = lane; i < nv; i += kWave) {
-          float sv = S[L.srch + i];
-          g1 += sv * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
-          sn += sv * sv;
-        }
-        sync();
-        float g2 = 0.f;
-        for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
-        g1 = wave_sum(g1);
-        g2 = wave_sum(g2);
-        sn = sqrtf(wave_sum(sn));
-        const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
-        // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
-        auto ls_eval = [&](float alpha, float* der, float* der2) {
-          float f1 = 0.f, f2 = 0.f;
-          for (int r = lane; r < nefc; r += kWave) {
-            float js = Js[r];
-            float v = jar[r] + alpha * js;
-            if (v < 0) {
-              float Dr = Dv[r];
-              f1 += Dr * v * js;
-              f2 += Dr * js * js;
-            }
-          }
-          *der = g1 + alpha * g2 + wave_sum(f1);
-          *der2 = g2 + wave_sum(f2);
-        };
-        float d0, dd0;
-        ls_eval(0.f, &d0, &dd0);
-        float alpha = 0.f;
-        if (d0 < 0) {
-          float c0 = 0.f;
-          for (int r = lane; r < nefc; r += kWave) {
-            float ja = jar[r], js = Js[r];
-            if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
-          }
-          c0 = g2 + wave_sum(c0);
-          float lo = 0.f, hi = -1.f, best = 0.f;
-          float a = -d0 / c0;
-          bool done = false;
-          for (int it = 0; it < o.ls_iterations; it++) {
-            float der, der2;
-            ls_eval(a, &der, &der2);
-            if (fabsf(der) <= gtol) { alpha = a; done = true; break; }
-            if (der < 0) { lo = a; best = a; } else { hi = a; }
-            float next = der2 > 0 ? a - der / der2 : a * 2;
-            if (hi >= 0 && !(next > lo && next < hi)) next = 0.5f * (lo + hi);
-            if (hi < 0 && next <= lo) next = lo + (lo > 0 ? lo : 1.0f);
-            a = next;
-          }
-          if (!done) alpha = best > 0 ? best : a;
-        }
-        niter = iter + 1;
-        if (alpha == 0.f) break;
-        for (int i = lane; i < nvp; i += kWave) {
-          S[L.x + i] += alpha * S[L.srch + i];
-          S[L.Mx + i] += alpha * S[L.Ms + i];
-        }
-        for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
-        sync();
-        float old = cost;
-        cost = cost_of(S + L.x, S + L.Mx);
-        if (scale * (old - cost) < o.tolerance) break;
-      }
-      // constraint forces and qfrc_constraint = J^T f over the active rows
-      sync();
-      for (int r = lane; r < nefc; r += kWave) {
-        float ja = jar[r];
-        wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
-      }
-      const int nact = build_active(act, jar, nefc, lane);
-      sync();
-      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, S + L.red, lane);
-    }
-    STAMP(9);
-    niter_last = niter;
-    // =========================================================== post-constraint acc
-    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
-    sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
-        float a[6];
-        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
-        for (int k = d0; k < d1 && d0 >= 0; k++)
-          for (int j = 0; j < 6; j++)
-            a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
-        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
-      }
-      sync();
-    }
-    STAMP(10);
     // =========================================================== sensors
     for (int s = lane; s < d.nsensor; s += kWave) {
       float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
       int obj = m.sensor_objid[s];
       int type = m.sensor_type[s];
+      // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
+      if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -1535,8 +1431,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
     }
     STAMP(11);
-    // =========================================================== write kinematics outputs
-    const bool last = (sub == nsubstep - 1);
+    // outputs final after phase A
     if (last) {
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 3 * nb; i += kWave) {
@@ -1551,10 +1446,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         D.xmat[wb * 9 + i] = S[L.xmat + i];
         D.ximat[wb * 9 + i] = S[L.ximat + i];
       }
-      for (int i = lane; i < 6 * nb; i += kWave) {
-        D.cvel[wb * 6 + i] = S[L.cvel + i];
-        D.cacc[wb * 6 + i] = S[L.cacc + i];
-      }
+      for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
       size_t wg = (size_t)w * d.ngeom;
       for (int i = lane; i < 3 * d.ngeom; i += kWave) D.geom_xpos[wg * 3 + i] = S[L.gxpos + i];
       for (int i = lane; i < 9 * d.ngeom; i += kWave) D.geom_xmat[wg * 9 + i] = S[L.gxmat + i];
@@ -1563,12 +1455,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];
       for (int i = lane; i < nv; i += kWave) {
         size_t k = (size_t)w * nv + i;
-        D.qacc[k] = S[L.x + i];
         D.qacc_smooth[k] = S[L.qacc_smooth + i];
         D.qfrc_bias[k] = S[L.qfrc_bias + i];
         D.qfrc_passive[k] = S[L.qfrc_passive + i];
         D.qfrc_actuator[k] = S[L.qfrc_act + i];
-        D.qfrc_constraint[k] = S[L.qfrc_con + i];
         D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
       }
       for (int u = lane; u < nu; u += kWave) {
@@ -1585,8 +1475,437 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
         for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
         for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? S[L.con_frame + 9 * c + t] : 0.f;
+      }
+      if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
+    }
+    // hand-off to phases B and C
+    const int C = d.nconmax;
+    const int nr4 = (nefc + 3) & ~3;
+    cp4(gw + G.M, S + L.M, nvp * nvp, lane);
+    cp4(gw + G.qacc_smooth, S + L.qacc_smooth, nvq, lane);
+    cp4(gw + G.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
+    cp4(gw + G.act_force, S + L.act_force, (nu + 3) & ~3, lane);
+    cp4(gw + G.cdof, S + L.cdof, 6 * nvp, lane);
+    cp4(gw + G.cdofdot, S + L.cdofdot, 6 * nvp, lane);
+    cp4(gw + G.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
+    cp4(gw + G.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
+    cp4(gw + G.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
+    cp4(gw + G.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    const int C4 = (C + 3) & ~3;
+    cp4(gw + G.con_g1, S + L.con_g1, C4, lane);
+    cp4(gw + G.con_g2, S + L.con_g2, C4, lane);
+    cp4(gw + G.con_dist, S + L.con_dist, C4, lane);
+    cp4(gw + G.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
+    cp4(gw + G.con_frame, S + L.con_frame, (9 * C + 3) & ~3, lane);
+    cp4(gw + G.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
+    cp4(gw + G.con_dim, S + L.con_dim, C4, lane);
+    cp4(gw + G.con_efc, S + L.con_efc, C4, lane);
+    cp4(gw + G.efc_aref, S + L.efc_aref, nr4, lane);
+    cp4(gw + G.efc_D, S + L.efc_D, nr4, lane);
+    cp4(gw + G.ints, S + L.ints, 8, lane);
+    STAMP(14);
+  } else if constexpr (PH == 1) {
+    // ----------------------------------------------------------- phase B (Newton)
+    const Tiles T = make_tiles(nvp, lane);
+    for (int i = lane; i < nvp; i += kWave) {
+      S[L.qacc_ws + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f; S[L.grad + i] = 0.f;
+      S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
+    }
+    sync();
+    for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
+    cp4(S + L.ints, gw + G.ints, 8, lane);
+    cp4(S + L.M, gw + G.M, nvp * nvp, lane);
+    cp4(S + L.qacc_smooth, gw + G.qacc_smooth, nvq, lane);
+    cp4(S + L.qfrc_smooth, gw + G.qfrc_smooth, nvq, lane);
+    sync();
+    const int nefc = ints[1];
+    int ncon = ints[4];
+    (void)ncon;
+    {
+      const int nr4 = (nefc + 3) & ~3;
+      cp4(S + L.efc_J, gw + G.efc_J, nefc * nvp, lane);
+      cp4(S + L.efc_aref, gw + G.efc_aref, nr4, lane);
+      cp4(S + L.efc_D, gw + G.efc_D, nr4, lane);
+    }
+    sync();
+    STAMP(15);
+    // =========================================================== Newton solver
+    int niter = 0;
+    if (nefc == 0) {
+      for (int i = lane; i < nvp; i += kWave) {
+        S[L.x + i] = S[L.qacc_smooth + i];
+        S[L.qfrc_con + i] = 0.f;
+      }
+      sync();
+    } else {
+      float* jar = S + L.efc_jar;
+      float* Js = S + L.efc_Js;
+      float* wv = S + L.efc_force;
+      const float* Dv = S + L.efc_D;
+      const float* J = S + L.efc_J;
+      int* act = Si + L.efc_act;
+      float* Lm = S + L.H;
+      const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
+#ifdef MJX_STAMPS
+      sub_prev = __builtin_amdgcn_s_memtime();
+#endif
+      // jar = J x - aref for every row (lane per row)
+      auto set_jar = [&](const float* xv) {
+        matvec_rows(jar, J, xv, nefc, nvp, lane);
+        for (int r = lane; r < nefc; r += kWave) jar[r] -= S[L.efc_aref + r];
+      };
+      // total cost at (x, Mx, jar): Gauss term + active half-quadratics (wave-uniform)
+      auto cost_of = [&](const float* xv, const float* Mxv) -> float {
+        float g = 0.f;
+        for (int i = lane; i < nv; i += kWave)
+          g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
+        for (int r = lane; r < nefc; r += kWave) {
+          float v = jar[r];
+          if (v < 0.f) g += 0.5f * Dv[r] * v * v;
+        }
+        return wave_sum(g);
+      };
+      // warmstart: keep qacc_warmstart if its cost beats qacc_smooth
+      for (int i = lane; i < nvp; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
+      sync();
+      matvec_rows(S + L.Mx, S + L.M, S + L.x, nvp, nvp, lane);
+      set_jar(S + L.x);
+      sync();
+      const float cost_ws = cost_of(S + L.x, S + L.Mx);
+      sync();
+      set_jar(S + L.qacc_smooth);
+      sync();
+      const float cost_sm = cost_of(S + L.qacc_smooth, S + L.qfrc_smooth);
+      sync();
+      float cost;
+      if (cost_sm < cost_ws) {
+        for (int i = lane; i < nvp; i += kWave) {
+          S[L.x + i] = S[L.qacc_smooth + i];
+          S[L.Mx + i] = S[L.qfrc_smooth + i];
+        }
+        cost = cost_sm;
+      } else {
+        set_jar(S + L.x);
+        cost = cost_ws;
+      }
+      sync();
+      SUBSTAMP(0);
+      for (int iter = 0; iter < o.iterations; iter++) {
+        // gradient = M x - qfrc_smooth + J_act^T (D jar)
+        const int nact = build_active(act, jar, nefc, lane);
+        for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
+        sync();
+        jt_mul(S + L.grad, J, wv, act, nact, nvp, S + L.red, lane);
+        float gn = 0.f;
+        for (int i = lane; i < nvp; i += kWave) {
+          float g = S[L.grad + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];
+          S[L.grad + i] = g;
+          S[L.srch + i] = -g;
+          gn += g * g;
+        }
+        gn = sqrtf(wave_sum(gn));
+        SUBSTAMP(1);
+        if (iter > 0 && scale * gn < o.tolerance) break;
+        // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
+        {
+          float A[2][16];
+          tiles_load(A, T, S + L.M, nvp);
+          tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
+          tiles_store(A, T, Lm, nvp);
+        }
+        sync();
+        SUBSTAMP(2);
+        {
+          float R[NR];
+          rows_load<NR>(R, Lm, nvp, lane);
+          float rd;
+          rows_chol<NR>(R, rd, nvp, lane);
+          rows_store_strict<NR>(R, Lm, nvp, lane);
+          sync();
+          SUBSTAMP(3);
+          float xs = lane < nvp ? S[L.srch + lane] : 0.f;
+          xs = rows_solve<NR>(R, rd, Lm, xs, nvp, lane);
+          if (lane < nvp) S[L.srch + lane] = xs;
+          sync();
+        }
+        SUBSTAMP(4);
+        matvec_rows(S + L.Ms, S + L.M, S + L.srch, nvp, nvp, lane);
+        matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
+        float g1 = 0.f, sn = 0.f;
+        for (int i = lane; i < nv; i += kWave) {
+          float sv = S[L.srch + i];
+          g1 += sv * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
+          sn += sv * sv;
+        }
+        sync();
+        float g2 = 0.f;
+        for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
+        g1 = wave_sum(g1);
+        g2 = wave_sum(g2);
+        sn = sqrtf(wave_sum(sn));
+        const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
+        SUBSTAMP(5);
+        // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
+        // The derivative is a sum of O(nefc) terms; once |der| is within its fp32
+        // rounding floor the root of the piecewise-linear derivative has been found to
+        // working precision (gtol itself, 1e-10 relative by default, is an fp64 target).
+        auto ls_eval = [&](float alpha, float* der, float* der2, float* noise) {
+          float f1 = 0.f, f2 = 0.f, fa = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float js = Js[r];
+            float v = jar[r] + alpha * js;
+            if (v < 0) {
+              float Dr = Dv[r];
+              float t = Dr * v * js;
+              f1 += t;
+              fa += fabsf(t);
+              f2 += Dr * js * js;
+            }
+          }
+          f1 = wave_sum(f1);
+          f2 = wave_sum(f2);
+          fa = wave_sum(fa);
+          *der = g1 + alpha * g2 + f1;
+          *der2 = g2 + f2;
+          *noise = 64.f * FLT_EPSILON * (fabsf(g1) + fabsf(alpha * g2) + fa);
+        };
+        float d0, dd0, nz0;
+        ls_eval(0.f, &d0, &dd0, &nz0);
+        float alpha = 0.f;
+        if (d0 < 0) {
+          float c0 = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float ja = jar[r], js = Js[r];
+            if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
+          }
+          c0 = g2 + wave_sum(c0);
+          float lo = 0.f, hi = -1.f, best = 0.f;
+          float a = -d0 / c0;
+          bool done = false;
+          for (int it = 0; it < o.ls_iterations; it++) {
+            float der, der2, nz;
+            ls_eval(a, &der, &der2, &nz);
+            if (fabsf(der) <= fmaxf(gtol, nz)) { alpha = a; done = true; break; }
+            if (der < 0) { lo = a; best = a; } else { hi = a; }
+            float next = der2 > 0 ? a - der / der2 : a * 2;
+            if (hi >= 0 && !(next > lo && next < hi)) next = 0.5f * (lo + hi);
+            if (hi < 0 && next <= lo) next = lo + (lo > 0 ? lo : 1.0f);
+            a = next;
+          }
+          if (!done) alpha = best > 0 ? best : a;
+        }
+        niter = iter + 1;
+        SUBSTAMP(6);
+        if (alpha == 0.f) break;
+        for (int i = lane; i < nvp; i += kWave) {
+          S[L.x + i] += alpha * S[L.srch + i];
+          S[L.Mx + i] += alpha * S[L.Ms + i];
+        }
+        for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
+        sync();
+        float old = cost;
+        cost = cost_of(S + L.x, S + L.Mx);
+        SUBSTAMP(7);
+        if (scale * (old - cost) < o.tolerance) break;
+      }
+      // constraint forces and qfrc_constraint = J^T f over the active rows
+      sync();
+      for (int r = lane; r < nefc; r += kWave) {
+        float ja = jar[r];
+        wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
+      }
+      const int nact = build_active(act, jar, nefc, lane);
+      sync();
+      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, S + L.red, lane);
+      SUBSTAMP(8);
+    }
+    STAMP(9);
+    if (lane == 0) ints[5] = niter;
+    sync();
+    cp4(gw + G.x, S + L.x, nvq, lane);
+    cp4(gw + G.qfrc_con, S + L.qfrc_con, nvq, lane);
+    cp4(gw + G.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
+    cp4(gw + G.ints, S + L.ints, 8, lane);
+    if (last) {
+      for (int i = lane; i < nv; i += kWave) {
+        size_t k = (size_t)w * nv + i;
+        D.qacc[k] = S[L.x + i];
+        D.qfrc_constraint[k] = S[L.qfrc_con + i];
+      }
+      if (lane == 0) D.solver_niter[w] = niter;
+    }
+    STAMP(14);
+  } else {
+    // ----------------------------------------------------------- phase C
+    for (int i = lane; i < nvp; i += kWave) {
+      S[L.qvel + i] = 0.f; S[L.qacc_ws + i] = 0.f; S[L.vtmp + i] = 0.f;
+    }
+    sync();
+    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
+    for (int i = lane; i < nv; i += kWave) {
+      S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
+      S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
+    }
+    float time = D.time[w];
+    const int C = d.nconmax;
+    const int C4 = (C + 3) & ~3;
+    cp4(S + L.ints, gw + G.ints, 8, lane);
+    cp4(S + L.M, gw + G.M, nvp * nvp, lane);
+    cp4(S + L.x, gw + G.x, nvq, lane);
+    cp4(S + L.qfrc_con, gw + G.qfrc_con, nvq, lane);
+    cp4(S + L.qfrc_smooth, gw + G.qfrc_smooth, nvq, lane);
+    cp4(S + L.act_force, gw + G.act_force, (nu + 3) & ~3, lane);
+    cp4(S + L.cdof, gw + G.cdof, 6 * nvp, lane);
+    cp4(S + L.cdofdot, gw + G.cdofdot, 6 * nvp, lane);
+    cp4(S + L.cvel, gw + G.cvel, (6 * nb + 3) & ~3, lane);
+    cp4(S + L.subtree_com, gw + G.subtree_com, (3 * nb + 3) & ~3, lane);
+    cp4(S + L.sxpos, gw + G.sxpos, (3 * d.nsite + 3) & ~3, lane);
+    cp4(S + L.sxmat, gw + G.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    cp4(S + L.con_g1, gw + G.con_g1, C4, lane);
+    cp4(S + L.con_g2, gw + G.con_g2, C4, lane);
+    cp4(S + L.con_dist, gw + G.con_dist, C4, lane);
+    cp4(S + L.con_pos, gw + G.con_pos, (3 * C + 3) & ~3, lane);
+    cp4(S + L.con_frame, gw + G.con_frame, (9 * C + 3) & ~3, lane);
+    cp4(S + L.con_mu, gw + G.con_mu, (2 * C + 3) & ~3, lane);
+    cp4(S + L.con_dim, gw + G.con_dim, C4, lane);
+    cp4(S + L.con_efc, gw + G.con_efc, C4, lane);
+    sync();
+    const int nefc = ints[1];
+    int ncon = ints[4];
+    const int niter_last = ints[5];
+    cp4(S + L.efc_force, gw + G.efc_force, (nefc + 3) & ~3, lane);
+    sync();
+    STAMP(15);
+    // =========================================================== post-constraint acc
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
+      for (int i = s0 + lane; i < s1; i += kWave) {
+        int b = m.level_body[i];
+        int p = m.body_parentid[b];
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++)
+            a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+      }
+      sync();
+    }
+    STAMP(10);
+    // =========================================================== sensors
+    for (int s = lane; s < d.nsensor; s += kWave) {
+      float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
+      int obj = m.sensor_objid[s];
+      int type = m.sensor_type[s];
+      // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
+      if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
+        int b = m.site_bodyid[obj];
+        const float* R = S + L.sxmat + 9 * obj;
+        const float* cv = S + L.cvel + 6 * b;
+        V3 rel = v3(S + L.sxpos + 3 * obj) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+        V3 r;
+        if (type == SENS_GYRO) {
+          r = mulTv(R, v3(cv));
+        } else {
+          V3 v = v3(cv + 3) + cross(v3(cv), rel);
+          if (type == SENS_VELOCIMETER) {
+            r = mulTv(R, v);
+          } else {
+            const float* ca = S + L.cacc + 6 * b;
+            V3 a = v3(ca + 3) + cross(v3(ca), rel) + cross(v3(cv), v);
+            r = mulTv(R, a);
+          }
+        }
+        out[0] = r.x; out[1] = r.y; out[2] = r.z;
+      } else if (type == SENS_SUBTREEANGMOM) {
+        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+      } else if (type == SENS_FRAMEPOS) {
+        const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
+        out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+      } else if (type == SENS_JOINTPOS) {
+        out[0] = S[L.qpos + m.jnt_qposadr[obj]];
+      } else if (type == SENS_JOINTVEL) {
+        out[0] = S[L.qvel + m.jnt_dofadr[obj]];
+      } else if (type == SENS_CONTACT) {
+        const int32_t* ip = m.sensor_intprm + 3 * s;
+        int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
+        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
+        int dim = m.sensor_dim[s];
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        int found = 0;
+        V3 net = {0, 0, 0};
+        int sel[8];
+        float key[8];
+        int nsel = 0;
+        for (int c = 0; c < ncon; c++) {
+          int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+          bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+          bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+          if (!a1 && !a2) continue;
+          found++;
+          // contact force in contact frame
+          int r0 = Si[L.con_efc + c];
+          V3 f = {0, 0, 0};
+          if (Si[L.con_dim + c] == 1) {
+            f.x = S[L.efc_force + r0];
+          } else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          net = net + fg * (a1 ? 1.f : -1.f);
+          float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
+                  : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
+          if (nsel < nslot || k < key[nsel - 1]) {
+            int pos = nsel < nslot ? nsel++ : nslot - 1;
+            while (pos > 0 && key[pos - 1] > k) { key[pos] = key[pos - 1]; sel[pos] = sel[pos - 1]; pos--; }
+            key[pos] = k;
+            sel[pos] = c * 2 + (a1 ? 0 : 1);
+          }
+        }
+        if (reduce == REDUCE_NETFORCE) {
+          if (bits & 1) out[0] = (float)found;
+          else if (bits & 2) { out[0] = net.x; out[1] = net.y; out[2] = net.z; }
+        } else {
+          for (int k = 0; k < nsel; k++) {
+            int c = sel[k] >> 1;
+            float sg = (sel[k] & 1) ? -1.f : 1.f;
+            float* oo = out + k * fdim;
+            if (bits & 1) oo[0] = (float)found;
+            else if (bits & 8) oo[0] = S[L.con_dist + c];
+            else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 2) {
+              int r0 = Si[L.con_efc + c];
+              if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
+              else {
+                float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+                float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+                oo[0] = e0 + e1 + e2 + e3;
+                oo[1] = (e0 - e1) * S[L.con_mu + 2 * c];
+                oo[2] = (e2 - e3) * S[L.con_mu + 2 * c + 1];
+              }
+            }
+          }
+        }
+      }
+    }
+    STAMP(11);
+    if (last) {
+      size_t wb = (size_t)w * nb;
+      for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
+      size_t wc = (size_t)w * d.nconmax;
+      for (int c = lane; c < d.nconmax; c += kWave) {
         V3 f = {0, 0, 0};
-        if (v && nefc > 0) {
+        if (c < ncon && nefc > 0) {
           int r0 = Si[L.con_efc + c];
           if (Si[L.con_dim + c] == 1) f.x = S[L.efc_force + r0];
           else {
@@ -1600,9 +1919,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
         D.contact_force[(wc + c) * 3 + 2] = f.z;
       }
       if (lane == 0) {
-        D.ncon[w] = ncon;
-        D.nefc[w] = nefc;
-        D.solver_niter[w] = niter_last;
         atomicMax(&D.stats[0], ints[0]);
         atomicMax(&D.stats[1], nefc);
         if (ints[3] & 1) atomicAdd(&D.stats[2], 1);
@@ -1612,7 +1928,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
     }
     STAMP(12);
-    if (!integrate) break;
+    if (integrate) {
+      sync();
     // =========================================================== implicitfast / Euler
     sync();
     {
@@ -1637,18 +1954,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       }
       for (int i = lane; i < nvp; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
       sync();
-      {
-        float A[2][16];
-        tiles_load(A, T, S + L.M, nvp);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; s2++) {
-          if (!(T.own[s2] && T.bi[s2] == T.bj[s2])) continue;
-#pragma unroll
-          for (int r = 0; r < 4; r++) A[s2][5 * r] += S[L.hdiag + 4 * T.bi[s2] + r];
-        }
-        tiles_chol(A, T, S + L.H, nvp);
-      }
-      tiles_solve(S + L.H, S + L.vtmp, T.nb, nvp, lane);
+      spd_factor_solve<NR>(S + L.M, S + L.hdiag, S + L.H, S + L.vtmp, nvp, lane);
       for (int i = lane; i < nv; i += kWave) S[L.qvel + i] += h * S[L.vtmp + i];
       sync();
       for (int k = lane; k < d.njnt; k += kWave) {
@@ -1670,16 +1976,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(const Params* __restrict__ 
       time += h;
       sync();
     }
-  }
-  STAMP(13);
-  // ------------------------------------------------------------- store state
-  if (integrate) {
-    for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];
-    for (int i = lane; i < nv; i += kWave) {
-      D.qvel[(size_t)w * nv + i] = S[L.qvel + i];
-      D.qacc_warmstart[(size_t)w * nv + i] = S[L.qacc_ws + i];
+
+      for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];
+      for (int i = lane; i < nv; i += kWave) {
+        D.qvel[(size_t)w * nv + i] = S[L.qvel + i];
+        D.qacc_warmstart[(size_t)w * nv + i] = S[L.qacc_ws + i];
+      }
+      if (lane == 0) D.time[w] = time;
     }
-    if (lane == 0) D.time[w] = time;
+    STAMP(13);
   }
 }
 
@@ -1712,20 +2017,55 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
   if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
 }
 
+// One instantiation per (register-row length NR: multiple of 8, >= padded nv; phase).
+using StepFn = void (*)(const Params*, int, int, int, const uint8_t*);
+template <int NR>
+static StepFn phase_fn_nr(int ph) {
+  return ph == 0 ? step_phase<NR, 0> : ph == 1 ? step_phase<NR, 1> : step_phase<NR, 2>;
+}
+static StepFn step_fn(int nv, int ph) {
+  const int nvp = (nv + 3) & ~3;
+  if (nvp <= 8) return phase_fn_nr<8>(ph);
+  if (nvp <= 16) return phase_fn_nr<16>(ph);
+  if (nvp <= 24) return phase_fn_nr<24>(ph);
+  if (nvp <= 32) return phase_fn_nr<32>(ph);
+  if (nvp <= 40) return phase_fn_nr<40>(ph);
+  if (nvp <= 48) return phase_fn_nr<48>(ph);
+  if (nvp <= 56) return phase_fn_nr<56>(ph);
+  return phase_fn_nr<64>(ph);
+}
+
+// Diagnostic: MJX355_LDS_PAD=<bytes> adds unused dynamic LDS per world, to measure how
+// throughput depends on resident worlds per CU.
+static size_t lds_bytes(const Params& host, int ph) {
+  static const long pad = [] {
+    const char* e = getenv("MJX355_LDS_PAD");
+    return e ? atol(e) : 0L;
+  }();
+  return (size_t)host.LP[ph].total * 4 + (size_t)(pad > 0 ? pad : 0);
+}
+
 hipError_t prepare_step(const Params& host) {
-  size_t shmem = (size_t)host.L.total * 4;
-  if (shmem > 64 * 1024)
-    return hipFuncSetAttribute((const void*)step_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+  for (int ph = 0; ph < 3; ph++) {
+    size_t shmem = lds_bytes(host, ph);
+    if (shmem > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)step_fn(host.d.nv, ph),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+      if (e != hipSuccess) return e;
+    }
+  }
   return hipSuccess;
 }
 
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream) {
   if (nworld <= 0) return hipSuccess;
-  size_t shmem = (size_t)host.L.total * 4;
-  hipLaunchKernelGGL(step_kernel, dim3(nworld), dim3(kWave), shmem, stream, dev, nworld,
-                     nsubstep, integrate, mask);
+  for (int sub = 0; sub < nsubstep; sub++) {
+    const int last = sub == nsubstep - 1;
+    for (int ph = 0; ph < 3; ph++)
+      hipLaunchKernelGGL(step_fn(host.d.nv, ph), dim3(nworld), dim3(kWave), lds_bytes(host, ph),
+                         stream, dev, nworld, last, integrate, mask);
+  }
   return hipGetLastError();
 }
 

@@ -19,9 +19,14 @@ for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
     env.step(2 * torch.rand(N, env.action_manager.total_action_dim, device="cuda:0", generator=g) - 1)
   p1 = env.sim.profile()
   d = [b - a for a, b in zip(p0, p1)]
-  tot = sum(d)
+  tot = sum(d[:16])
   nsub = 20 * env.cfg.decimation * N
   print(f"== {task}: {tot / nsub:.0f} cycles per world-substep (s_memtime ticks)")
   for i, n in enumerate(NAMES):
     print(f"  {n:22s} {d[i] / nsub:10.0f}  {100 * d[i] / max(tot, 1):5.1f}%")
-  print("  stats", env.sim.stats())
+  SUB = ["  nt: warmstart", "  nt: grad (active, J^T w)", "  nt: H assembly", "  nt: cholesky",
+         "  nt: solve", "  nt: M s, J s, dots", "  nt: line search", "  nt: update+cost",
+         "  nt: final forces"]
+  for i, n in enumerate(SUB):
+    print(f"  {n:22s} {d[16 + i] / nsub:10.0f}  {100 * d[16 + i] / max(tot, 1):5.1f}%")
+  print("  stats", env.sim.stats(), "mean niter", float(env.sim.field("solver_niter").float().mean()))
