@@ -75,8 +75,8 @@ struct mjxSim_ {
   mjx::Dims d;
   mjx::DModel dm;  // per-sim copy: expanded fields point to per-world buffers
   mjx::DData dd;
-  mjx::Lds lds;       // full layout (global scratch)
   mjx::Lds lds_ph[3];  // per-phase LDS carves
+  int gC = 0, gstride = 0;
   float* gscr = nullptr;
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
@@ -93,8 +93,9 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.m = s->dm;
   p.D = s->dd;
   for (int i = 0; i < 3; i++) p.LP[i] = s->lds_ph[i];
-  p.LG = s->lds;
   p.gscr = s->gscr;
+  p.gC = s->gC;
+  p.gstride = s->gstride;
   return p;
 }
 
@@ -205,7 +206,6 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   s->d.nconmax = nconmax;
   s->d.njmax = njmax;
   s->dm = model->dm;
-  s->lds = mjx::make_lds(s->d, -1);
   for (int i = 0; i < 3; i++) {
     s->lds_ph[i] = mjx::make_lds(s->d, i);
     if ((size_t)s->lds_ph[i].total * 4 > 160 * 1024) {
@@ -213,6 +213,8 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
   }
+  s->gC = (s->lds_ph[1].pack_len + 63) & ~63;
+  s->gstride = s->gC + ((s->lds_ph[2].pack_len + 63) & ~63);
   const mjx::Dims& d = s->d;
   // data arena: one allocation, 256-B aligned sub-buffers
   size_t off = 0;
@@ -229,9 +231,9 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
   reserve("__prof", sizeof(unsigned long long) * 32);
-  hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->lds.total);
+  hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
-  e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->lds.total);
+  e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
   e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }

@@ -65,11 +65,13 @@ struct Lds {
       con_solimp, con_imargin, con_dim, con_efc;
   int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_type, efc_act, hdiag;
   int red;      // 5*kWave scratch (J^T w partial sums)
-  int ints;     // small int block: [0]=ncon [1]=nefc [2]=nlimit [3]=overflow
+  int ints;     // small int block: [0]=raw ncon [1]=nefc [2]=nlimit [3]=flags [4]=ncon [5]=niter
+  int pack_len; // length of the phase's input pack (carved first; see make_lds)
+  int packC_b;  // C carve: offset of the part of the pack written by phase B
   int total;
 };
 
-Lds make_lds(const Dims& d, int phase);  // phase -1: full layout (global scratch)
+Lds make_lds(const Dims& d, int phase);  // phase 0/1/2 = A/B/C
 
 // Everything a launch needs, resident in device memory (read through the scalar cache
 // instead of occupying ~500 SGPRs of kernarg space).
@@ -79,8 +81,9 @@ struct Params {
   DModel m;
   DData D;
   Lds LP[3];     // per-phase LDS carves (A, B, C)
-  Lds LG;        // full layout of the per-world global scratch
-  float* gscr;   // nworld * LG.total floats: phase hand-off buffers
+  float* gscr;   // per-world hand-off scratch: [B pack | C pack], gstride floats per world
+  int gC;        // offset of the C pack inside a world's scratch
+  int gstride;
 };
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of

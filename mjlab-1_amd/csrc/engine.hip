@@ -38,49 +38,69 @@ enum { OBJ_SITE = 6 };
 enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
 
 // --------------------------------------------------------------------------- host: LDS
-// Phase masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4 (post/integrate).
-// ph < 0 carves the full layout (the per-world global scratch); otherwise only the regions
-// the phase touches, the rest at an offset past the allocation (never accessed).
+// Phase carves.  Masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4
+// (post/integrate).  A phase carve holds only the regions that phase touches (the rest sit
+// past the allocation and are never accessed).  Phase inputs are carved FIRST, in a fixed
+// order, so the per-world global scratch holds them as one contiguous "pack" with the same
+// internal offsets: B pack = [ints M qacc_smooth qfrc_smooth efc_aref efc_D efc_J] (J last,
+// so only the live rows are copied), C pack = [A outputs | B outputs].  Each phase then
+// fills its inputs with a single bulk copy.
 Lds make_lds(const Dims& d, int ph) {
   Lds L{};
-  int o = 0;
-  const int bit = ph < 0 ? 7 : (1 << ph);
-  constexpr int kAbsent = 1 << 24;
-  auto take = [&](int n, int phases) {
-    if (!(phases & bit)) return kAbsent;
-    int r = o;
-    o += (n + 3) & ~3;  // 16-B aligned carve
-    return r;
-  };
   const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
   constexpr int A = 1, B = 2, Cp = 4;
-  L.ints = take(8, A | B | Cp);
-  L.qpos = take(d.nq, A | Cp); L.qvel = take(nv, A | Cp); L.ctrl = take(d.nu, A);
-  L.qacc_ws = take(nv, B | Cp); L.qfrc_applied = take(nv, A); L.xfrc = take(6 * nb, A);
-  L.xpos = take(3 * nb, A); L.xquat = take(4 * nb, A); L.xmat = take(9 * nb, A);
-  L.xipos = take(3 * nb, A); L.ximat = take(9 * nb, A); L.xanchor = take(3 * d.njnt, A);
-  L.xaxis = take(3 * d.njnt, A);
-  L.stmass = take(nb, A); L.subtree_com = take(3 * nb, A | Cp); L.cinert = take(10 * nb, A);
-  L.crb = take(10 * nb, A); L.cvel = take(6 * nb, A | Cp); L.cacc = take(6 * nb, A | Cp);
-  L.stlin = take(3 * nb, A); L.stang = take(3 * nb, A);
-  L.cdof = take(6 * nv, A | Cp); L.cdofdot = take(6 * nv, A | Cp);
-  L.gxpos = take(3 * d.ngeom, A); L.gxmat = take(9 * d.ngeom, A);
-  L.sxpos = take(3 * d.nsite, A | Cp); L.sxmat = take(9 * d.nsite, A | Cp);
-  L.M = take(nv * nv, A | B | Cp); L.H = take(nv * nv, A | B | Cp);
-  L.qfrc_bias = take(nv, A); L.qfrc_passive = take(nv, A); L.qfrc_act = take(nv, A);
-  L.qfrc_smooth = take(nv, A | B | Cp); L.qacc_smooth = take(nv, A | B); L.x = take(nv, B | Cp);
-  L.Mx = take(nv, B); L.grad = take(nv, B); L.srch = take(nv, B); L.Ms = take(nv, B);
-  L.qfrc_con = take(nv, B | Cp); L.vtmp = take(nv, Cp);
-  L.act_force = take(d.nu, A | Cp); L.act_len = take(d.nu, A); L.act_vel = take(d.nu, A);
-  L.con_g1 = take(C, A | Cp); L.con_g2 = take(C, A | Cp); L.con_key = take(C, A);
-  L.con_dist = take(C, A | Cp); L.con_pos = take(3 * C, A | Cp); L.con_frame = take(9 * C, A | Cp);
-  L.con_mu = take(2 * C, A | Cp); L.con_solref = take(2 * C, A); L.con_solimp = take(5 * C, A);
-  L.con_imargin = take(C, A); L.con_dim = take(C, A | Cp); L.con_efc = take(C, A | Cp);
-  L.efc_J = take(R * nv, B);  // phase A writes J rows straight to the global scratch
-  L.efc_aref = take(R, A | B); L.efc_D = take(R, A | B); L.efc_jar = take(R, B);
-  L.efc_Js = take(R, B); L.efc_force = take(R, B | Cp); L.efc_cid = take(R, A);
-  L.efc_type = take(R, A); L.efc_act = take(R, B); L.hdiag = take(nv, Cp);
-  L.red = take(5 * kWave, B);
+  struct Spec { int Lds::*f; int n; int mask; };
+  const Spec all[] = {
+    {&Lds::ints, 8, A | B | Cp},
+    {&Lds::qpos, d.nq, A | Cp}, {&Lds::qvel, nv, A | Cp}, {&Lds::ctrl, d.nu, A},
+    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, A}, {&Lds::xfrc, 6 * nb, A},
+    {&Lds::xpos, 3 * nb, A}, {&Lds::xquat, 4 * nb, A}, {&Lds::xmat, 9 * nb, A},
+    {&Lds::xipos, 3 * nb, A}, {&Lds::ximat, 9 * nb, A}, {&Lds::xanchor, 3 * d.njnt, A},
+    {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, A}, {&Lds::subtree_com, 3 * nb, A | Cp},
+    {&Lds::cinert, 10 * nb, A}, {&Lds::crb, 10 * nb, A}, {&Lds::cvel, 6 * nb, A | Cp},
+    {&Lds::cacc, 6 * nb, A | Cp}, {&Lds::stlin, 3 * nb, A}, {&Lds::stang, 3 * nb, A},
+    {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
+    {&Lds::gxpos, 3 * d.ngeom, A}, {&Lds::gxmat, 9 * d.ngeom, A},
+    {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
+    {&Lds::M, nv * nv, A | B | Cp}, {&Lds::H, nv * nv, A | B | Cp},
+    {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
+    {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
+    {&Lds::Mx, nv, B}, {&Lds::grad, nv, B}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
+    {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, Cp},
+    {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
+    {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
+    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, A | Cp},
+    {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_solref, 2 * C, A}, {&Lds::con_solimp, 5 * C, A},
+    {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
+    {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
+    {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
+    {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
+    {&Lds::efc_type, R, A}, {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, Cp},
+    {&Lds::red, 5 * kWave, B},
+  };
+  static int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
+                                     &Lds::efc_aref, &Lds::efc_D, &Lds::efc_J};
+  static int Lds::* const packC[] = {
+      &Lds::cdof, &Lds::cdofdot, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
+      &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
+      &Lds::con_frame, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::M, &Lds::qfrc_smooth,
+      // written by phase B:
+      &Lds::ints, &Lds::x, &Lds::qfrc_con, &Lds::efc_force};
+  constexpr int kAbsent = 1 << 24;
+  for (const Spec& sp : all) L.*(sp.f) = kAbsent;
+  int o = 0;
+  auto take = [&](int Lds::*f) {
+    if (L.*f != kAbsent) return;
+    for (const Spec& sp : all)
+      if (sp.f == f) { L.*f = o; o += (sp.n + 3) & ~3; return; }  // 16-B aligned carve
+  };
+  if (ph == 1) for (auto f : packB) take(f);
+  if (ph == 2) for (auto f : packC) take(f);
+  L.pack_len = o;
+  L.packC_b = ph == 2 ? L.ints : 0;  // start of the phase-B-written part of the C pack
+  const int bit = 1 << ph;
+  for (const Spec& sp : all)
+    if (sp.mask & bit) take(sp.f);
   L.total = o;
   return L;
 }
@@ -550,6 +570,24 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
 __device__ __forceinline__ void cp4(float* dst, const float* src, int n, int lane) {
   for (int i = 4 * lane; i < n; i += 4 * kWave) st4v(dst + i, ld4(src + i));
 }
+// Bulk global->LDS copy of a phase's input pack: 8 float4 loads in flight per lane per
+// round trip (n is a multiple of 4 floats).
+__device__ __forceinline__ void cp_pack(float* __restrict__ dst, const float* __restrict__ src,
+                                        int n, int lane) {
+  for (int i0 = 4 * lane; i0 < n; i0 += 8 * 4 * kWave) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = i0 + k * 4 * kWave;
+      if (i < n) v[k] = ld4(src + i);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = i0 + k * 4 * kWave;
+      if (i < n) st4v(dst + i, v[k]);
+    }
+  }
+}
 __device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DModel& m, int b, V3 p) {
   if (b <= 0) return {0.f, 0.f, 0.f};
   const float* cv = S + L.cvel + 6 * b;
@@ -566,11 +604,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const DModel& m = P->m;
   const DData& D = P->D;
   const Lds& L = P->LP[PH];
-  const Lds& G = P->LG;
+  const Lds& LB = P->LP[1];
+  const Lds& LC = P->LP[2];
   const int w = blockIdx.x;
   if (w >= nworld) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
-  float* gw = P->gscr + (size_t)w * G.total;
+  float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
+  float* gc = gw + P->gC;
+  (void)LB; (void)LC; (void)gc;
   const int lane = threadIdx.x;
   int* Si = reinterpret_cast<int*>(S);
   int* ints = Si + L.ints;
@@ -616,7 +657,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       any_xfrc |= (v != 0.f);
     }
     any_xfrc = __any(any_xfrc);
-    float* Jg = gw + G.efc_J;
+    float* Jg = gw + LB.efc_J;
     sync();
     // =========================================================== kinematics (levels)
     if (lane == 0) {
@@ -1478,31 +1519,33 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
-    // hand-off to phases B and C
+    // hand-off: B pack (J rows already written) and the A part of the C pack
     const int C = d.nconmax;
-    const int nr4 = (nefc + 3) & ~3;
-    cp4(gw + G.M, S + L.M, nvp * nvp, lane);
-    cp4(gw + G.qacc_smooth, S + L.qacc_smooth, nvq, lane);
-    cp4(gw + G.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
-    cp4(gw + G.act_force, S + L.act_force, (nu + 3) & ~3, lane);
-    cp4(gw + G.cdof, S + L.cdof, 6 * nvp, lane);
-    cp4(gw + G.cdofdot, S + L.cdofdot, 6 * nvp, lane);
-    cp4(gw + G.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
-    cp4(gw + G.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
-    cp4(gw + G.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
-    cp4(gw + G.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
     const int C4 = (C + 3) & ~3;
-    cp4(gw + G.con_g1, S + L.con_g1, C4, lane);
-    cp4(gw + G.con_g2, S + L.con_g2, C4, lane);
-    cp4(gw + G.con_dist, S + L.con_dist, C4, lane);
-    cp4(gw + G.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
-    cp4(gw + G.con_frame, S + L.con_frame, (9 * C + 3) & ~3, lane);
-    cp4(gw + G.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
-    cp4(gw + G.con_dim, S + L.con_dim, C4, lane);
-    cp4(gw + G.con_efc, S + L.con_efc, C4, lane);
-    cp4(gw + G.efc_aref, S + L.efc_aref, nr4, lane);
-    cp4(gw + G.efc_D, S + L.efc_D, nr4, lane);
-    cp4(gw + G.ints, S + L.ints, 8, lane);
+    const int nr4 = (nefc + 3) & ~3;
+    cp4(gw + LB.ints, S + L.ints, 8, lane);
+    cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
+    cp4(gw + LB.qacc_smooth, S + L.qacc_smooth, nvq, lane);
+    cp4(gw + LB.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
+    cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
+    cp4(gw + LB.efc_D, S + L.efc_D, nr4, lane);
+    cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
+    cp4(gc + LC.cdofdot, S + L.cdofdot, 6 * nvp, lane);
+    cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
+    cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
+    cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
+    cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    cp4(gc + LC.act_force, S + L.act_force, (nu + 3) & ~3, lane);
+    cp4(gc + LC.con_g1, S + L.con_g1, C4, lane);
+    cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
+    cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
+    cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_frame, S + L.con_frame, (9 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
+    cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
+    cp4(gc + LC.M, S + L.M, nvp * nvp, lane);
+    cp4(gc + LC.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
     STAMP(14);
   } else if constexpr (PH == 1) {
     // ----------------------------------------------------------- phase B (Newton)
@@ -1513,21 +1556,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     sync();
     for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
-    cp4(S + L.ints, gw + G.ints, 8, lane);
-    cp4(S + L.M, gw + G.M, nvp * nvp, lane);
-    cp4(S + L.qacc_smooth, gw + G.qacc_smooth, nvq, lane);
-    cp4(S + L.qfrc_smooth, gw + G.qfrc_smooth, nvq, lane);
+    {
+      const int nefc_in = reinterpret_cast<const int*>(gw)[LB.ints + 1];
+      cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
+    }
     sync();
     const int nefc = ints[1];
     int ncon = ints[4];
     (void)ncon;
-    {
-      const int nr4 = (nefc + 3) & ~3;
-      cp4(S + L.efc_J, gw + G.efc_J, nefc * nvp, lane);
-      cp4(S + L.efc_aref, gw + G.efc_aref, nr4, lane);
-      cp4(S + L.efc_D, gw + G.efc_D, nr4, lane);
-    }
-    sync();
     STAMP(15);
     // =========================================================== Newton solver
     int niter = 0;
@@ -1722,10 +1758,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     STAMP(9);
     if (lane == 0) ints[5] = niter;
     sync();
-    cp4(gw + G.x, S + L.x, nvq, lane);
-    cp4(gw + G.qfrc_con, S + L.qfrc_con, nvq, lane);
-    cp4(gw + G.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
-    cp4(gw + G.ints, S + L.ints, 8, lane);
+    cp4(gc + LC.ints, S + L.ints, 8, lane);
+    cp4(gc + LC.x, S + L.x, nvq, lane);
+    cp4(gc + LC.qfrc_con, S + L.qfrc_con, nvq, lane);
+    cp4(gc + LC.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
     if (last) {
       for (int i = lane; i < nv; i += kWave) {
         size_t k = (size_t)w * nv + i;
@@ -1747,34 +1783,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
     }
     float time = D.time[w];
-    const int C = d.nconmax;
-    const int C4 = (C + 3) & ~3;
-    cp4(S + L.ints, gw + G.ints, 8, lane);
-    cp4(S + L.M, gw + G.M, nvp * nvp, lane);
-    cp4(S + L.x, gw + G.x, nvq, lane);
-    cp4(S + L.qfrc_con, gw + G.qfrc_con, nvq, lane);
-    cp4(S + L.qfrc_smooth, gw + G.qfrc_smooth, nvq, lane);
-    cp4(S + L.act_force, gw + G.act_force, (nu + 3) & ~3, lane);
-    cp4(S + L.cdof, gw + G.cdof, 6 * nvp, lane);
-    cp4(S + L.cdofdot, gw + G.cdofdot, 6 * nvp, lane);
-    cp4(S + L.cvel, gw + G.cvel, (6 * nb + 3) & ~3, lane);
-    cp4(S + L.subtree_com, gw + G.subtree_com, (3 * nb + 3) & ~3, lane);
-    cp4(S + L.sxpos, gw + G.sxpos, (3 * d.nsite + 3) & ~3, lane);
-    cp4(S + L.sxmat, gw + G.sxmat, (9 * d.nsite + 3) & ~3, lane);
-    cp4(S + L.con_g1, gw + G.con_g1, C4, lane);
-    cp4(S + L.con_g2, gw + G.con_g2, C4, lane);
-    cp4(S + L.con_dist, gw + G.con_dist, C4, lane);
-    cp4(S + L.con_pos, gw + G.con_pos, (3 * C + 3) & ~3, lane);
-    cp4(S + L.con_frame, gw + G.con_frame, (9 * C + 3) & ~3, lane);
-    cp4(S + L.con_mu, gw + G.con_mu, (2 * C + 3) & ~3, lane);
-    cp4(S + L.con_dim, gw + G.con_dim, C4, lane);
-    cp4(S + L.con_efc, gw + G.con_efc, C4, lane);
+    cp_pack(S, gc, L.pack_len, lane);  // C pack: carve offsets == pack offsets
     sync();
     const int nefc = ints[1];
     int ncon = ints[4];
     const int niter_last = ints[5];
-    cp4(S + L.efc_force, gw + G.efc_force, (nefc + 3) & ~3, lane);
-    sync();
     STAMP(15);
     // =========================================================== post-constraint acc
     if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];

@@ -6,7 +6,7 @@ import torch
 from mjlab_amd.envs import make_env
 NAMES = ["kinematics", "com/cinert/cdof", "crb+M", "collision", "contact sort+params",
          "constraints", "velocity+rne+act", "smooth solve", "subtree mom", "newton",
-         "post acc", "sensors", "outputs", "integrate"]
+         "post acc", "sensors", "outputs", "integrate", "phase hand-off out", "phase hand-off in"]
 for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
   N = 4096
   env = make_env(task, N, "cuda:0", seed=42)
