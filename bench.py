@@ -82,19 +82,17 @@ def main():
   ap.add_argument("--eager", action="store_true", help="reference-style eager env.step (host syncs)")
   args = ap.parse_args()
 
-  world = int(os.environ.get("WORLD_SIZE", "1"))
-  rank = int(os.environ.get("RANK", "0"))
-  local = int(os.environ.get("LOCAL_RANK", "0"))
+  from mjlab_amd import distributed as mjdist
+  world, rank, local = mjdist.world_info()
   dist = None
+  torch.cuda.set_device(local)
   if world > 1:
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    mjdist.init("nccl", torch.device("cuda", local))
   device = f"cuda:{local}"
-  torch.cuda.set_device(local)
 
   from mjlab_amd.envs import make_env
-  env = make_env(args.task, num_envs=args.num_envs, device=device, seed=42 + rank)
+  env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
   m = env.sim.mj_model
   dec = env.cfg.decimation
   gen = torch.Generator(device=device)
@@ -135,13 +133,9 @@ def main():
     env.sim.step()
   launch_ms = env.sim.timing_end()
   if dist is not None:
-    t = torch.tensor([el], device=device, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    el = mjdist.max_over_ranks(el, device)
     # episode statistics: one packed all-gather over RCCL
-    stats = env.packed_episode_stats()
-    gathered = [torch.zeros_like(stats) for _ in range(world)]
-    dist.all_gather(gathered, stats)
+    mjdist.gather_stats(env.packed_episode_stats())
 
   total = args.steps * args.num_envs * world
   value = total / el

@@ -147,13 +147,15 @@ class Model:
 
 
 def _resolve(value, names, default):
-  """`resolve_field` of mjlab's spec_config: scalar or {regex: value} per name."""
+  """`resolve_field` of mjlab's spec_config (utils/string.py:5-38): scalar or
+  {regex: value} per name; first pattern that matches at the START of the name wins
+  (re.match semantics, so ".*_collision" also covers "FR_thigh_collision1")."""
   if isinstance(value, dict):
     out = []
     for n in names:
       v = default
       for pat, val in value.items():
-        if re.fullmatch(pat, n):
+        if re.match(pat, n):
           v = val
           break
       out.append(v)
@@ -162,6 +164,12 @@ def _resolve(value, names, default):
 
 
 def _filter_exp(exprs, names):
+  """`filter_exp` (utils/string.py:24-30): prefix match (re.match)."""
+  return [n for n in names if any(re.match(e, n) for e in exprs)]
+
+
+def _find_names(exprs, names):
+  """Entity.find_joints / resolve_matching_names (lab_api/string.py:227): full match."""
   return [n for n in names if any(re.fullmatch(e, n) for e in exprs)]
 
 
@@ -321,7 +329,7 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
                           prefix + attrs.get("name", "")))
     # actuators (cfg order, joints in natural order)
     for grp in ent.actuators:
-      names = _filter_exp(grp.joint_names_expr, joint_name_order)
+      names = _find_names(grp.joint_names_expr, joint_name_order)
       if not names:
         raise ValueError(f"no joints for actuator {grp.joint_names_expr}")
       for n in names:
@@ -651,8 +659,8 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
         key[a + 3:a + 7] = ent.init_rot
       elif ent.init_joint_pos is not None:
         short = j["name"][len(prefix):]
-        for pat, val in ent.init_joint_pos.items():
-          if re.fullmatch(pat, short):
+        for pat, val in ent.init_joint_pos.items():  # resolve_expr: re.match semantics
+          if re.match(pat, short):
             key[a] = val
             break
   A["key_qpos"] = key
