@@ -11,10 +11,13 @@ Workload semantics follow the reference's scripts/benchmarks/measure_throughput.
     `--mode physics` times decimation x Simulation.step only (measure_physics_sps).
 Actions are uniform[-1,1) from a torch Generator seeded 0 (scripts/play.py:173-176).
 
-roofline: dominant kernel = the batched step kernel; algorithmic bytes per env-step
+roofline: dominant kernel = one Simulation.step launch group (step_phase<NR,0|1|2>, the
+three phases of one substep); algorithmic bytes per env-step
 B_env = 4*[dec*(2nq+5nv+2nu+ns+1) + 16*nbody + 72], per launch
 B_env/dec per world; achieved = bytes/launch / mean launch time (HIP events on the
-launch stream); peak 8 TB/s (MI355X_MICROARCH.md).
+launch stream); peak 8 TB/s (MI355X_MICROARCH.md).  `traffic` = HBM bytes per launch from
+the committed PMC measurement profiles/r01_hbm_traffic.json (FETCH_SIZE x2 + WRITE_SIZE,
+separate rocprofv3 passes) when it was taken on this task / num_envs / nv, else null.
 cpu_baseline: the fp64 CPU oracle (oracle/liboracle.so, "port"), OpenMP over worlds on
 the box's host cores, bounded sample.
 """
@@ -40,6 +43,18 @@ HBM_PEAK_GBS = 8000.0
 
 def b_env(m, dec):
   return 4 * (dec * (2 * m.nq + 5 * m.nv + 2 * m.nu + m.nsensordata + 1) + 16 * m.nbody + 72)
+
+
+def measured_traffic(task, num_envs, nv):
+  path = os.path.join(ROOT, "profiles", "r01_hbm_traffic.json")
+  try:
+    with open(path) as fh:
+      t = json.load(fh)
+  except (OSError, ValueError):
+    return None
+  if (t.get("task"), t.get("num_envs"), t.get("nv")) != (task, num_envs, nv):
+    return None
+  return float(t["traffic_bytes_per_launch"])
 
 
 def cpu_baseline(model, dec, budget_s=12.0):
@@ -152,8 +167,9 @@ def main():
                  "parallelism": f"dp{world}", "mode": args.mode,
                  "step_path": "eager" if (args.eager or args.mode != "env") else "sync-free, HIP-graph captured"},
       "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                   "kernel": "mjx::step_kernel", "launch_ms": launch_ms,
+                   "frac": achieved / HBM_PEAK_GBS,
+                   "traffic": measured_traffic(args.task, args.num_envs, m.nv),
+                   "kernel": "mjx::step_phase<NR,0|1|2> (one Simulation.step)", "launch_ms": launch_ms,
                    "bytes_per_launch": bytes_launch},
       "cpu_baseline": None,
     }
