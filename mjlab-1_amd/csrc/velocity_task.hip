@@ -1,0 +1,571 @@
+// velocity_task.hip — fused per-env managers of mjlab's velocity tasks (gfx950).
+//
+// One thread per env; every manager stage of ManagerBasedRlEnv.step() that the torch
+// stack runs as ~700 small kernels per env step becomes one of five launches (see
+// include/mjx355_task.h for the reference functions each kernel replaces).  The work is
+// a few hundred flops per env against ~1-2 KB of per-env state, so the kernels are
+// latency-bound; they read the mjx355 data arena and write the managers' torch tensors
+// in place.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <string>
+
+#include "../../include/mjx355_task.h"
+
+namespace mjxt {
+
+constexpr int kBlock = 128;
+
+struct Acc {  // device accumulators, reduced across envs with atomics
+  float reward[MJX_TASK_MAX_TERMS];
+  float term[MJX_TASK_MAX_TERMS];
+  float cmd[2];
+  float metric_sum[MJX_MT_COUNT];
+  float metric_cnt[MJX_MT_COUNT];
+  float count;
+};
+
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(const float* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// quaternions (w, x, y, z): utils/lab_api/math.py quat_apply(_inverse) :629-670
+__device__ __forceinline__ V3 qrot(const float* q, V3 v, float sgn) {
+  const float w = q[0];
+  V3 u = {sgn * q[1], sgn * q[2], sgn * q[3]};
+  V3 t = cross(u, v);
+  t = {2.f * t.x, 2.f * t.y, 2.f * t.z};
+  V3 c = cross(u, t);
+  return {v.x + w * t.x + c.x, v.y + w * t.y + c.y, v.z + w * t.z + c.z};
+}
+__device__ __forceinline__ V3 qapply(const float* q, V3 v) { return qrot(q, v, 1.f); }
+__device__ __forceinline__ V3 qapply_inv(const float* q, V3 v) { return qrot(q, v, -1.f); }
+__device__ __forceinline__ void qmul(const float* a, const float* b, float* r) {
+  r[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  r[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  r[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  r[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+}
+// quat_from_euler_xyz (math.py:275-302)
+__device__ __forceinline__ void quat_euler(float r, float p, float y, float* q) {
+  float cy = cosf(y * 0.5f), sy = sinf(y * 0.5f), cr = cosf(r * 0.5f), sr = sinf(r * 0.5f);
+  float cp = cosf(p * 0.5f), sp = sinf(p * 0.5f);
+  q[0] = cy * cr * cp + sy * sr * sp;
+  q[1] = cy * sr * cp - sy * cr * sp;
+  q[2] = cy * cr * sp + sy * sr * cp;
+  q[3] = sy * cr * cp - cy * sr * sp;
+}
+__device__ __forceinline__ float wrap_to_pi(float a) {
+  const float tp = 6.283185307179586f;
+  float w = fmodf(a + 3.141592653589793f, tp);
+  if (w < 0.f) w += tp;
+  return w - 3.141592653589793f;
+}
+
+// counter-based uniform randoms: splitmix64 of (seed, env, step, draw)
+__device__ __forceinline__ float urand(uint64_t seed, uint32_t env, uint64_t step, uint32_t draw) {
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(env + 1)) ^
+               (0xBF58476D1CE4E5B9ull * (step + 1)) ^ (0x94D049BB133111EBull * (uint64_t)(draw + 1));
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+}
+__device__ __forceinline__ float uniform(float lo, float hi, float u) { return lo + (hi - lo) * u; }
+
+// draw ids (per env, per env-step), kept disjoint between kernels
+enum : uint32_t { D_RESET = 0x1000, D_CMD_RESET = 0x2000, D_CMD = 0x3000, D_PUSH = 0x4000,
+                  D_NOISE = 0x5000 };
+
+// EntityData derived reads (entity/data.py:20-31, 219-229, 320-327)
+struct Root {
+  V3 lin_w, ang_w, lin_b, ang_b, grav_b;
+  const float* quat;
+};
+__device__ __forceinline__ Root root_state(const mjxTaskDesc& t, int e) {
+  Root r;
+  const int b = t.root_body;
+  const size_t nb = (size_t)t.nbody;
+  const float* cv = t.cvel + ((size_t)e * nb + b) * 6;
+  V3 ang = v3(cv), linc = v3(cv + 3);
+  V3 off = sub(v3(t.subtree_com + ((size_t)e * nb + b) * 3), v3(t.xpos + ((size_t)e * nb + b) * 3));
+  V3 c = cross(ang, off);
+  r.lin_w = sub(linc, c);
+  r.ang_w = ang;
+  r.quat = t.xquat + ((size_t)e * nb + b) * 4;
+  r.lin_b = qapply_inv(r.quat, r.lin_w);
+  r.ang_b = qapply_inv(r.quat, r.ang_w);
+  r.grav_b = qapply_inv(r.quat, V3{0.f, 0.f, -1.f});
+  return r;
+}
+// site velocity (world, linear part) with the entity root's subtree com
+__device__ __forceinline__ V3 site_lin_vel(const mjxTaskDesc& t, int e, int site, int body) {
+  const size_t nb = (size_t)t.nbody;
+  const float* cv = t.cvel + ((size_t)e * nb + body) * 6;
+  V3 sc = v3(t.subtree_com + ((size_t)e * nb + t.root_body) * 3);
+  V3 p = v3(t.site_xpos + ((size_t)e * t.nsite + site) * 3);
+  return sub(v3(cv + 3), cross(v3(cv), sub(sc, p)));
+}
+__device__ __forceinline__ float command_active(const float* c, float thr) {
+  return (sqrtf(c[0] * c[0] + c[1] * c[1]) + fabsf(c[2])) > thr ? 1.f : 0.f;
+}
+
+// ----------------------------------------------------------------------------- kernels
+__global__ void k_action(const mjxTaskDesc* __restrict__ T, const float* __restrict__ a) {
+  const mjxTaskDesc& t = *T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) *t.step_counter += 1;  // later kernels of this env step read the new value
+  if (e >= t.nworld) return;
+  const int nj = t.njoint;
+  for (int k = 0; k < nj; k++) {
+    const size_t i = (size_t)e * nj + k;
+    const float raw = a[i];
+    t.prev_prev_action[i] = t.prev_action[i];
+    t.prev_action[i] = t.action[i];
+    t.action[i] = raw;
+    // separately rounded mul + add, as torch computes raw * scale + offset (no FMA), so
+    // ctrl is bitwise identical to the torch manager path
+    const float target = __fadd_rn(__fmul_rn(raw, t.action_scale[k]), t.action_offset[k]);
+    t.joint_pos_target[(size_t)e * nj + t.target_of_action[k]] = target;
+    t.ctrl[(size_t)e * t.nu + t.ctrl_of_action[k]] = target;
+  }
+}
+
+__global__ void k_substep(const mjxTaskDesc* __restrict__ T) {
+  const mjxTaskDesc& t = *T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= t.nworld) return;
+  const float now = t.time[e];
+  const float el = now - t.last_time[e];
+  for (int f = 0; f < t.nfeet; f++) {
+    const size_t i = (size_t)e * t.nfeet + f;
+    const bool contact = t.sensordata[(size_t)e * t.nsensordata + t.feet_found_adr[f]] > 0.f;
+    const float ca = t.cur_air[i], cc = t.cur_contact[i];
+    if (ca > 0.f && contact) t.last_air[i] = ca + el;
+    t.cur_air[i] = contact ? 0.f : ca + el;
+    if (cc > 0.f && !contact) t.last_contact[i] = cc + el;
+    t.cur_contact[i] = contact ? cc + el : 0.f;
+  }
+  t.last_time[e] = now;
+}
+
+__global__ void k_post(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
+  const mjxTaskDesc& t = *T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= t.nworld) return;
+  const int64_t len = t.episode_length[e] + 1;
+  t.episode_length[e] = len;
+  const Root r = root_state(t, e);
+  const float* sd = t.sensordata + (size_t)e * t.nsensordata;
+  // ---- terminations (termination_manager.py:87-97)
+  bool terminated = false, truncated = false;
+  for (int k = 0; k < t.ntermination; k++) {
+    bool v = false;
+    switch (t.termination_kind[k]) {
+      case MJX_TM_TIME_OUT: v = len >= t.max_episode_length; break;
+      case MJX_TM_BAD_ORIENT: v = fabsf(acosf(-r.grav_b.z)) > t.termination_p0[k]; break;  // NaN -> false, as torch
+      case MJX_TM_ILLEGAL_CONTACT:
+        for (int s = 0; s < t.nillegal; s++) v |= sd[t.illegal_found_adr[s]] > 0.f;
+        break;
+    }
+    t.term_dones[(size_t)k * t.nworld + e] = v;
+    if (t.termination_is_timeout[k]) truncated |= v; else terminated |= v;
+  }
+  const bool reset = terminated || truncated;
+  t.terminated[e] = terminated;
+  t.time_outs[e] = truncated;
+  t.reset_buf[e] = reset;
+  // ---- rewards (reward_manager.py:77-91)
+  const float dt = t.step_dt;
+  const float* cmd = t.command + (size_t)e * 3;
+  const int nj = t.njoint;
+  float total = 0.f;
+  for (int k = 0; k < t.nreward; k++) {
+    const float w = t.reward_weight[k];
+    float* sr = t.step_reward + (size_t)e * t.nreward + k;
+    if (w == 0.f) { *sr = 0.f; continue; }
+    const float p0 = t.reward_p0[k], p1 = t.reward_p1[k], p2 = t.reward_p2[k];
+    float f = 0.f;
+    switch (t.reward_kind[k]) {
+      case MJX_RW_TRACK_LIN: {  // rewards.py:23-40
+        float dx = cmd[0] - r.lin_b.x, dy = cmd[1] - r.lin_b.y;
+        f = expf(-(dx * dx + dy * dy + r.lin_b.z * r.lin_b.z) / (p0 * p0));
+      } break;
+      case MJX_RW_TRACK_ANG: {  // rewards.py:43-60
+        float dz = cmd[2] - r.ang_b.z;
+        f = expf(-(dz * dz + r.ang_b.x * r.ang_b.x + r.ang_b.y * r.ang_b.y) / (p0 * p0));
+      } break;
+      case MJX_RW_FLAT_ORIENT: {  // rewards.py:63-85
+        V3 g = r.grav_b;
+        if (t.orient_body >= 0)
+          g = qapply_inv(t.xquat + ((size_t)e * t.nbody + t.orient_body) * 4, V3{0.f, 0.f, -1.f});
+        f = expf(-(g.x * g.x + g.y * g.y) / (p0 * p0));
+      } break;
+      case MJX_RW_POSE: {  // rewards.py:291-359 (p0 walking, p1 running threshold)
+        const float speed = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) + fabsf(cmd[2]);
+        const float* std = speed < p0 ? t.std_standing : (speed < p1 ? t.std_walking : t.std_running);
+        float s = 0.f;
+        for (int j = 0; j < nj; j++) {
+          float d = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j];
+          s += d * d / (std[j] * std[j]);
+        }
+        f = expf(-s / (float)nj);
+      } break;
+      case MJX_RW_BODY_ANG_VEL: {  // rewards.py:98-107
+        const float* cv = t.cvel + ((size_t)e * t.nbody + t.orient_body) * 6;
+        f = cv[0] * cv[0] + cv[1] * cv[1];
+      } break;
+      case MJX_RW_ANGMOM: {  // rewards.py:110-120
+        const float* h = sd + t.angmom_adr;
+        f = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+        atomicAdd(&acc->metric_sum[MJX_MT_ANGMOM], sqrtf(f));
+        atomicAdd(&acc->metric_cnt[MJX_MT_ANGMOM], 1.f);
+      } break;
+      case MJX_RW_JOINT_POS_LIMITS: {  // envs/mdp/rewards.py:73-88
+        for (int j = 0; j < nj; j++) {
+          float q = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
+          f += fmaxf(t.soft_lo[j] - q, 0.f) + fmaxf(q - t.soft_hi[j], 0.f);
+        }
+      } break;
+      case MJX_RW_ACTION_RATE: {  // envs/mdp/rewards.py:56-60
+        for (int j = 0; j < nj; j++) {
+          float d = t.action[(size_t)e * nj + j] - t.prev_action[(size_t)e * nj + j];
+          f += d * d;
+        }
+      } break;
+      case MJX_RW_FEET_AIR_TIME: {  // rewards.py:123-152 (p0 min, p1 max, p2 cmd thr)
+        float in_air_t = 0.f, in_air_n = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          float at = t.cur_air[(size_t)e * t.nfeet + s];
+          f += (at > p0 && at < p1) ? 1.f : 0.f;
+          if (at > 0.f) { in_air_t += at; in_air_n += 1.f; }
+        }
+        atomicAdd(&acc->metric_sum[MJX_MT_AIR_TIME], in_air_t);
+        atomicAdd(&acc->metric_cnt[MJX_MT_AIR_TIME], in_air_n);
+        f *= command_active(cmd, p2);
+      } break;
+      case MJX_RW_FEET_CLEARANCE: {  // rewards.py:155-177 (p0 target, p1 cmd thr)
+        for (int s = 0; s < t.nfeet; s++) {
+          float z = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
+          V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
+          f += fabsf(z - p0) * sqrtf(v.x * v.x + v.y * v.y);
+        }
+        f *= command_active(cmd, p1);
+      } break;
+      case MJX_RW_FEET_SWING: {  // rewards.py:180-229 (p0 target, p1 cmd thr)
+        float land_n = 0.f, land_h = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          const size_t i = (size_t)e * t.nfeet + s;
+          float z = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
+          float peak = t.peak_heights[i];
+          if (sd[t.feet_found_adr[s]] == 0.f) peak = fmaxf(peak, z);
+          const float cc = t.cur_contact[i];
+          const bool first = cc > 0.f && cc < dt + 1e-8f;
+          if (first) {
+            float err = peak / p0 - 1.f;
+            f += err * err;
+            land_n += 1.f;
+            land_h += peak;
+            peak = 0.f;
+          }
+          t.peak_heights[i] = peak;
+        }
+        atomicAdd(&acc->metric_sum[MJX_MT_PEAK_HEIGHT], land_h);
+        atomicAdd(&acc->metric_cnt[MJX_MT_PEAK_HEIGHT], land_n);
+        f *= command_active(cmd, p1);
+      } break;
+      case MJX_RW_FEET_SLIP: {  // rewards.py:232-259 (p0 cmd thr)
+        float vs = 0.f, n = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          if (!(sd[t.feet_found_adr[s]] > 0.f)) continue;
+          V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
+          float v2 = v.x * v.x + v.y * v.y;
+          f += v2;
+          vs += sqrtf(v2);
+          n += 1.f;
+        }
+        atomicAdd(&acc->metric_sum[MJX_MT_SLIP], vs);
+        atomicAdd(&acc->metric_cnt[MJX_MT_SLIP], n);
+        f *= command_active(cmd, p0);
+      } break;
+      case MJX_RW_SOFT_LANDING: {  // rewards.py:262-288 (p0 cmd thr)
+        float n = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          const float cc = t.cur_contact[(size_t)e * t.nfeet + s];
+          if (!(cc > 0.f && cc < dt + 1e-8f)) continue;
+          const float* fv = sd + t.feet_force_adr[s];
+          f += sqrtf(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]);
+          n += 1.f;
+        }
+        atomicAdd(&acc->metric_sum[MJX_MT_LANDING], f);
+        atomicAdd(&acc->metric_cnt[MJX_MT_LANDING], n);
+        f *= command_active(cmd, p0);
+      } break;
+      case MJX_RW_SELF_COLLISION: f = sd[t.selfcol_found_adr]; break;  // rewards.py:88-95
+    }
+    float v = f * w * dt;
+    if (!isfinite(v)) v = 0.f;  // nan_to_num
+    total += v;
+    float* es = t.episode_sums + (size_t)k * t.nworld + e;
+    *es += v;
+    *sr = v / dt;
+  }
+  t.reward_buf[e] = total;
+  // ---- reset bookkeeping of this step's resets (reward/termination/command manager logs)
+  if (reset) {
+    atomicAdd(&acc->count, 1.f);
+    for (int k = 0; k < t.nreward; k++) {
+      float* es = t.episode_sums + (size_t)k * t.nworld + e;
+      atomicAdd(&acc->reward[k], *es);
+      *es = 0.f;
+    }
+    for (int k = 0; k < t.ntermination; k++)
+      if (t.term_dones[(size_t)k * t.nworld + e]) atomicAdd(&acc->term[k], 1.f);
+    atomicAdd(&acc->cmd[0], t.metric_err_xy[e]);
+    atomicAdd(&acc->cmd[1], t.metric_err_yaw[e]);
+    t.metric_err_xy[e] = 0.f;
+    t.metric_err_yaw[e] = 0.f;
+  }
+}
+
+__device__ __forceinline__ void resample_command(const mjxTaskDesc& t, int e, uint64_t step,
+                                                 uint32_t base) {
+  // CommandTerm._resample + UniformVelocityCommand._resample_command (velocity_command.py:65-95)
+  const uint64_t seed = t.seed;
+  t.cmd_time_left[e] = uniform(t.resampling_time[0], t.resampling_time[1], urand(seed, e, step, base + 0));
+  float* c = t.command + (size_t)e * 3;
+  c[0] = uniform(t.lin_vel_x[0], t.lin_vel_x[1], urand(seed, e, step, base + 1));
+  c[1] = uniform(t.lin_vel_y[0], t.lin_vel_y[1], urand(seed, e, step, base + 2));
+  c[2] = uniform(t.ang_vel_z[0], t.ang_vel_z[1], urand(seed, e, step, base + 3));
+  if (t.heading_command) {
+    t.heading_target[e] = uniform(t.heading[0], t.heading[1], urand(seed, e, step, base + 4));
+    t.is_heading_env[e] = urand(seed, e, step, base + 5) <= t.rel_heading_envs;
+  }
+  t.is_standing_env[e] = urand(seed, e, step, base + 6) <= t.rel_standing_envs;
+  t.command_counter[e] += 1;
+}
+
+__global__ void k_reset(const mjxTaskDesc* __restrict__ T) {
+  const mjxTaskDesc& t = *T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= t.nworld || !t.reset_buf[e]) return;
+  const uint64_t step = *t.step_counter, seed = t.seed;
+  const int nj = t.njoint;
+  // scene reset: contact-sensor air time, entity targets (scene.py reset_masked)
+  for (int f = 0; f < t.nfeet; f++) {
+    const size_t i = (size_t)e * t.nfeet + f;
+    t.cur_air[i] = t.last_air[i] = t.cur_contact[i] = t.last_contact[i] = 0.f;
+  }
+  t.last_time[e] = t.time[e];
+  for (int j = 0; j < nj; j++) t.joint_pos_target[(size_t)e * nj + j] = 0.f;
+  // reset_root_state_uniform (events.py:81-120)
+  float ps[6], vs[6];
+  for (int i = 0; i < 6; i++) {
+    ps[i] = uniform(t.reset_pose_range[i][0], t.reset_pose_range[i][1], urand(seed, e, step, D_RESET + i));
+    vs[i] = uniform(t.reset_vel_range[i][0], t.reset_vel_range[i][1], urand(seed, e, step, D_RESET + 6 + i));
+  }
+  float* q = t.qpos + (size_t)e * t.nq + t.free_q_adr;
+  const float* o = t.env_origins + (size_t)e * 3;
+  const float* rs = t.default_root_state;
+  q[0] = rs[0] + ps[0] + o[0];
+  q[1] = rs[1] + ps[1] + o[1];
+  q[2] = rs[2] + ps[2] + o[2];
+  float qe[4];
+  quat_euler(ps[3], ps[4], ps[5], qe);
+  qmul(rs + 3, qe, q + 3);
+  float* v = t.qvel + (size_t)e * t.nv + t.free_v_adr;
+  V3 ang_b = qapply_inv(q + 3, V3{rs[10] + vs[3], rs[11] + vs[4], rs[12] + vs[5]});
+  v[0] = rs[7] + vs[0]; v[1] = rs[8] + vs[1]; v[2] = rs[9] + vs[2];
+  v[3] = ang_b.x; v[4] = ang_b.y; v[5] = ang_b.z;
+  // reset_joints_by_offset (events.py:123-160): clamp to soft limits
+  for (int j = 0; j < nj; j++) {
+    float jp = t.default_joint_pos[j] +
+               uniform(t.reset_joint_pos_range[0], t.reset_joint_pos_range[1], urand(seed, e, step, D_RESET + 12 + j));
+    jp = fminf(fmaxf(jp, t.soft_lo[j]), t.soft_hi[j]);
+    float jv = uniform(t.reset_joint_vel_range[0], t.reset_joint_vel_range[1],
+                       urand(seed, e, step, D_RESET + 12 + MJX_TASK_MAX_JOINTS + j));
+    t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] = jp;
+    t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]] = jv;
+  }
+  // action manager reset
+  for (int j = 0; j < nj; j++) {
+    const size_t i = (size_t)e * nj + j;
+    t.action[i] = t.prev_action[i] = t.prev_prev_action[i] = 0.f;
+  }
+  // command manager reset: counter 0 then resample
+  t.command_counter[e] = 0;
+  resample_command(t, e, step, D_CMD_RESET);
+  // event manager reset: interval timers
+  if (t.has_push)
+    t.push_time_left[e] = uniform(t.push_interval[0], t.push_interval[1], urand(seed, e, step, D_CMD_RESET + 16));
+  t.episode_length[e] = 0;
+}
+
+__global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
+  const mjxTaskDesc& t = *T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) {
+    // logs of the previous kernels' reductions (k_post ran to completion before this launch)
+    if (acc->count > 0.f) {
+      for (int k = 0; k < t.nreward; k++) t.log_reward[k] = acc->reward[k] / acc->count / t.episode_length_s;
+      for (int k = 0; k < t.ntermination; k++) t.log_termination[k] = acc->term[k];
+      t.log_command[0] = acc->cmd[0] / acc->count;
+      t.log_command[1] = acc->cmd[1] / acc->count;
+    }
+    for (int m = 0; m < MJX_MT_COUNT; m++) {
+      t.log_metric[m] = acc->metric_sum[m] / fmaxf(acc->metric_cnt[m], 1.f);
+      acc->metric_sum[m] = acc->metric_cnt[m] = 0.f;
+    }
+    for (int k = 0; k < MJX_TASK_MAX_TERMS; k++) acc->reward[k] = acc->term[k] = 0.f;
+    acc->cmd[0] = acc->cmd[1] = 0.f;
+    acc->count = 0.f;
+  }
+  if (e >= t.nworld) return;
+  const uint64_t step = *t.step_counter, seed = t.seed;
+  const Root r = root_state(t, e);
+  float* c = t.command + (size_t)e * 3;
+  // ---- CommandTerm.compute: metrics, timer, resample, heading control (velocity_command.py)
+  const float mcs = t.resampling_time[1] / t.step_dt;
+  t.metric_err_xy[e] += sqrtf((c[0] - r.lin_b.x) * (c[0] - r.lin_b.x) + (c[1] - r.lin_b.y) * (c[1] - r.lin_b.y)) / mcs;
+  t.metric_err_yaw[e] += fabsf(c[2] - r.ang_b.z) / mcs;
+  float tl = t.cmd_time_left[e] - t.step_dt;
+  t.cmd_time_left[e] = tl;
+  if (tl <= 0.f) resample_command(t, e, step, D_CMD);
+  if (t.heading_command) {
+    V3 fwd = qapply(r.quat, V3{1.f, 0.f, 0.f});
+    const float heading = atan2f(fwd.y, fwd.x);
+    const float err = wrap_to_pi(t.heading_target[e] - heading);
+    t.heading_error[e] = err;
+    if (t.is_heading_env[e])
+      c[2] = fminf(fmaxf(t.heading_stiffness * err, t.ang_vel_z[0]), t.ang_vel_z[1]);
+  }
+  if (t.is_standing_env[e]) c[0] = c[1] = c[2] = 0.f;
+  // ---- interval event: push_by_setting_velocity (event_manager.py:124-146, events.py:209-223)
+  if (t.has_push) {
+    float pt = t.push_time_left[e] - t.step_dt;
+    if (pt < 1e-6f) {
+      pt = uniform(t.push_interval[0], t.push_interval[1], urand(seed, e, step, D_PUSH));
+      float u[6];
+      for (int i = 0; i < 6; i++)
+        u[i] = uniform(t.push_vel_range[i][0], t.push_vel_range[i][1], urand(seed, e, step, D_PUSH + 1 + i));
+      float* v = t.qvel + (size_t)e * t.nv + t.free_v_adr;
+      const float* qq = t.qpos + (size_t)e * t.nq + t.free_q_adr + 3;
+      V3 ang_b = qapply_inv(qq, V3{r.ang_w.x + u[3], r.ang_w.y + u[4], r.ang_w.z + u[5]});
+      v[0] = r.lin_w.x + u[0]; v[1] = r.lin_w.y + u[1]; v[2] = r.lin_w.z + u[2];
+      v[3] = ang_b.x; v[4] = ang_b.y; v[5] = ang_b.z;
+    }
+    t.push_time_left[e] = pt;
+  }
+  // ---- observations (observation_manager.py:154-208; velocity_env_cfg.py observation terms)
+  const float* sd = t.sensordata + (size_t)e * t.nsensordata;
+  const int nj = t.njoint;
+  float* po = t.obs_policy + (size_t)e * t.npolicy;
+  float* co = t.obs_critic + (size_t)e * t.ncritic;
+  const bool noisy = t.corrupt_policy != 0;
+  uint32_t dn = D_NOISE;
+  auto put = [&](int& i, float val, float noise) {
+    co[i] = val;
+    po[i] = noisy && noise > 0.f ? val + uniform(-noise, noise, urand(seed, e, step, dn)) : val;
+    dn++;
+    i++;
+  };
+  int i = 0;
+  for (int k = 0; k < 3; k++) put(i, sd[t.imu_lin_vel_adr + k], t.noise_lin_vel);
+  for (int k = 0; k < 3; k++) put(i, sd[t.imu_ang_vel_adr + k], t.noise_ang_vel);
+  put(i, r.grav_b.x, t.noise_gravity);
+  put(i, r.grav_b.y, t.noise_gravity);
+  put(i, r.grav_b.z, t.noise_gravity);
+  for (int j = 0; j < nj; j++)
+    put(i, t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j], t.noise_joint_pos);
+  for (int j = 0; j < nj; j++) put(i, t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]], t.noise_joint_vel);
+  for (int j = 0; j < nj; j++) put(i, t.action[(size_t)e * nj + j], 0.f);
+  for (int k = 0; k < 3; k++) put(i, c[k], 0.f);
+  if (t.critic_extras) {
+    int ic = i;
+    for (int s = 0; s < t.nfeet; s++) co[ic++] = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
+    for (int s = 0; s < t.nfeet; s++) co[ic++] = t.cur_air[(size_t)e * t.nfeet + s];
+    for (int s = 0; s < t.nfeet; s++) co[ic++] = sd[t.feet_found_adr[s]] > 0.f ? 1.f : 0.f;
+    for (int s = 0; s < t.nfeet; s++)
+      for (int k = 0; k < 3; k++) {
+        float fv = sd[t.feet_force_adr[s] + k];
+        co[ic++] = copysignf(log1pf(fabsf(fv)), fv) * (fv != 0.f ? 1.f : 0.f);
+      }
+  }
+}
+
+}  // namespace mjxt
+
+// ----------------------------------------------------------------------------- C ABI
+struct mjxTask_ {
+  mjxTaskDesc host;
+  mjxTaskDesc* dev = nullptr;
+  mjxt::Acc* acc = nullptr;
+  int nworld = 0;
+};
+
+static thread_local std::string g_task_err;
+static int task_fail(const std::string& s) {
+  g_task_err = s;
+  return -1;
+}
+
+extern "C" {
+
+size_t mjx_task_desc_size(void) { return sizeof(mjxTaskDesc); }
+
+int mjx_task_create(const mjxTaskDesc* desc, mjxTask** out) {
+  if (!desc || !out) return task_fail("null argument");
+  if (desc->njoint > MJX_TASK_MAX_JOINTS || desc->nfeet > MJX_TASK_MAX_FEET ||
+      desc->nreward > MJX_TASK_MAX_TERMS || desc->ntermination > MJX_TASK_MAX_TERMS ||
+      desc->nillegal > MJX_TASK_MAX_CONTACT_SLOTS)
+    return task_fail("task descriptor exceeds compiled capacities");
+  auto* t = new mjxTask_();
+  t->host = *desc;
+  t->nworld = desc->nworld;
+  if (hipMalloc((void**)&t->dev, sizeof(mjxTaskDesc)) != hipSuccess ||
+      hipMalloc((void**)&t->acc, sizeof(mjxt::Acc)) != hipSuccess) {
+    delete t;
+    return task_fail("hipMalloc failed");
+  }
+  if (hipMemcpy(t->dev, desc, sizeof(mjxTaskDesc), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(t->acc, 0, sizeof(mjxt::Acc)) != hipSuccess) {
+    delete t;
+    return task_fail("upload failed");
+  }
+  *out = t;
+  return 0;
+}
+
+int mjx_task_destroy(mjxTask* t) {
+  if (!t) return 0;
+  if (t->dev) (void)hipFree(t->dev);
+  if (t->acc) (void)hipFree(t->acc);
+  delete t;
+  return 0;
+}
+
+#define TASK_LAUNCH(kern, ...)                                                             \
+  do {                                                                                     \
+    if (!t) return task_fail("null task");                                                 \
+    const int nb = (t->nworld + mjxt::kBlock - 1) / mjxt::kBlock;                          \
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(mjxt::kBlock), 0, (hipStream_t)stream, __VA_ARGS__); \
+    hipError_t e_ = hipGetLastError();                                                      \
+    if (e_ != hipSuccess) return task_fail(std::string(#kern ": ") + hipGetErrorString(e_)); \
+    return 0;                                                                              \
+  } while (0)
+
+int mjx_task_action(mjxTask* t, const float* action, void* stream) { TASK_LAUNCH(mjxt::k_action, t->dev, action); }
+int mjx_task_substep(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_substep, t->dev); }
+int mjx_task_post(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_post, t->dev, t->acc); }
+int mjx_task_reset(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_reset, t->dev); }
+int mjx_task_observe(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_observe, t->dev, t->acc); }
+
+const char* mjx_task_last_error(void) { return g_task_err.c_str(); }
+
+}  // extern "C"

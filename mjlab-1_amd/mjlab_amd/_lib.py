@@ -19,7 +19,11 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
            "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile",
-           "mjx_forward_masked")
+           "mjx_forward_masked",
+           # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
+           "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
+           "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
+           "mjx_task_last_error")
 
 _lib = None
 
@@ -57,6 +61,8 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp]
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
   for name in EXPORTS:
+    if name.startswith("mjx_task_"):
+      continue  # bound by mjlab_amd.fused
     if name not in ("mjx_last_error", "mjx_field_name", "mjx_model_desc_size"):
       getattr(L, name).restype = ci
   if L.mjx_abi_version() != 1:

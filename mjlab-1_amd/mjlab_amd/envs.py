@@ -10,6 +10,7 @@ restate `tasks/velocity/velocity_env_cfg.py:33-354` and
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Any
 
@@ -74,6 +75,7 @@ class ManagerBasedRlEnv:
     self._sim_step_counter = 0
     self.extras: dict[str, Any] = {}
     self.obs_buf = {}
+    self._fused = None
     model = load_scene(cfg.scene.scene_name)
     self.scene = Scene(model, cfg.scene.num_envs, device, cfg.scene.entities,
                        cfg.scene.contact_sensors, cfg.scene.env_spacing)
@@ -156,7 +158,13 @@ class ManagerBasedRlEnv:
   # ------------------------------------------------------------------ sync-free + graph
   def _step_sync_free(self, action: torch.Tensor):
     """Same stages as step(), with every data-dependent branch turned into masks so the
-    whole env step is host-sync-free and can be captured in one HIP graph."""
+    whole env step is host-sync-free and can be captured in one HIP graph.  Velocity-task
+    configs run the fused HIP managers instead (mjlab_amd/fused.py)."""
+    if self._fused is not None:
+      self.obs_buf, rew, term, trunc = self._fused.step(action)
+      self.reward_buf, self.reset_terminated, self.reset_time_outs = rew, term, trunc
+      self.reset_buf = self._fused.reset_buf
+      return self.obs_buf, rew, term, trunc
     self.action_manager.process_action(action)
     for _ in range(self.cfg.decimation):
       self.action_manager.apply_action()
@@ -194,16 +202,24 @@ class ManagerBasedRlEnv:
       return ()
     return tuple(repr(getattr(t.cfg, "ranges", None)) for t in self.command_manager._terms.values())
 
-  def enable_graph(self, capture: bool = True) -> None:
+  def enable_graph(self, capture: bool = True, fused: bool = True) -> None:
     """Switch to the sync-free step; with capture=True record it into a HIP graph
     (replayed per step; re-recorded when a curriculum changes command ranges)."""
     self.sync_free = True
     self._use_graph = capture
+    self._fused = None
+    if fused and os.environ.get("MJX355_FUSED", "1") != "0":
+      from .fused import FusedVelocityStep
+      self._fused = FusedVelocityStep.build(self)
+      if self._fused is not None:
+        self.extras["log"] = self._fused.log()
     self._graph = None
     self._static_action = torch.zeros(self.num_envs, self.action_manager.total_action_dim,
                                       device=self.device)
 
   def _capture(self) -> None:
+    if self._fused is not None:
+      self._fused.upload()  # command ranges may have changed (curriculum)
     s = torch.cuda.Stream(device=self.device)
     s.wait_stream(torch.cuda.current_stream(self.device))
     with torch.cuda.stream(s):
@@ -222,7 +238,10 @@ class ManagerBasedRlEnv:
       self._sim_step_counter += self.cfg.decimation
       self.common_step_counter += 1
       if not self._use_graph:
-        out = self._step_sync_free(action.to(self.device))
+        if self._fused is not None and self._graph_key() != getattr(self, "_fused_key", None):
+          self._fused.upload()
+          self._fused_key = self._graph_key()
+        out = self._step_sync_free(action.to(self.device).contiguous())
         return (*out, self.extras)
       if self._graph is None or self._graph_key() != self._graph_key_captured:
         self._static_action.copy_(action)

@@ -555,7 +555,7 @@ class UniformVelocityCommand(CommandTerm):
 
   def _update_command(self):
     if self.cfg.heading_command:
-      self.heading_error = wrap_to_pi(self.heading_target - self.robot.data.heading_w)
+      self.heading_error.copy_(wrap_to_pi(self.heading_target - self.robot.data.heading_w))
       lo, hi = self.cfg.ranges.ang_vel_z
       hc = torch.clip(self.cfg.heading_control_stiffness * self.heading_error, min=lo, max=hi)
       self.vel_command_b[:, 2] = torch.where(self.is_heading_env, hc, self.vel_command_b[:, 2])

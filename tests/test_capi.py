@@ -11,12 +11,12 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "mjx355.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("mjx355.h", "mjx355_task.h")]
 LIB = os.path.join(ROOT, "mjlab-1_amd", "mjlab_amd", "libmjx355.so")
 
 
 def _declared():
-  text = open(HEADER).read()
+  text = "".join(open(h).read() for h in HEADERS)
   text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
   return sorted(set(re.findall(r"\b(mjx_[a-z_]+)\s*\(", text)))
 
@@ -31,7 +31,8 @@ def lib():
 def test_header_declares_the_api():
   names = _declared()
   for must in ("mjx_model_create", "mjx_sim_create", "mjx_step", "mjx_forward", "mjx_reset",
-               "mjx_field", "mjx_expand_field", "mjx_last_error", "mjx_forward_masked"):
+               "mjx_field", "mjx_expand_field", "mjx_last_error", "mjx_forward_masked",
+               "mjx_task_create", "mjx_task_post", "mjx_task_observe"):
     assert must in names
 
 
@@ -57,9 +58,12 @@ def test_python_binding_lists_every_export():
 
 def test_abi_version_and_desc_layout(lib):
   from mjlab_amd._capi import ModelDesc
+  from mjlab_amd.fused import TaskDesc
   lib.mjx_model_desc_size.restype = ctypes.c_size_t
+  lib.mjx_task_desc_size.restype = ctypes.c_size_t
   assert lib.mjx_abi_version() == 1
   assert lib.mjx_model_desc_size() == ctypes.sizeof(ModelDesc)
+  assert lib.mjx_task_desc_size() == ctypes.sizeof(TaskDesc)
 
 
 def test_last_error_is_a_string(lib):

@@ -210,6 +210,7 @@ def test_heading_command_update():
   cmd.heading_target = _t(tgt)
   cmd.is_heading_env = torch.as_tensor(is_h)
   cmd.is_standing_env = torch.as_tensor(is_s)
+  cmd.heading_error = torch.zeros(n)
   cmd.robot = ns(data=ns(heading_w=_t(head)))
   cmd._update_command()
   err = (tgt.astype(np.float64) - head + np.pi) % (2 * np.pi) - np.pi
