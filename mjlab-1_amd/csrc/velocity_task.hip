@@ -131,7 +131,12 @@ __global__ void k_action(const mjxTaskDesc* __restrict__ T, const float* __restr
     t.action[i] = raw;
     // separately rounded mul + add, as torch computes raw * scale + offset (no FMA), so
     // ctrl is bitwise identical to the torch manager path
-    const float target = __fadd_rn(__fmul_rn(raw, t.action_scale[k]), t.action_offset[k]);
+    float target;
+    {
+#pragma clang fp contract(off)
+      const float scaled = raw * t.action_scale[k];
+      target = scaled + t.action_offset[k];
+    }
     t.joint_pos_target[(size_t)e * nj + t.target_of_action[k]] = target;
     t.ctrl[(size_t)e * t.nu + t.ctrl_of_action[k]] = target;
   }
