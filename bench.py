@@ -165,7 +165,9 @@ def main():
       "config": {"workload": f"{args.task} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
                  "task": args.task, "num_envs_per_gpu": args.num_envs, "decimation": dec,
                  "parallelism": f"dp{world}", "mode": args.mode,
-                 "step_path": "eager" if (args.eager or args.mode != "env") else "sync-free, HIP-graph captured"},
+                 "step_path": ("eager" if (args.eager or args.mode != "env") else
+                               "sync-free, HIP-graph captured" +
+                               (", fused HIP managers" if getattr(env, "_fused", None) is not None else ""))},
       "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": achieved / HBM_PEAK_GBS,
                    "traffic": measured_traffic(args.task, args.num_envs, m.nv),
