@@ -17,6 +17,8 @@
 // stage by stage, restated in oracle/oracle.c (the parity checker).
 #include <float.h>
 #include <stdlib.h>
+#include <initializer_list>
+#include <utility>
 #include <math.h>
 
 #include "engine.h"
@@ -53,7 +55,7 @@ Lds make_lds(const Dims& d, int ph) {
   const Spec all[] = {
     {&Lds::ints, 8, A | B | Cp},
     {&Lds::qpos, d.nq, A | Cp}, {&Lds::qvel, nv, A | Cp}, {&Lds::ctrl, d.nu, A},
-    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, A}, {&Lds::xfrc, 6 * nb, A},
+    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, A}, {&Lds::xfrc, 6 * nb, 0},  // xfrc read from HBM (rare)
     {&Lds::xpos, 3 * nb, A}, {&Lds::xquat, 4 * nb, A}, {&Lds::xmat, 9 * nb, A},
     {&Lds::xipos, 3 * nb, A}, {&Lds::ximat, 9 * nb, A}, {&Lds::xanchor, 3 * d.njnt, A},
     {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, A}, {&Lds::subtree_com, 3 * nb, A | Cp},
@@ -98,6 +100,30 @@ Lds make_lds(const Dims& d, int ph) {
   if (ph == 2) for (auto f : packC) take(f);
   L.pack_len = o;
   L.packC_b = ph == 2 ? L.ints : 0;  // start of the phase-B-written part of the C pack
+  if (ph == 0) {
+    // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
+    // collision, contacts, rows.  Two aliases follow from it:
+    //  - H (Cholesky scratch of the smooth solve) lives in the contact/row block, which
+    //    is first written by collision, after the smooth solve;
+    //  - geom frames (computed at the start of collision) live in [cinert crb cacc
+    //    xanchor xaxis], all dead once RNE has run.
+    auto group = [&](std::initializer_list<int Lds::*> fs) {
+      const int start = o;
+      for (auto f : fs) take(f);
+      return std::make_pair(start, o - start);
+    };
+    auto g1 = group({&Lds::con_g1, &Lds::con_g2, &Lds::con_key, &Lds::con_dist, &Lds::con_pos,
+                     &Lds::con_frame, &Lds::con_mu, &Lds::con_solref, &Lds::con_solimp,
+                     &Lds::con_imargin, &Lds::con_dim, &Lds::con_efc, &Lds::efc_aref, &Lds::efc_D,
+                     &Lds::efc_cid, &Lds::efc_type});
+    if (g1.second >= nv * nv) L.H = g1.first;
+    auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc, &Lds::xanchor, &Lds::xaxis});
+    const int gp = (3 * d.ngeom + 3) & ~3;
+    if (g2.second >= gp + 9 * d.ngeom) {
+      L.gxpos = g2.first;
+      L.gxmat = g2.first + gp;
+    }
+  }
   const int bit = 1 << ph;
   for (const Spec& sp : all)
     if (sp.mask & bit) take(sp.f);
@@ -653,7 +679,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     int any_xfrc = 0;
     for (int i = lane; i < 6 * nb; i += kWave) {
       float v = D.xfrc_applied[(size_t)w * 6 * nb + i];
-      S[L.xfrc + i] = v;
       any_xfrc |= (v != 0.f);
     }
     any_xfrc = __any(any_xfrc);
@@ -720,16 +745,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     sync();
     {
-      const float* gpos = MF(geom_pos);
-      const float* gquat = MF(geom_quat);
-      for (int g = lane; g < d.ngeom; g += kWave) {
-        int b = m.geom_bodyid[g];
-        const float* R = S + L.xmat + 9 * b;
-        st3(S + L.gxpos + 3 * g, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
-        float Rg[9];
-        qmat(Rg, q4(gquat + 4 * g));
-        mat3mul(S + L.gxmat + 9 * g, R, Rg);
-      }
       const float* spos = MF(site_pos);
       const float* squat = MF(site_quat);
       for (int s = lane; s < d.nsite; s += kWave) {
@@ -976,7 +991,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         V3 cang = v3(cd), clin = v3(cd + 3);
         for (int b = 1; b < nb; b++) {
           if (!((bm >> b) & 1ull)) continue;
-          const float* xf = S + L.xfrc + 6 * b;
+          const float* xf = D.xfrc_applied + ((size_t)w * nb + b) * 6;
           V3 jp = clin + cross(cang, v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
           f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
         }
@@ -1049,6 +1064,19 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     STAMP(8);
     if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
+    // geom frames (here, not in kinematics: their LDS aliases regions dead after RNE)
+    {
+      const float* gpos = MF(geom_pos);
+      const float* gquat = MF(geom_quat);
+      for (int g = lane; g < d.ngeom; g += kWave) {
+        int b = m.geom_bodyid[g];
+        const float* R = S + L.xmat + 9 * b;
+        st3(S + L.gxpos + 3 * g, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
+        float Rg[9];
+        qmat(Rg, q4(gquat + 4 * g));
+        mat3mul(S + L.gxmat + 9 * g, R, Rg);
+      }
+    }
     sync();
     // =========================================================== collision
     {
