@@ -439,8 +439,17 @@ __device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, int nvp,
     const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
     A[j] *= r;
     rdiag = lane == j ? r : rdiag;
+    // pairs of broadcasts -> one SGPR pair feeding a packed FMA (v_pk_fma_f32)
 #pragma unroll
-    for (int k = j + 1; k < NR; k++) A[k] = fmaf(-A[j], rl(A[j], k), A[k]);
+    for (int k = j + 1; k < NR; k += 2) {
+      if (k + 1 < NR) {
+        const float b0 = rl(A[j], k), b1 = rl(A[j], k + 1);
+        A[k] = fmaf(-A[j], b0, A[k]);
+        A[k + 1] = fmaf(-A[j], b1, A[k + 1]);
+      } else {
+        A[k] = fmaf(-A[j], rl(A[j], k), A[k]);
+      }
+    }
   }
 }
 // Publish the strictly-lower part of L (row stride nvp) for the transposed solve.
@@ -2058,18 +2067,21 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
   if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
 }
 
-// One instantiation per (register-row length NR: multiple of 8, >= padded nv; phase).
+// One instantiation per (register-row length NR >= padded nv; phase).
 using StepFn = void (*)(const Params*, int, int, int, const uint8_t*);
 template <int NR>
 static StepFn phase_fn_nr(int ph) {
   return ph == 0 ? step_phase<NR, 0> : ph == 1 ? step_phase<NR, 1> : step_phase<NR, 2>;
 }
 static StepFn step_fn(int nv, int ph) {
+  // exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36), multiples of 8 otherwise
   const int nvp = (nv + 3) & ~3;
   if (nvp <= 8) return phase_fn_nr<8>(ph);
   if (nvp <= 16) return phase_fn_nr<16>(ph);
+  if (nvp <= 20) return phase_fn_nr<20>(ph);
   if (nvp <= 24) return phase_fn_nr<24>(ph);
   if (nvp <= 32) return phase_fn_nr<32>(ph);
+  if (nvp <= 36) return phase_fn_nr<36>(ph);
   if (nvp <= 40) return phase_fn_nr<40>(ph);
   if (nvp <= 48) return phase_fn_nr<48>(ph);
   if (nvp <= 56) return phase_fn_nr<56>(ph);
