@@ -67,7 +67,7 @@ Lds make_lds(const Dims& d, int ph) {
     {&Lds::M, nv * nv, A | B | Cp}, {&Lds::H, nv * nv, A | B | Cp},
     {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
     {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
-    {&Lds::Mx, nv, B}, {&Lds::grad, nv, B}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
+    {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
     {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, Cp},
     {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
@@ -100,6 +100,14 @@ Lds make_lds(const Dims& d, int ph) {
   if (ph == 2) for (auto f : packC) take(f);
   L.pack_len = o;
   L.packC_b = ph == 2 ? L.ints : 0;  // start of the phase-B-written part of the C pack
+  if (ph == 1) {
+    // Phase B holds M in register tiles for the whole solve (tiles_symv), so M's pack slot
+    // is reused as the Cholesky staging area H and as jt_mul's partial sums; the line-search
+    // direction J s reuses efc_aref (only read by the warmstart).
+    L.H = L.M;
+    L.red = L.M;
+    L.efc_Js = L.efc_aref;
+  }
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
     // collision, contacts, rows.  Two aliases follow from it:
@@ -498,6 +506,32 @@ __device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles
       st4v(Mm + (4 * T.bi[s] + r) * nvp + 4 * T.bj[s],
            make_float4(A[s][4 * r], A[s][4 * r + 1], A[s][4 * r + 2], A[s][4 * r + 3]));
   }
+}
+// out = A v for the symmetric matrix held as lower 4x4 register tiles (diagonal blocks
+// full); each tile contributes its block and, off the diagonal, its transpose, through LDS
+// float atomics.  Ends synced.
+__device__ __forceinline__ void tiles_symv(const float (&A)[2][16], const Tiles& T, const float* v,
+                                           float* out, int nvp, int lane) {
+  for (int i = lane; i < nvp; i += kWave) out[i] = 0.f;
+  sync();
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+    const int bi = T.bi[s], bj = T.bj[s];
+    const float4 vj = ld4(v + 4 * bj);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      atomicAdd(out + 4 * bi + r, A[s][4 * r] * vj.x + A[s][4 * r + 1] * vj.y +
+                                      A[s][4 * r + 2] * vj.z + A[s][4 * r + 3] * vj.w);
+    if (bi != bj) {
+      const float4 vi = ld4(v + 4 * bi);
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        atomicAdd(out + 4 * bj + c, A[s][c] * vi.x + A[s][4 + c] * vi.y + A[s][8 + c] * vi.z +
+                                        A[s][12 + c] * vi.w);
+    }
+  }
+  sync();
 }
 // Factor the nvp x nvp SPD matrix in Mm (row stride nvp) and solve for vector v (LDS,
 // length nvp) in place.  Lm (nvp*nvp) receives the strictly-lower factor.  Lm may alias Mm.
@@ -1588,7 +1622,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // ----------------------------------------------------------- phase B (Newton)
     const Tiles T = make_tiles(nvp, lane);
     for (int i = lane; i < nvp; i += kWave) {
-      S[L.qacc_ws + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f; S[L.grad + i] = 0.f;
+      S[L.qacc_ws + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
       S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
     }
     sync();
@@ -1601,6 +1635,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     const int nefc = ints[1];
     int ncon = ints[4];
     (void)ncon;
+    float Mt[2][16];  // M as register tiles; its LDS slot becomes H / jt_mul scratch
+    tiles_load(Mt, T, S + L.M, nvp);
+    sync();
     STAMP(15);
     // =========================================================== Newton solver
     int niter = 0;
@@ -1641,7 +1678,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       // warmstart: keep qacc_warmstart if its cost beats qacc_smooth
       for (int i = lane; i < nvp; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
       sync();
-      matvec_rows(S + L.Mx, S + L.M, S + L.x, nvp, nvp, lane);
+      tiles_symv(Mt, T, S + L.x, S + L.Mx, nvp, lane);
       set_jar(S + L.x);
       sync();
       const float cost_ws = cost_of(S + L.x, S + L.Mx);
@@ -1668,11 +1705,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         const int nact = build_active(act, jar, nefc, lane);
         for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
         sync();
-        jt_mul(S + L.grad, J, wv, act, nact, nvp, S + L.red, lane);
+        jt_mul(S + L.srch, J, wv, act, nact, nvp, S + L.red, lane);
         float gn = 0.f;
         for (int i = lane; i < nvp; i += kWave) {
-          float g = S[L.grad + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];
-          S[L.grad + i] = g;
+          float g = S[L.srch + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];  // gradient
           S[L.srch + i] = -g;
           gn += g * g;
         }
@@ -1682,7 +1718,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
         {
           float A[2][16];
-          tiles_load(A, T, S + L.M, nvp);
+#pragma unroll
+          for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int e2 = 0; e2 < 16; e2++) A[s2][e2] = Mt[s2][e2];
           tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
           tiles_store(A, T, Lm, nvp);
         }
@@ -1702,8 +1741,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           sync();
         }
         SUBSTAMP(4);
-        matvec_rows(S + L.Ms, S + L.M, S + L.srch, nvp, nvp, lane);
         matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
+        tiles_symv(Mt, T, S + L.srch, S + L.Ms, nvp, lane);
         float g1 = 0.f, sn = 0.f;
         for (int i = lane; i < nv; i += kWave) {
           float sv = S[L.srch + i];
