@@ -1706,15 +1706,20 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
         sync();
         jt_mul(S + L.srch, J, wv, act, nact, nvp, S + L.red, lane);
-        float gn = 0.f;
+        float gn = 0.f, gr = 0.f;
         for (int i = lane; i < nvp; i += kWave) {
-          float g = S[L.srch + i] + S[L.Mx + i] - S[L.qfrc_smooth + i];  // gradient
+          const float jf = S[L.srch + i], mx = S[L.Mx + i], fs = S[L.qfrc_smooth + i];
+          const float g = jf + mx - fs;  // gradient
           S[L.srch + i] = -g;
           gn += g * g;
+          const float a = fabsf(jf) + fabsf(mx) + fabsf(fs);
+          gr += a * a;
         }
         gn = sqrtf(wave_sum(gn));
+        gr = sqrtf(wave_sum(gr));
         SUBSTAMP(1);
-        if (iter > 0 && scale * gn < o.tolerance) break;
+        // MuJoCo's gradient test; floor = fp32 rounding scale of the summed terms
+        if (iter > 0 && scale * gn < fmaxf(o.tolerance, 16.f * FLT_EPSILON * scale * gr)) break;
         // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
         {
           float A[2][16];
@@ -1818,7 +1823,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         float old = cost;
         cost = cost_of(S + L.x, S + L.Mx);
         SUBSTAMP(7);
-        if (scale * (old - cost) < o.tolerance) break;
+        // MuJoCo's improvement test, with the fp32 resolution of the cost (a sum of
+        // non-negative terms, so its rounding error is ~eps*|cost|) as the floor: below
+        // it, further iterations only chase rounding noise.
+        if (scale * (old - cost) < fmaxf(o.tolerance, 4.f * FLT_EPSILON * scale * fabsf(cost))) break;
       }
       // constraint forces and qfrc_constraint = J^T f over the active rows
       sync();

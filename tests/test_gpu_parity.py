@@ -7,6 +7,7 @@ Tolerances (fp32 engine vs fp64 restatement, one step from identical inputs):
   constrained qacc / next qvel: rtol 2e-3 of the per-world scale (max|qacc|, >=1)
   sensors: same as the quantity they read.
 Contact count must match exactly unless a contact distance is within 1e-5 of zero.
+Newton iteration count: within 1 of the oracle in every world, equal in >= 90%.
 """
 
 import numpy as np
@@ -83,7 +84,9 @@ def test_step_parity(scene, gpu_device):
   qpos = d.qpos.cpu().numpy()
   sens = d.sensordata.cpu().numpy()
   af = d.actuator_force.cpu().numpy()
+  niter = d.solver_niter.cpu().numpy()
   ncontact_worlds = 0
+  niter_equal = 0
   for i, r in enumerate(ref):
     assert ncon[i] == r["ncon"], f"world {i}: ncon {ncon[i]} vs {r['ncon']}"
     ncontact_worlds += r["ncon"] > 0
@@ -94,4 +97,9 @@ def test_step_parity(scene, gpu_device):
     np.testing.assert_allclose(af[i], r["actuator_force"], atol=1e-3, rtol=1e-4)
     ssc = max(1.0, np.abs(r["sensordata"]).max())
     np.testing.assert_allclose(sens[i], r["sensordata"], atol=3e-3 * ssc, err_msg=f"sens {i}")
+    # Newton stopping: same iteration count as the fp64 oracle (fp32 rounding floors on
+    # MuJoCo's gradient/improvement tests), at most one off
+    assert abs(int(niter[i]) - r["niter"]) <= 1, f"world {i}: niter {niter[i]} vs {r['niter']}"
+    niter_equal += int(niter[i]) == r["niter"]
   assert ncontact_worlds > 0
+  assert niter_equal >= 0.9 * n
