@@ -663,6 +663,82 @@ __device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DMod
   return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
 }
 
+// mjSENS_CONTACT with one slot (sensor/contact_sensor.py:16-97, 472-533), one wave per
+// world, lane = contact: match by the geom masks, then found = popcount(ballot), netforce =
+// wave sums of the signed world-frame forces, and for mindist / maxforce / none the
+// single selected contact is the wave argmin of its key (ties -> lowest contact index).
+__device__ __forceinline__ void contact_sensors_wave(const float* S, const int* Si, const Lds& L,
+                                                     const DModel& m, const Dims& d, float* sd,
+                                                     int ncon, int lane) {
+  const int c = lane;
+  const bool valid = c < ncon;
+  int g1 = 0, g2 = 0;
+  V3 fg = {0, 0, 0}, fc = {0, 0, 0};
+  float dist = 0.f;
+  if (valid) {
+    g1 = Si[L.con_g1 + c];
+    g2 = Si[L.con_g2 + c];
+    dist = S[L.con_dist + c];
+    const int r0 = Si[L.con_efc + c];
+    if (Si[L.con_dim + c] == 1) {
+      fc.x = S[L.efc_force + r0];
+    } else {
+      float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+      float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+      fc = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+    }
+    fg = mulTv(S + L.con_frame + 9 * c, fc);
+  }
+  for (int s = 0; s < d.nsensor; s++) {
+    if (m.sensor_type[s] != SENS_CONTACT) continue;
+    const int32_t* ip = m.sensor_intprm + 3 * s;
+    if (ip[2] > 1) continue;  // multi-slot: serial path
+    const int bits = ip[0], reduce = ip[1];
+    float* out = sd + m.sensor_adr[s];
+    const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+    const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+    bool a1 = false, a2 = false;
+    if (valid) {
+      a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+      a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+    }
+    const bool match = a1 || a2;
+    const unsigned long long bal = __ballot(match);
+    const float found = (float)__popcll(bal);
+    const int dim = m.sensor_dim[s];
+    if (reduce == REDUCE_NETFORCE) {
+      const float sg = match ? (a1 ? 1.f : -1.f) : 0.f;
+      const float nx = wave_sum(sg * fg.x), ny = wave_sum(sg * fg.y), nz = wave_sum(sg * fg.z);
+      if (lane == 0) {
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        if (bits & 1) out[0] = found;
+        else if (bits & 2) { out[0] = nx; out[1] = ny; out[2] = nz; }
+      }
+      continue;
+    }
+    // one slot: the matching contact with the smallest key
+    float key = reduce == REDUCE_MINDIST ? dist
+              : reduce == REDUCE_MAXFORCE ? -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z)
+              : (float)c;
+    if (!match) key = FLT_MAX;
+    float kmin = key;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kmin = fminf(kmin, __shfl_xor(kmin, o));
+    const unsigned long long win = __ballot(match && key == kmin);
+    const int sel = win ? __ffsll((long long)win) - 1 : -1;
+    if (lane == 0) for (int i = 0; i < dim; i++) out[i] = 0.f;
+    if (sel >= 0 && lane == sel) {
+      const float sg = a1 ? 1.f : -1.f;
+      if (bits & 1) out[0] = found;
+      else if (bits & 8) out[0] = dist;
+      else if (bits & 16) { for (int t = 0; t < 3; t++) out[t] = S[L.con_pos + 3 * c + t]; }
+      else if (bits & 32) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + t]; }
+      else if (bits & 64) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+      else if (bits & 2) { out[0] = fc.x; out[1] = fc.y; out[2] = fc.z; }
+    }
+  }
+}
+
 template <int NR, int PH>
 __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int nworld,
                                                     int last, int integrate,
@@ -1446,6 +1522,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       int type = m.sensor_type[s];
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -1899,6 +1977,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       int type = m.sensor_type[s];
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -1995,6 +2075,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         }
       }
     }
+    contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon, lane);
     STAMP(11);
     if (last) {
       size_t wb = (size_t)w * nb;
