@@ -119,6 +119,9 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   if (!desc || !out) return fail("null argument");
   if (desc->abi_version != MJX_ABI_VERSION) return fail("ABI version mismatch");
   if (desc->nbody > mjx::kMaxBodies) return fail("at most 64 bodies per world supported");
+  if (desc->nv > mjx::kMaxDof) return fail("at most 64 dofs per world supported");
+  if (desc->nu > mjx::kMaxLanes || desc->njnt > mjx::kMaxLanes)
+    return fail("at most 64 actuators and 64 joints per world supported");
   if (desc->cone != 0) return fail("only pyramidal cones are supported");
   HIPCHK(hipSetDevice(device));
   auto* m = new mjxModel_();
@@ -177,6 +180,16 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   void* p = nullptr;
   if (upload(desc->dof_bodymask, sizeof(uint64_t) * d.nv, &p)) { delete m; return -1; }
   m->dm.dof_bodymask = (const uint64_t*)p;
+  {
+    // ancestor masks along dof_parentid (parents precede children in dof order)
+    std::vector<uint64_t> anc(d.nv > 0 ? d.nv : 1, 0);
+    for (int i = 0; i < d.nv; i++) {
+      const int par = desc->dof_parentid[i];
+      anc[i] = (1ull << i) | (par >= 0 && par < i ? anc[par] : 0ull);
+    }
+    if (upload(anc.data(), sizeof(uint64_t) * anc.size(), &p)) { delete m; return -1; }
+    m->dm.dof_ancmask = (const uint64_t*)p;
+  }
   if (upload(desc->sensor_geommask1, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask1 = (const uint32_t*)p;
   if (upload(desc->sensor_geommask2, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }

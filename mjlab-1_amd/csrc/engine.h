@@ -14,6 +14,7 @@ constexpr int kWave = 64;        // CDNA wavefront width
 constexpr int kMaskWords = 4;    // contact-sensor geom masks (128 geoms)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
+constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
 
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
@@ -37,6 +38,7 @@ struct DModel {
 #undef X_INT
 #undef X_FLT
   const uint64_t* dof_bodymask;
+  const uint64_t* dof_ancmask;  // bit j set: dof j is dof i itself or an ancestor (host-derived)
   const uint32_t* sensor_geommask1;
   const uint32_t* sensor_geommask2;
 };

@@ -260,13 +260,15 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
 
 #define MF(f) (m.f + (size_t)w * m.f##_ws)
 
-// Diagnostic build only (-DMJX_STAMPS): per-stage s_memtime deltas summed over worlds.
+// Diagnostic build only (-DMJX_STAMPS): per-stage s_memtime deltas, accumulated in
+// registers and added to D.prof once per wave at kernel end (STAMP_FLUSH) -- per-stamp global
+// atomics sit in vmcnt and would charge their contention to the next memory wait.
 #ifdef MJX_STAMPS
 #define STAMP(k)                                                                 \
   do {                                                                           \
     __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
-    if (lane == 0) atomicAdd((unsigned long long*)&D.prof[k], t_ - stamp_prev);   \
+    stamp_acc[k] += t_ - stamp_prev;                                             \
     stamp_prev = t_;                                                             \
   } while (0)
 // SUBSTAMP(k): nested split of the Newton stage into slots 16+ (does not advance STAMP).
@@ -274,12 +276,19 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
   do {                                                                           \
     __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
-    if (lane == 0) atomicAdd((unsigned long long*)&D.prof[16 + (k)], t_ - sub_prev); \
+    stamp_acc[16 + (k)] += t_ - sub_prev;                                        \
     sub_prev = t_;                                                               \
+  } while (0)
+#define STAMP_FLUSH()                                                            \
+  do {                                                                           \
+    if (lane == 0)                                                               \
+      for (int k_ = 0; k_ < 32; k_++)                                            \
+        if (stamp_acc[k_]) atomicAdd((unsigned long long*)&D.prof[k_], stamp_acc[k_]); \
   } while (0)
 #else
 #define STAMP(k) do {} while (0)
 #define SUBSTAMP(k) do {} while (0)
+#define STAMP_FLUSH() do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- tiled SPD algebra
@@ -639,28 +648,119 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
 __device__ __forceinline__ void cp4(float* dst, const float* src, int n, int lane) {
   for (int i = 4 * lane; i < n; i += 4 * kWave) st4v(dst + i, ld4(src + i));
 }
-// Bulk global->LDS copy of a phase's input pack: 8 float4 loads in flight per lane per
-// round trip (n is a multiple of 4 floats).
+// Bulk global->LDS copy of a phase's input pack by LDS-DMA (global_load_lds_dwordx4: each
+// wave-instruction lands 1 KiB at the wave-uniform LDS base + 16*lane, no VGPR staging), so
+// the whole pack is in flight at once; the caller waits with lds_dma_wait() before reading.
+// n is a multiple of 4 floats and dst/src are 16-byte aligned.
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* glob_void_t;
 __device__ __forceinline__ void cp_pack(float* __restrict__ dst, const float* __restrict__ src,
                                         int n, int lane) {
-  for (int i0 = 4 * lane; i0 < n; i0 += 8 * 4 * kWave) {
-    float4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int i = i0 + k * 4 * kWave;
-      if (i < n) v[k] = ld4(src + i);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int i = i0 + k * 4 * kWave;
-      if (i < n) st4v(dst + i, v[k]);
-    }
-  }
+  for (int i0 = 0; i0 < n; i0 += 4 * kWave)
+    if (i0 + 4 * lane < n)
+      __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + 4 * lane), (lds_void_t)(dst + i0),
+                                       16, 0, 0);
+}
+__device__ __forceinline__ void lds_dma_wait() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DModel& m, int b, V3 p) {
   if (b <= 0) return {0.f, 0.f, 0.f};
   const float* cv = S + L.cvel + 6 * b;
   return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+}
+
+// Per-lane model records, loaded once at phase entry: the tree passes then index registers
+// instead of walking level_body -> body_* -> jnt_* chains of dependent global loads per
+// level.  Lane i holds level-order body i (BodyRec), dof i (DofRec) and actuator i (ActRec);
+// nbody, nv, nu <= 64 (mjx_model_create).  Only a body's first joint and five children are
+// cached; further ones (rare) are read from the model arrays.
+struct BodyRec {
+  int b, p, lv, j0, jn, jt, qa, da, d0, dn, mocap, root, c0, cn, chp;
+  V3 pos, jpos, jaxis, ipos, inert;
+  Q4 quat, iquat;
+  float qp0, mass;
+};
+struct BodyPtrs {
+  const float *pos, *quat, *ipos, *iquat, *mass, *inertia, *jpos, *jaxis, *qpos0;
+};
+__device__ __forceinline__ BodyRec load_body(const DModel& m, const Dims& d, const BodyPtrs& P,
+                                             int i) {
+  BodyRec r;
+  const int b = m.level_body[i];
+  r.b = b;
+  r.lv = 0;
+  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
+  r.p = m.body_parentid[b];
+  r.j0 = m.body_jntadr[b]; r.jn = m.body_jntnum[b];
+  r.d0 = m.body_dofadr[b]; r.dn = m.body_dofnum[b];
+  r.mocap = m.body_mocapid[b];
+  r.root = m.body_rootid[b];
+  r.c0 = m.body_childadr[b]; r.cn = m.body_childadr[b + 1] - r.c0;
+  r.chp = 0;
+  for (int t = 0; t < 5 && t < r.cn; t++) r.chp |= m.body_child[r.c0 + t] << (6 * t);
+  r.pos = v3(P.pos + 3 * b); r.quat = q4(P.quat + 4 * b);
+  r.ipos = v3(P.ipos + 3 * b); r.iquat = q4(P.iquat + 4 * b);
+  r.mass = P.mass[b]; r.inert = v3(P.inertia + 3 * b);
+  const int k = r.jn > 0 ? r.j0 : 0;
+  r.jt = m.jnt_type[k]; r.qa = m.jnt_qposadr[k]; r.da = m.jnt_dofadr[k];
+  r.jpos = v3(P.jpos + 3 * k); r.jaxis = v3(P.jaxis + 3 * k);
+  r.qp0 = P.qpos0[r.qa];
+  return r;
+}
+__device__ __forceinline__ int body_child(const DModel& m, const BodyRec& r, int t) {
+  return t < 5 ? (r.chp >> (6 * t)) & 63 : m.body_child[r.c0 + t];
+}
+// joint k of body r: the cached first joint or a model read
+struct JntRec { int jt, qa, da; V3 jpos, jaxis; float qp0; };
+__device__ __forceinline__ JntRec jnt_of(const DModel& m, const BodyPtrs& P, const BodyRec& r,
+                                         int k) {
+  if (k == r.j0) return {r.jt, r.qa, r.da, r.jpos, r.jaxis, r.qp0};
+  const int qa = m.jnt_qposadr[k];
+  return {m.jnt_type[k], qa, m.jnt_dofadr[k], v3(P.jpos + 3 * k), v3(P.jaxis + 3 * k), P.qpos0[qa]};
+}
+struct BodyLite { int b, p, lv, d0, dn; };
+__device__ __forceinline__ BodyLite load_body_lite(const DModel& m, const Dims& d, int i) {
+  BodyLite r;
+  r.b = m.level_body[i];
+  r.lv = 0;
+  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
+  r.p = m.body_parentid[r.b];
+  r.d0 = m.body_dofadr[r.b]; r.dn = m.body_dofnum[r.b];
+  return r;
+}
+struct DofRec {
+  int body, jt, qa;
+  uint64_t anc;
+  float arm, damp, stiff, qs;
+};
+struct ActRec {
+  int dof, qa, ctrllim, forcelim;
+  float gear, gain, b0, b1, b2, fr0, fr1, cr0, cr1;
+};
+__device__ __forceinline__ ActRec load_act(const DModel& m, const float* gear, const float* gain,
+                                           const float* bias, const float* frange,
+                                           const float* crange, int u) {
+  ActRec r;
+  const int j = m.actuator_trnid[u];
+  r.dof = m.jnt_dofadr[j]; r.qa = m.jnt_qposadr[j];
+  r.ctrllim = m.actuator_ctrllimited[u]; r.forcelim = m.actuator_forcelimited[u];
+  r.gear = gear[u]; r.gain = gain[3 * u];
+  r.b0 = bias[3 * u]; r.b1 = bias[3 * u + 1]; r.b2 = bias[3 * u + 2];
+  r.fr0 = frange[2 * u]; r.fr1 = frange[2 * u + 1];
+  r.cr0 = crange[2 * u]; r.cr1 = crange[2 * u + 1];
+  return r;
+}
+// contact bodies packed in one int (nbody <= 64): b1 | b2 << 8 | root(b1) << 16 | root(b2) << 24
+__device__ __forceinline__ int cb_b1(int v) { return v & 255; }
+__device__ __forceinline__ int cb_b2(int v) { return (v >> 8) & 255; }
+__device__ __forceinline__ int cb_r1(int v) { return (v >> 16) & 255; }
+__device__ __forceinline__ int cb_r2(int v) { return (v >> 24) & 255; }
+__device__ __forceinline__ V3 point_vel_r(const float* S, const Lds& L, int b, int root, V3 p) {
+  if (b <= 0) return {0.f, 0.f, 0.f};
+  const float* cv = S + L.cvel + 6 * b;
+  return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * root));
 }
 
 // mjSENS_CONTACT with one slot (sensor/contact_sensor.py:16-97, 472-533), one wave per
@@ -768,6 +868,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
 #ifdef MJX_STAMPS
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
   unsigned long long sub_prev = stamp_prev;
+  unsigned long long stamp_acc[32];
+#pragma unroll
+  for (int k_ = 0; k_ < 32; k_++) stamp_acc[k_] = 0;
 #endif
   const float* body_pos = MF(body_pos);
   const float* body_quat = MF(body_quat);
@@ -802,6 +905,25 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     any_xfrc = __any(any_xfrc);
     float* Jg = gw + LB.efc_J;
+    const BodyPtrs BP{body_pos, body_quat, body_ipos, body_iquat, body_mass, body_inertia,
+                      jnt_pos, jnt_axis, qpos0};
+    const BodyRec B = load_body(m, d, BP, min(lane, nb - 1));
+    const bool bl = lane < nb;  // this lane holds a body record
+    DofRec Dr;
+    {
+      const int i = min(lane, max(nv - 1, 0));
+      const int j = m.dof_jntid[i];
+      const float* arm = MF(dof_armature);
+      const float* damping = MF(dof_damping);
+      const float* jstiff = MF(jnt_stiffness);
+      const float* qspring = MF(qpos_spring);
+      Dr.body = m.dof_bodyid[i]; Dr.anc = m.dof_ancmask[i];
+      Dr.jt = m.jnt_type[j]; Dr.qa = m.jnt_qposadr[j];
+      Dr.arm = arm[i]; Dr.damp = damping[i]; Dr.stiff = jstiff[j]; Dr.qs = qspring[Dr.qa];
+    }
+    const ActRec Ar = load_act(m, MF(actuator_gear), MF(actuator_gainprm), MF(actuator_biasprm),
+                               MF(actuator_forcerange), MF(actuator_ctrlrange),
+                               min(lane, max(nu - 1, 0)));
     sync();
     // =========================================================== kinematics (levels)
     if (lane == 0) {
@@ -810,42 +932,39 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     sync();
     for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
         float Rp[9];
         qmat(Rp, q4(S + L.xquat + 4 * p));
-        V3 pos = v3(S + L.xpos + 3 * p) + mulv(Rp, v3(body_pos + 3 * b));
-        Q4 q = qmul(q4(S + L.xquat + 4 * p), q4(body_quat + 4 * b));
-        int mid = m.body_mocapid[b];
-        if (mid >= 0) {
-          pos = v3(D.mocap_pos + ((size_t)w * d.nmocap + mid) * 3);
-          q = q4(D.mocap_quat + ((size_t)w * d.nmocap + mid) * 4);
+        V3 pos = v3(S + L.xpos + 3 * p) + mulv(Rp, B.pos);
+        Q4 q = qmul(q4(S + L.xquat + 4 * p), B.quat);
+        if (B.mocap >= 0) {
+          pos = v3(D.mocap_pos + ((size_t)w * d.nmocap + B.mocap) * 3);
+          q = q4(D.mocap_quat + ((size_t)w * d.nmocap + B.mocap) * 4);
         }
-        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
-        for (int k = j0; k < j1; k++) {
-          int a = m.jnt_qposadr[k];
+        for (int k = B.j0; k < B.j0 + B.jn; k++) {
+          const JntRec J = jnt_of(m, BP, B, k);
+          const int a = J.qa;
           float R[9];
-          if (m.jnt_type[k] == JNT_FREE) {
+          if (J.jt == JNT_FREE) {
             pos = v3(S + L.qpos + a);
             q = qnorm(q4(S + L.qpos + a + 3));
             st3(S + L.xanchor + 3 * k, pos);
             qmat(R, q);
-            st3(S + L.xaxis + 3 * k, mulv(R, v3(jnt_axis + 3 * k)));
+            st3(S + L.xaxis + 3 * k, mulv(R, J.jaxis));
             continue;
           }
           qmat(R, q);
-          V3 anchor = mulv(R, v3(jnt_pos + 3 * k)) + pos;
-          V3 axis = mulv(R, v3(jnt_axis + 3 * k));
+          V3 anchor = mulv(R, J.jpos) + pos;
+          V3 axis = mulv(R, J.jaxis);
           st3(S + L.xanchor + 3 * k, anchor);
           st3(S + L.xaxis + 3 * k, axis);
-          if (m.jnt_type[k] == JNT_HINGE) {
-            q = qmul(q, qaxisangle(v3(jnt_axis + 3 * k), S[L.qpos + a] - qpos0[a]));
+          if (J.jt == JNT_HINGE) {
+            q = qmul(q, qaxisangle(J.jaxis, S[L.qpos + a] - J.qp0));
             qmat(R, q);
-            pos = anchor - mulv(R, v3(jnt_pos + 3 * k));
-          } else if (m.jnt_type[k] == JNT_SLIDE) {
-            pos = pos + axis * (S[L.qpos + a] - qpos0[a]);
+            pos = anchor - mulv(R, J.jpos);
+          } else if (J.jt == JNT_SLIDE) {
+            pos = pos + axis * (S[L.qpos + a] - J.qp0);
           }
         }
         q = qnorm(q);
@@ -854,12 +973,13 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       sync();
     }
-    for (int b = lane; b < nb; b += kWave) {
+    if (bl) {
+      const int b = B.b;
       float* R = S + L.xmat + 9 * b;
       qmat(R, q4(S + L.xquat + 4 * b));
-      st3(S + L.xipos + 3 * b, v3(S + L.xpos + 3 * b) + mulv(R, v3(body_ipos + 3 * b)));
+      st3(S + L.xipos + 3 * b, v3(S + L.xpos + 3 * b) + mulv(R, B.ipos));
       float Ri[9];
-      qmat(Ri, q4(body_iquat + 4 * b));
+      qmat(Ri, B.iquat);
       mat3mul(S + L.ximat + 9 * b, R, Ri);
     }
     sync();
@@ -877,20 +997,18 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     STAMP(0);
     // =========================================================== com / cinert / cdof
-    for (int b = lane; b < nb; b += kWave) {
-      float ms = body_mass[b];
-      S[L.stmass + b] = ms;
-      st3(S + L.subtree_com + 3 * b, v3(S + L.xipos + 3 * b) * ms);
+    if (bl) {
+      S[L.stmass + B.b] = B.mass;
+      st3(S + L.subtree_com + 3 * B.b, v3(S + L.xipos + 3 * B.b) * B.mass);
     }
     sync();
     for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
+      if (bl && B.lv == lv) {
+        const int b = B.b;
         float ms = S[L.stmass + b];
         V3 c = v3(S + L.subtree_com + 3 * b);
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
-          int ch = m.body_child[k];
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
           ms += S[L.stmass + ch];
           c = c + v3(S + L.subtree_com + 3 * ch);
         }
@@ -899,21 +1017,22 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       sync();
     }
-    for (int b = lane; b < nb; b += kWave) {
+    if (bl) {
+      const int b = B.b;
       float ms = S[L.stmass + b];
       V3 c = ms > MINVAL ? v3(S + L.subtree_com + 3 * b) * (1.0f / ms) : v3(S + L.xipos + 3 * b);
       st3(S + L.subtree_com + 3 * b, c);
     }
     sync();
-    for (int b = lane; b < nb; b += kWave) {
+    if (bl) {
+      const int b = B.b;
       float* c = S + L.cinert + 10 * b;
       if (b == 0) {
         for (int i = 0; i < 10; i++) c[i] = 0;
-        continue;
-      }
-      V3 off = v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      } else {
+      V3 off = v3(S + L.subtree_com + 3 * B.root);
       const float* R = S + L.ximat + 9 * b;
-      const float* I = body_inertia + 3 * b;
+      const float I[3] = {B.inert.x, B.inert.y, B.inert.z};
       float full[9];
 #pragma unroll
       for (int i = 0; i < 3; i++)
@@ -922,7 +1041,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           full[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] +
                             R[3 * i + 2] * I[2] * R[3 * j + 2];
       V3 dv = v3(S + L.xipos + 3 * b) - off;
-      float ms = body_mass[b], dd = dot(dv, dv);
+      float ms = B.mass, dd = dot(dv, dv);
       c[0] = full[0] + ms * (dd - dv.x * dv.x);
       c[1] = full[4] + ms * (dd - dv.y * dv.y);
       c[2] = full[8] + ms * (dd - dv.z * dv.z);
@@ -930,11 +1049,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       c[4] = full[2] - ms * dv.x * dv.z;
       c[5] = full[5] - ms * dv.y * dv.z;
       c[6] = ms * dv.x; c[7] = ms * dv.y; c[8] = ms * dv.z; c[9] = ms;
+      }
     }
-    for (int k = lane; k < d.njnt; k += kWave) {
-      int b = m.jnt_bodyid[k], dof = m.jnt_dofadr[k];
-      V3 rel = v3(S + L.subtree_com + 3 * m.body_rootid[b]) - v3(S + L.xanchor + 3 * k);
-      int t = m.jnt_type[k];
+    // cdof: lane per body over its joints
+    for (int k = B.j0; bl && k < B.j0 + B.jn; k++) {
+      const int b = B.b;
+      const JntRec J = jnt_of(m, BP, B, k);
+      const int dof = J.da;
+      V3 rel = v3(S + L.subtree_com + 3 * B.root) - v3(S + L.xanchor + 3 * k);
+      const int t = J.jt;
       if (t == JNT_FREE) {
         for (int i = 0; i < 3; i++) {
           float* c = S + L.cdof + 6 * (dof + i);
@@ -965,13 +1088,12 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     for (int i = lane; i < 10 * nb; i += kWave) S[L.crb + i] = S[L.cinert + i];
     sync();
     for (int lv = d.nlevel - 2; lv >= 1; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
+      if (bl && B.lv == lv) {
+        const int b = B.b;
         float acc[10];
         for (int j = 0; j < 10; j++) acc[j] = S[L.crb + 10 * b + j];
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
-          int ch = m.body_child[k];
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
           for (int j = 0; j < 10; j++) acc[j] += S[L.crb + 10 * ch + j];
         }
         for (int j = 0; j < 10; j++) S[L.crb + 10 * b + j] = acc[j];
@@ -981,34 +1103,30 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     for (int i = lane; i < nvp * nvp; i += kWave) S[L.M + i] = 0;
     sync();
     for (int i = nv + lane; i < nvp; i += kWave) S[L.M + i * nvp + i] = 1.f;  // identity padding
-    {
-      const float* arm = MF(dof_armature);
-      for (int i = lane; i < nv; i += kWave) {
-        float f[6];
-        inert_mul(f, S + L.crb + 10 * m.dof_bodyid[i], S + L.cdof + 6 * i);
-        for (int j = i; j >= 0; j = m.dof_parentid[j]) {
-          float v = dot6(S + L.cdof + 6 * j, f);
-          S[L.M + i * nvp + j] = v;
-          S[L.M + j * nvp + i] = v;
-        }
-        S[L.M + i * nvp + i] += arm[i];
+    if (lane < nv) {
+      const int i = lane;
+      float f[6];
+      inert_mul(f, S + L.crb + 10 * Dr.body, S + L.cdof + 6 * i);
+      for (uint64_t a = Dr.anc; a; a &= a - 1) {  // dof i and its ancestors
+        const int j = __builtin_ctzll(a);
+        float v = dot6(S + L.cdof + 6 * j, f);
+        S[L.M + i * nvp + j] = v;
+        S[L.M + j * nvp + i] = v;
       }
+      S[L.M + i * nvp + i] += Dr.arm;
     }
     STAMP(2);
     // =========================================================== velocity stage
     if (lane < 6) S[L.cvel + lane] = 0;
     sync();
     for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
         float v[6];
         for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
-        int j0 = m.body_jntadr[b], j1 = j0 + m.body_jntnum[b];
-        for (int k = j0; k < j1; k++) {
-          int dof = m.jnt_dofadr[k];
-          if (m.jnt_type[k] == JNT_FREE) {
+        for (int k = B.j0; k < B.j0 + B.jn; k++) {
+          const int dof = k == B.j0 ? B.da : m.jnt_dofadr[k];
+          if ((k == B.j0 ? B.jt : m.jnt_type[k]) == JNT_FREE) {
             for (int a = 0; a < 3; a++) {
               for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
               for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
@@ -1029,13 +1147,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
     sync();
     for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
         float a[6];
         for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        const int d0 = B.d0, d1 = d0 + B.dn;
         for (int k = d0; k < d1 && d0 >= 0; k++)
           for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
         for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
@@ -1048,58 +1164,41 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       sync();
     }
     for (int lv = d.nlevel - 2; lv >= 1; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
+      if (bl && B.lv == lv) {
+        const int b = B.b;
         float acc[6];
         for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++) {
-          int ch = m.body_child[k];
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
           for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
         }
         for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
       }
       sync();
     }
-    {
-      const float* damping = MF(dof_damping);
-      const float* jstiff = MF(jnt_stiffness);
-      const float* qspring = MF(qpos_spring);
-      for (int i = lane; i < nv; i += kWave) {
-        S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * m.dof_bodyid[i]);
-        float pf = -damping[i] * S[L.qvel + i];
-        int j = m.dof_jntid[i];
-        int t = m.jnt_type[j];
-        if ((t == JNT_HINGE || t == JNT_SLIDE) && jstiff[j] != 0.f) {
-          int a = m.jnt_qposadr[j];
-          pf -= jstiff[j] * (S[L.qpos + a] - qspring[a]);
-        }
-        S[L.qfrc_passive + i] = pf;
-        S[L.qfrc_act + i] = 0.f;
-      }
+    if (lane < nv) {
+      const int i = lane;
+      S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * Dr.body);
+      float pf = -Dr.damp * S[L.qvel + i];
+      if ((Dr.jt == JNT_HINGE || Dr.jt == JNT_SLIDE) && Dr.stiff != 0.f)
+        pf -= Dr.stiff * (S[L.qpos + Dr.qa] - Dr.qs);
+      S[L.qfrc_passive + i] = pf;
+      S[L.qfrc_act + i] = 0.f;
     }
     sync();
     // actuation: position / motor actuators on joints
-    {
-      const float* gear = MF(actuator_gear);
-      const float* gain = MF(actuator_gainprm);
-      const float* bias = MF(actuator_biasprm);
-      const float* frange = MF(actuator_forcerange);
-      const float* crange = MF(actuator_ctrlrange);
-      for (int u = lane; u < nu; u += kWave) {
-        int j = m.actuator_trnid[u];
-        int dof = m.jnt_dofadr[j], a = m.jnt_qposadr[j];
-        float g = gear[u];
-        float len = g * S[L.qpos + a], vel = g * S[L.qvel + dof];
-        float c = S[L.ctrl + u];
-        if (m.actuator_ctrllimited[u]) c = fminf(fmaxf(c, crange[2 * u]), crange[2 * u + 1]);
-        float f = gain[3 * u] * c + bias[3 * u] + bias[3 * u + 1] * len + bias[3 * u + 2] * vel;
-        if (m.actuator_forcelimited[u]) f = fminf(fmaxf(f, frange[2 * u]), frange[2 * u + 1]);
-        S[L.act_force + u] = f;
-        S[L.act_len + u] = len;
-        S[L.act_vel + u] = vel;
-        atomicAdd(S + L.qfrc_act + dof, g * f);
-      }
+    if (lane < nu) {
+      const int u = lane;
+      const float g = Ar.gear;
+      float len = g * S[L.qpos + Ar.qa], vel = g * S[L.qvel + Ar.dof];
+      float c = S[L.ctrl + u];
+      if (Ar.ctrllim) c = fminf(fmaxf(c, Ar.cr0), Ar.cr1);
+      float f = Ar.gain * c + Ar.b0 + Ar.b1 * len + Ar.b2 * vel;
+      if (Ar.forcelim) f = fminf(fmaxf(f, Ar.fr0), Ar.fr1);
+      S[L.act_force + u] = f;
+      S[L.act_len + u] = len;
+      S[L.act_vel + u] = vel;
+      atomicAdd(S + L.qfrc_act + Ar.dof, g * f);
     }
     sync();
     for (int i = lane; i < nv; i += kWave) {
@@ -1119,16 +1218,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       S[L.qacc_smooth + i] = f;
     }
     // subtree momenta (for subtreeangmom sensors)
-    for (int b = lane; b < nb; b += kWave) {
+    if (bl) {
+      const int b = B.b;
       const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
       V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      st3(S + L.stlin + 3 * b, vc * body_mass[b]);
+      st3(S + L.stlin + 3 * b, vc * B.mass);
       const float* Ri = S + L.ximat + 9 * b;
       V3 wl = mulTv(Ri, v3(cv));
-      V3 hl = {body_inertia[3 * b] * wl.x, body_inertia[3 * b + 1] * wl.y, body_inertia[3 * b + 2] * wl.z};
+      V3 hl = {B.inert.x * wl.x, B.inert.y * wl.y, B.inert.z * wl.z};
       st3(S + L.stang + 3 * b, mulv(Ri, hl));
-      // stash body com velocity in cacc? no: recompute when needed
     }
     sync();
     STAMP(6);
@@ -1137,42 +1236,40 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     STAMP(7);
     // linear momentum of subtrees -> velocity of subtree com
     for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
+      if (bl && B.lv == lv) {
+        const int b = B.b;
         V3 acc = v3(S + L.stlin + 3 * b);
-        for (int k = m.body_childadr[b]; k < m.body_childadr[b + 1]; k++)
-          acc = acc + v3(S + L.stlin + 3 * m.body_child[k]);
+        for (int t = 0; t < B.cn; t++) acc = acc + v3(S + L.stlin + 3 * body_child(m, B, t));
         st3(S + L.stlin + 3 * b, acc);
       }
       sync();
     }
-    for (int b = lane; b < nb; b += kWave) {
+    if (bl) {
+      const int b = B.b;
       float sm = S[L.stmass + b];
       const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
       V3 vc = v3(cv + 3) + cross(v3(cv), rel);
       V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
       st3(S + L.stlin + 3 * b, lin);
     }
     sync();
-    for (int b = lane; b < nb; b += kWave) {
-      if (b == 0) continue;
+    if (bl && B.b != 0) {
+      const int b = B.b;
       const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
       V3 vc = v3(cv + 3) + cross(v3(cv), rel);
       V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
-      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * body_mass[b];
+      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * B.mass;
       st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
     }
     sync();
     for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int p = m.level_body[i];
+      if (bl && B.lv == lv) {
+        const int p = B.b;
         V3 acc = v3(S + L.stang + 3 * p);
-        for (int k = m.body_childadr[p]; k < m.body_childadr[p + 1]; k++) {
-          int b = m.body_child[k];
+        for (int t = 0; t < B.cn; t++) {
+          const int b = body_child(m, B, t);
           V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
           V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
           acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
@@ -1291,6 +1388,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       sync();
       if (lane < ncon) {
         Si[L.con_g1 + lane] = g1; Si[L.con_g2 + lane] = g2; S[L.con_dist + lane] = dist;
+        {  // con_key is dead after the sort: it now holds the packed contact bodies
+          const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+          Si[L.con_key + lane] = b1 | b2 << 8 | m.body_rootid[b1] << 16 | m.body_rootid[b2] << 24;
+        }
         S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
         // contact frame (mju_makeFrame) from the normal
         V3 n = {nx, ny, nz};
@@ -1395,7 +1496,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           if (!((side < 0 ? lim_mask & 1 : lim_mask & 2))) continue;
           float dist = side * (jrange[2 * lane + (side + 1) / 2] - q);
           Si[L.efc_type + r] = EFC_LIMIT;
-          Si[L.efc_cid + r] = -1 - lane;  // negative: limit of joint lane
+          Si[L.efc_cid + r] = -1 - (lane | m.jnt_dofadr[lane] << 8);  // negative: limit (joint | dof << 8)
           S[L.efc_aref + r] = dist;       // temporarily: pos
           S[L.efc_D + r] = (float)(-side);  // temporarily: jacobian sign
           r++;
@@ -1414,8 +1515,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int i = lane; i < nvp; i += kWave) {
         // limits
         for (int r = 0; r < lim_total && r < nefc; r++) {
-          int j = -1 - Si[L.efc_cid + r];
-          Jg[r * nvp + i] = (m.jnt_dofadr[j] == i) ? S[L.efc_D + r] : 0.f;
+          const int jd = -1 - Si[L.efc_cid + r];
+          Jg[r * nvp + i] = (jd >> 8) == i ? S[L.efc_D + r] : 0.f;
         }
         if (i >= nv) {  // zero padding columns of the contact rows
           for (int r = lim_total; r < nefc; r++) Jg[r * nvp + i] = 0.f;
@@ -1425,13 +1526,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         const float* cd = S + L.cdof + 6 * i;
         V3 cang = v3(cd), clin = v3(cd + 3);
         for (int c = 0; c < ncon; c++) {
-          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
+          const int cb = Si[L.con_key + c];
+          const int b1 = cb_b1(cb), b2 = cb_b2(cb);
           V3 pos = v3(S + L.con_pos + 3 * c);
           V3 jd = {0, 0, 0};
           if (b2 > 0 && ((bm >> b2) & 1ull))
-            jd = jd + clin + cross(cang, pos - v3(S + L.subtree_com + 3 * m.body_rootid[b2]));
+            jd = jd + clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r2(cb)));
           if (b1 > 0 && ((bm >> b1) & 1ull))
-            jd = jd - (clin + cross(cang, pos - v3(S + L.subtree_com + 3 * m.body_rootid[b1])));
+            jd = jd - (clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r1(cb))));
           const float* fr = S + L.con_frame + 9 * c;
           float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
           int r0 = Si[L.con_efc + c];
@@ -1455,18 +1557,19 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         float pos, margin, diag;
         const float *sref, *simp;
         if (type == EFC_LIMIT) {
-          int j = -1 - Si[L.efc_cid + r];
+          const int jd = -1 - Si[L.efc_cid + r];
+          const int j = jd & 255;
           pos = S[L.efc_aref + r];
           margin = jmargin[j];
-          diag = dinvw[m.jnt_dofadr[j]];
+          diag = dinvw[jd >> 8];
           sref = jsolref + 2 * j;
           simp = jsolimp + 5 * j;
         } else {
           int c = Si[L.efc_cid + r];
           pos = S[L.con_dist + c];
           margin = S[L.con_imargin + c];
-          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
-          float tran = binvw[2 * b1] + binvw[2 * b2];
+          const int cb = Si[L.con_key + c];
+          float tran = binvw[2 * cb_b1(cb)] + binvw[2 * cb_b2(cb)];
           if (type == EFC_FRICTIONLESS) {
             diag = tran;
           } else {
@@ -1491,12 +1594,12 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         // efc_vel = J qvel, evaluated from the body velocities (cvel is the same chain sum)
         float vel;
         if (type == EFC_LIMIT) {
-          vel = S[L.efc_D + r] * S[L.qvel + m.jnt_dofadr[-1 - Si[L.efc_cid + r]]];
+          vel = S[L.efc_D + r] * S[L.qvel + ((-1 - Si[L.efc_cid + r]) >> 8)];
         } else {
           int c = Si[L.efc_cid + r];
           V3 pc = v3(S + L.con_pos + 3 * c);
-          int b1 = m.geom_bodyid[Si[L.con_g1 + c]], b2 = m.geom_bodyid[Si[L.con_g2 + c]];
-          V3 v = point_vel(S, L, m, b2, pc) - point_vel(S, L, m, b1, pc);
+          const int cb = Si[L.con_key + c];
+          V3 v = point_vel_r(S, L, cb_b2(cb), cb_r2(cb), pc) - point_vel_r(S, L, cb_b1(cb), cb_r1(cb), pc);
           const float* fr = S + L.con_frame + 9 * c;
           vel = fr[0] * v.x + fr[1] * v.y + fr[2] * v.z;
           if (type != EFC_FRICTIONLESS) {
@@ -1698,17 +1801,17 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     STAMP(14);
   } else if constexpr (PH == 1) {
     // ----------------------------------------------------------- phase B (Newton)
-    const Tiles T = make_tiles(nvp, lane);
-    for (int i = lane; i < nvp; i += kWave) {
-      S[L.qacc_ws + i] = 0.f; S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
-      S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
-    }
-    sync();
-    for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
     {
       const int nefc_in = reinterpret_cast<const int*>(gw)[LB.ints + 1];
-      cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
+        cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
     }
+    const Tiles T = make_tiles(nvp, lane);
+    for (int i = lane; i < nvp; i += kWave) {
+      S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
+      S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
+      S[L.qacc_ws + i] = i < nv ? D.qacc_warmstart[(size_t)w * nv + i] : 0.f;
+    }
+    lds_dma_wait();
     sync();
     const int nefc = ints[1];
     int ncon = ints[4];
@@ -1935,17 +2038,22 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     STAMP(14);
   } else {
     // ----------------------------------------------------------- phase C
-    for (int i = lane; i < nvp; i += kWave) {
-      S[L.qvel + i] = 0.f; S[L.qacc_ws + i] = 0.f; S[L.vtmp + i] = 0.f;
-    }
-    sync();
-    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
-    for (int i = lane; i < nv; i += kWave) {
-      S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
-      S[L.qacc_ws + i] = D.qacc_warmstart[(size_t)w * nv + i];
-    }
-    float time = D.time[w];
     cp_pack(S, gc, L.pack_len, lane);  // C pack: carve offsets == pack offsets
+    for (int i = lane; i < nvp; i += kWave) {
+      const bool in = i < nv;
+      S[L.qvel + i] = in ? D.qvel[(size_t)w * nv + i] : 0.f;
+      S[L.qacc_ws + i] = in ? D.qacc_warmstart[(size_t)w * nv + i] : 0.f;
+      S[L.vtmp + i] = 0.f;
+    }
+    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
+    float time = D.time[w];
+    const BodyLite B = load_body_lite(m, d, min(lane, nb - 1));
+    const bool bl = lane < nb;
+    const ActRec Ar = load_act(m, MF(actuator_gear), MF(actuator_gainprm), MF(actuator_biasprm),
+                               MF(actuator_forcerange), MF(actuator_ctrlrange),
+                               min(lane, max(nu - 1, 0)));
+    const float damp_l = MF(dof_damping)[min(lane, max(nv - 1, 0))];
+    lds_dma_wait();
     sync();
     const int nefc = ints[1];
     int ncon = ints[4];
@@ -1955,13 +2063,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
     sync();
     for (int lv = 1; lv < d.nlevel; lv++) {
-      int s0 = m.level_start[lv], s1 = m.level_start[lv + 1];
-      for (int i = s0 + lane; i < s1; i += kWave) {
-        int b = m.level_body[i];
-        int p = m.body_parentid[b];
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
         float a[6];
         for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        int d0 = m.body_dofadr[b], d1 = d0 + m.body_dofnum[b];
+        const int d0 = B.d0, d1 = d0 + B.dn;
         for (int k = d0; k < d1 && d0 >= 0; k++)
           for (int j = 0; j < 6; j++)
             a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
@@ -2106,35 +2212,32 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
     }
     STAMP(12);
+#ifdef MJX_STAMPS
+    sub_prev = __builtin_amdgcn_s_memtime();
+#endif
     if (integrate) {
       sync();
     // =========================================================== implicitfast / Euler
     sync();
     {
-      const float* damping = MF(dof_damping);
-      for (int i = lane; i < nvp; i += kWave) S[L.hdiag + i] = i < nv ? h * damping[i] : 0.f;
+      for (int i = lane; i < nvp; i += kWave) S[L.hdiag + i] = i < nv ? h * damp_l : 0.f;
       sync();
-      if (o.integrator == 1) {
-        const float* gear = MF(actuator_gear);
-        const float* bias = MF(actuator_biasprm);
-        const float* frange = MF(actuator_forcerange);
-        for (int u = lane; u < nu; u += kWave) {
-          if (m.actuator_forcelimited[u]) {
-            float fo = S[L.act_force + u];
-            if (fo <= frange[2 * u] || fo >= frange[2 * u + 1]) continue;
-          }
-          float bv = bias[3 * u + 2];
-          if (bv == 0.f) continue;
-          int dof = m.jnt_dofadr[m.actuator_trnid[u]];
-          float g = gear[u];
-          atomicAdd(S + L.hdiag + dof, -h * g * g * bv);
+      SUBSTAMP(9);
+      if (o.integrator == 1 && lane < nu) {
+        bool skip = Ar.b2 == 0.f;
+        if (Ar.forcelim) {
+          const float fo = S[L.act_force + lane];
+          skip = skip || fo <= Ar.fr0 || fo >= Ar.fr1;
         }
+        if (!skip) atomicAdd(S + L.hdiag + Ar.dof, -h * Ar.gear * Ar.gear * Ar.b2);
       }
       for (int i = lane; i < nvp; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
       sync();
+      SUBSTAMP(10);
       spd_factor_solve<NR>(S + L.M, S + L.hdiag, S + L.H, S + L.vtmp, nvp, lane);
       for (int i = lane; i < nv; i += kWave) S[L.qvel + i] += h * S[L.vtmp + i];
       sync();
+      SUBSTAMP(11);
       for (int k = lane; k < d.njnt; k += kWave) {
         int a = m.jnt_qposadr[k], dof = m.jnt_dofadr[k];
         int t = m.jnt_type[k];
@@ -2153,6 +2256,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = S[L.x + i];
       time += h;
       sync();
+      SUBSTAMP(12);
     }
 
       for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];
@@ -2164,6 +2268,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     STAMP(13);
   }
+  STAMP_FLUSH();
 }
 
 // --------------------------------------------------------------------------- reset
