@@ -63,9 +63,9 @@ struct Lds {
   int M, H;
   int qfrc_bias, qfrc_passive, qfrc_act, qfrc_smooth, qacc_smooth, x, Mx, grad, srch, Ms,
       qfrc_con, vtmp, act_force, act_len, act_vel;
-  int con_g1, con_g2, con_key, con_dist, con_pos, con_frame, con_mu, con_solref,
-      con_solimp, con_imargin, con_dim, con_efc;
-  int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_type, efc_act, hdiag;
+  int con_g1, con_g2, con_key, con_dist, con_pos, con_frame, con_mu, con_kb,
+      con_imp, con_imargin, con_dim, con_efc;
+  int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_act, hdiag;
   int red;      // 5*kWave scratch (J^T w partial sums)
   int ints;     // small int block: [0]=raw ncon [1]=nefc [2]=nlimit [3]=flags [4]=ncon [5]=niter
   int pack_len; // length of the phase's input pack (carved first; see make_lds)

@@ -72,12 +72,12 @@ Lds make_lds(const Dims& d, int ph) {
     {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
     {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, A | Cp},
-    {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_solref, 2 * C, A}, {&Lds::con_solimp, 5 * C, A},
+    {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_kb, 2 * C, A}, {&Lds::con_imp, C, A},
     {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
     {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
     {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
     {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
-    {&Lds::efc_type, R, A}, {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, Cp},
+    {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, Cp},
     {&Lds::red, 5 * kWave, B},
   };
   static int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
@@ -108,10 +108,11 @@ Lds make_lds(const Dims& d, int ph) {
     L.red = L.M;
     L.efc_Js = L.efc_aref;
   }
+  if (ph == 2) L.H = L.M;  // integrate factors M + h D in place (M is dead afterwards)
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
     // collision, contacts, rows.  Two aliases follow from it:
-    //  - H (Cholesky scratch of the smooth solve) lives in the contact/row block, which
+    //  - M and H (the smooth solve's in-place factor) live in the contact/row block, which
     //    is first written by collision, after the smooth solve;
     //  - geom frames (computed at the start of collision) live in [cinert crb cacc
     //    xanchor xaxis], all dead once RNE has run.
@@ -121,10 +122,12 @@ Lds make_lds(const Dims& d, int ph) {
       return std::make_pair(start, o - start);
     };
     auto g1 = group({&Lds::con_g1, &Lds::con_g2, &Lds::con_key, &Lds::con_dist, &Lds::con_pos,
-                     &Lds::con_frame, &Lds::con_mu, &Lds::con_solref, &Lds::con_solimp,
+                     &Lds::con_frame, &Lds::con_mu, &Lds::con_kb, &Lds::con_imp,
                      &Lds::con_imargin, &Lds::con_dim, &Lds::con_efc, &Lds::efc_aref, &Lds::efc_D,
-                     &Lds::efc_cid, &Lds::efc_type});
-    if (g1.second >= nv * nv) L.H = g1.first;
+                     &Lds::efc_cid});
+    // M (assembled after CRB, copied to the B/C packs at once, factored in place by the
+    // smooth solve) is dead before collision: M and H share the contact/row block too.
+    if (g1.second >= nv * nv) L.M = L.H = g1.first;
     auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc, &Lds::xanchor, &Lds::xaxis});
     const int gp = (3 * d.ngeom + 3) & ~3;
     if (g2.second >= gp + 9 * d.ngeom) {
@@ -636,6 +639,24 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
   return dmin + y * (dmax - dmin);
 }
 
+// reference stiffness / damping of a constraint row (mj_makeImpedance, solref > 0: time
+// constant and damping ratio; solref <= 0: direct stiffness and damping)
+__device__ __forceinline__ void solref_kb(const float* sref, const float* simp, float h, float& K,
+                                          float& B) {
+  const float dmax = fminf(MAXIMP, fmaxf(MINIMP, simp[1]));
+  if (sref[0] > 0) {
+    const float tc = fmaxf(sref[0], 2 * h), dr = sref[1];
+    K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+    B = 2.0f / (dmax * tc);
+  } else {
+    K = -sref[0] / (dmax * dmax);
+    B = -sref[1] / dmax;
+  }
+}
+// efc_cid row code: type (2 bits) | payload << 2; payload = contact index, or for joint
+// limits joint | dof << 8
+__device__ __forceinline__ int efc_code(int type, int payload) { return type | payload << 2; }
+
 // --------------------------------------------------------------------------- kernels
 // One substep = three launches, each holding only its own working set in LDS (more
 // resident worlds per CU); hand-off through the per-world global scratch P->gscr, laid out
@@ -1115,6 +1136,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       S[L.M + i * nvp + i] += Dr.arm;
     }
+    sync();
+    // M to the B and C packs now: its LDS slot is reused (in place factor, then contacts)
+    cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
+    cp4(gc + LC.M, S + L.M, nvp * nvp, lane);
     STAMP(2);
     // =========================================================== velocity stage
     if (lane < 6) S[L.cvel + lane] = 0;
@@ -1412,8 +1437,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         int p1 = m.geom_priority[g1], p2 = m.geom_priority[g2];
         int dim;
         float f0, f1;
-        float* sr = S + L.con_solref + 2 * lane;
-        float* si = S + L.con_solimp + 5 * lane;
+        float sr[2], si[5];
         if (p1 != p2) {
           int g = p1 > p2 ? g1 : g2;
           dim = m.geom_condim[g];
@@ -1444,7 +1468,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         S[L.con_mu + 2 * lane] = fmaxf(MINMU, f0);
         S[L.con_mu + 2 * lane + 1] = fmaxf(MINMU, f0);
         Si[L.con_dim + lane] = dim;
-        S[L.con_imargin + lane] = fmaxf(gmar[g1], gmar[g2]) - fmaxf(ggap[g1], ggap[g2]);
+        const float imargin = fmaxf(gmar[g1], gmar[g2]) - fmaxf(ggap[g1], ggap[g2]);
+        S[L.con_imargin + lane] = imargin;
+        // row impedance and reference K, B are per contact: computed once here
+        S[L.con_imp + lane] = impedance(si, dist, imargin);
+        solref_kb(sr, si, h, S[L.con_kb + 2 * lane], S[L.con_kb + 2 * lane + 1]);
       }
       sync();
     }
@@ -1495,8 +1523,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         for (int side = -1; side <= 1; side += 2) {
           if (!((side < 0 ? lim_mask & 1 : lim_mask & 2))) continue;
           float dist = side * (jrange[2 * lane + (side + 1) / 2] - q);
-          Si[L.efc_type + r] = EFC_LIMIT;
-          Si[L.efc_cid + r] = -1 - (lane | m.jnt_dofadr[lane] << 8);  // negative: limit (joint | dof << 8)
+          Si[L.efc_cid + r] = efc_code(EFC_LIMIT, lane | m.jnt_dofadr[lane] << 8);
           S[L.efc_aref + r] = dist;       // temporarily: pos
           S[L.efc_D + r] = (float)(-side);  // temporarily: jacobian sign
           r++;
@@ -1505,17 +1532,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       if (lane < ncon) {
         int r0 = lim_total + con_off;
         Si[L.con_efc + lane] = r0;
-        for (int k = 0; k < crow; k++) {
-          Si[L.efc_type + r0 + k] = cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL;
-          Si[L.efc_cid + r0 + k] = lane;
-        }
+        for (int k = 0; k < crow; k++)
+          Si[L.efc_cid + r0 + k] = efc_code(cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, lane);
       }
       sync();
       // Jacobian rows: lane per dof
       for (int i = lane; i < nvp; i += kWave) {
         // limits
         for (int r = 0; r < lim_total && r < nefc; r++) {
-          const int jd = -1 - Si[L.efc_cid + r];
+          const int jd = Si[L.efc_cid + r] >> 2;
           Jg[r * nvp + i] = (jd >> 8) == i ? S[L.efc_D + r] : 0.f;
         }
         if (i >= nv) {  // zero padding columns of the contact rows
@@ -1553,19 +1578,18 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       sync();
       // row parameters: lane per row
       for (int r = lane; r < nefc; r += kWave) {
-        int type = Si[L.efc_type + r];
-        float pos, margin, diag;
-        const float *sref, *simp;
+        const int code = Si[L.efc_cid + r];
+        const int type = code & 3, pl = code >> 2;  // pl: contact, or joint | dof << 8
+        float pos, margin, diag, imp, K, B;
         if (type == EFC_LIMIT) {
-          const int jd = -1 - Si[L.efc_cid + r];
-          const int j = jd & 255;
+          const int j = pl & 255;
           pos = S[L.efc_aref + r];
           margin = jmargin[j];
-          diag = dinvw[jd >> 8];
-          sref = jsolref + 2 * j;
-          simp = jsolimp + 5 * j;
+          diag = dinvw[pl >> 8];
+          imp = impedance(jsolimp + 5 * j, pos, margin);
+          solref_kb(jsolref + 2 * j, jsolimp + 5 * j, h, K, B);
         } else {
-          int c = Si[L.efc_cid + r];
+          const int c = pl;
           pos = S[L.con_dist + c];
           margin = S[L.con_imargin + c];
           const int cb = Si[L.con_key + c];
@@ -1576,27 +1600,17 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
             float mu = S[L.con_mu + 2 * c + ((r - Si[L.con_efc + c]) >> 1)];
             diag = (tran + mu * mu * tran) / o.impratio;
           }
-          sref = S + L.con_solref + 2 * c;
-          simp = S + L.con_solimp + 5 * c;
+          imp = S[L.con_imp + c];
+          K = S[L.con_kb + 2 * c];
+          B = S[L.con_kb + 2 * c + 1];
         }
-        float imp = impedance(simp, pos, margin);
         float Rr = fmaxf(MINVAL, (1 - imp) * diag / imp);
-        float dmax = fminf(MAXIMP, fmaxf(MINIMP, simp[1]));
-        float K, B;
-        if (sref[0] > 0) {
-          float tc = fmaxf(sref[0], 2 * h), dr = sref[1];
-          K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
-          B = 2.0f / (dmax * tc);
-        } else {
-          K = -sref[0] / (dmax * dmax);
-          B = -sref[1] / dmax;
-        }
         // efc_vel = J qvel, evaluated from the body velocities (cvel is the same chain sum)
         float vel;
         if (type == EFC_LIMIT) {
-          vel = S[L.efc_D + r] * S[L.qvel + ((-1 - Si[L.efc_cid + r]) >> 8)];
+          vel = S[L.efc_D + r] * S[L.qvel + (pl >> 8)];
         } else {
-          int c = Si[L.efc_cid + r];
+          const int c = pl;
           V3 pc = v3(S + L.con_pos + 3 * c);
           const int cb = Si[L.con_key + c];
           V3 v = point_vel_r(S, L, cb_b2(cb), cb_r2(cb), pc) - point_vel_r(S, L, cb_b1(cb), cb_r1(cb), pc);
@@ -1776,7 +1790,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     const int C4 = (C + 3) & ~3;
     const int nr4 = (nefc + 3) & ~3;
     cp4(gw + LB.ints, S + L.ints, 8, lane);
-    cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
     cp4(gw + LB.qacc_smooth, S + L.qacc_smooth, nvq, lane);
     cp4(gw + LB.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
     cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
@@ -1796,7 +1809,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
     cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
     cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
-    cp4(gc + LC.M, S + L.M, nvp * nvp, lane);
     cp4(gc + LC.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
     STAMP(14);
   } else if constexpr (PH == 1) {
