@@ -390,7 +390,10 @@ __device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const f
 // out[c] = sum_k J[act[k], c] * wv[act[k]] (c < nvp).  Lanes split (column block, row
 // group); partial sums reduced through `part` (>= 64*4 floats).  Ends with a sync.
 __device__ __forceinline__ void jt_mul(float* out, const float* J, const float* wv, const int* act, int nact,
-                       int nvp, float* part, int lane) {
+                       int nvp, int lane) {
+  // lane = g * nb + cb: column block cb (4 columns) summed over the rows k = g (mod ng),
+  // then the ng group partials are folded by a fixed shuffle tree (no LDS scratch, so the
+  // Newton factor in the H slot survives across iterations)
   const int nb = nvp >> 2;
   const int ng = kWave / nb;
   const int cb = lane % nb, g = lane / nb;
@@ -402,26 +405,36 @@ __device__ __forceinline__ void jt_mul(float* out, const float* J, const float* 
       float wr = wv[r];
       acc.x += j.x * wr; acc.y += j.y * wr; acc.z += j.z * wr; acc.w += j.w * wr;
     }
-    st4v(part + g * nvp + 4 * cb, acc);
   }
-  sync();
-  for (int c = lane; c < nvp; c += kWave) {
-    float s = 0.f;
-    for (int gg = 0; gg < ng; gg++) s += part[gg * nvp + c];
-    out[c] = s;
+  for (int off = 1; off < ng; off <<= 1) {
+    const int src = min(lane + off * nb, kWave - 1);
+    const bool take = g + off < ng;
+    const float x = __shfl(acc.x, src), y = __shfl(acc.y, src);
+    const float z = __shfl(acc.z, src), w = __shfl(acc.w, src);
+    if (take) { acc.x += x; acc.y += y; acc.z += z; acc.w += w; }
   }
+  if (g == 0) st4v(out + 4 * cb, acc);
   sync();
 }
-// Compact the rows with jar < 0 into act[]; returns the count (wave-uniform).
-__device__ __forceinline__ int build_active(int* act, const float* jar, int nefc, int lane) {
+// Compact the rows with jar < 0 into act[]; returns the count (wave-uniform).  sig holds
+// the active set of the previous call as 64-row ballots; *same is set when it is unchanged
+// (then H = M + J_act^T D J_act is unchanged too).  Sets over 4*64 rows never compare same.
+__device__ __forceinline__ int build_active(int* act, const float* jar, int nefc, int lane,
+                                            unsigned long long (&sig)[4], bool* same) {
   int base = 0;
-  for (int r0 = 0; r0 < nefc; r0 += kWave) {
+  bool eq = nefc <= 4 * kWave;
+  for (int r0 = 0, k = 0; r0 < nefc; r0 += kWave, k++) {
     int r = r0 + lane;
     bool f = r < nefc && jar[r] < 0.f;
     unsigned long long bal = __ballot(f);
     if (f) act[base + __popcll(bal & ((1ull << lane) - 1ull))] = r;
     base += __popcll(bal);
+    if (k < 4) {
+      eq = eq && bal == sig[k];
+      sig[k] = bal;
+    }
   }
+  *same = eq;
   return base;
 }
 
@@ -472,15 +485,27 @@ __device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, int nvp,
     }
   }
 }
-// Publish the strictly-lower part of L (row stride nvp) for the transposed solve.
+// Publish L (row stride nvp): strictly-lower part, 1/L[i][i] on the diagonal, zeros above.
+// The solves never let a diagonal entry reach another lane (a lane's own y is dead once it
+// has been broadcast), so rows_solve can run from these rows (rows_load_factor) as well.
 template <int NR>
-__device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float* Lm, int nvp, int lane) {
+__device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float rd, float* Lm, int nvp,
+                                                  int lane) {
   if (lane >= nvp) return;
 #pragma unroll
   for (int c = 0; c < NR; c += 4)
     if (c < nvp)
-      st4v(Lm + lane * nvp + c, make_float4(c < lane ? A[c] : 0.f, c + 1 < lane ? A[c + 1] : 0.f,
-                                            c + 2 < lane ? A[c + 2] : 0.f, c + 3 < lane ? A[c + 3] : 0.f));
+      st4v(Lm + lane * nvp + c,
+           make_float4(c < lane ? A[c] : c == lane ? rd : 0.f, c + 1 < lane ? A[c + 1] : c + 1 == lane ? rd : 0.f,
+                       c + 2 < lane ? A[c + 2] : c + 2 == lane ? rd : 0.f,
+                       c + 3 < lane ? A[c + 3] : c + 3 == lane ? rd : 0.f));
+}
+// Rows of a factor stored by rows_store_strict, and this lane's 1/L[i][i].
+template <int NR>
+__device__ __forceinline__ void rows_load_factor(float (&A)[NR], float& rd, const float* Lm, int nvp,
+                                                 int lane) {
+  rows_load<NR>(A, Lm, nvp, lane);
+  rd = lane < nvp ? Lm[lane * nvp + lane] : 1.f;
 }
 // x (lane i holds x[i]) <- (L L^T)^-1 x.  Forward from the register rows, backward from
 // columns of the strictly-lower L in Lm (written by rows_store_strict, then synced).
@@ -558,7 +583,7 @@ __device__ __forceinline__ void spd_factor_solve(const float* Mm, const float* d
   }
   float rd;
   rows_chol<NR>(A, rd, nvp, lane);
-  rows_store_strict<NR>(A, Lm, nvp, lane);
+  rows_store_strict<NR>(A, rd, Lm, nvp, lane);
   sync();
   float x = lane < nvp ? v[lane] : 0.f;
   x = rows_solve<NR>(A, rd, Lm, x, nvp, lane);
@@ -1893,12 +1918,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       sync();
       SUBSTAMP(0);
+      unsigned long long act_sig[4] = {~0ull, ~0ull, ~0ull, ~0ull};
       for (int iter = 0; iter < o.iterations; iter++) {
         // gradient = M x - qfrc_smooth + J_act^T (D jar)
-        const int nact = build_active(act, jar, nefc, lane);
+        bool same_set;
+        const int nact = build_active(act, jar, nefc, lane, act_sig, &same_set);
+        // H depends on the active set only: unchanged set -> reuse the stored factor (exact)
+        const bool refactor = iter == 0 || !same_set;
         for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
         sync();
-        jt_mul(S + L.srch, J, wv, act, nact, nvp, S + L.red, lane);
+        jt_mul(S + L.srch, J, wv, act, nact, nvp, lane);
         float gn = 0.f, gr = 0.f;
         for (int i = lane; i < nvp; i += kWave) {
           const float jf = S[L.srch + i], mx = S[L.Mx + i], fs = S[L.qfrc_smooth + i];
@@ -1914,7 +1943,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         // MuJoCo's gradient test; floor = fp32 rounding scale of the summed terms
         if (iter > 0 && scale * gn < fmaxf(o.tolerance, 16.f * FLT_EPSILON * scale * gr)) break;
         // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
-        {
+        if (refactor) {
           float A[2][16];
 #pragma unroll
           for (int s2 = 0; s2 < 2; s2++)
@@ -1927,10 +1956,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         SUBSTAMP(2);
         {
           float R[NR];
-          rows_load<NR>(R, Lm, nvp, lane);
           float rd;
-          rows_chol<NR>(R, rd, nvp, lane);
-          rows_store_strict<NR>(R, Lm, nvp, lane);
+          if (refactor) {
+            rows_load<NR>(R, Lm, nvp, lane);
+            rows_chol<NR>(R, rd, nvp, lane);
+            rows_store_strict<NR>(R, rd, Lm, nvp, lane);
+          } else {
+            rows_load_factor<NR>(R, rd, Lm, nvp, lane);
+          }
           sync();
           SUBSTAMP(3);
           float xs = lane < nvp ? S[L.srch + lane] : 0.f;
@@ -2027,9 +2060,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         float ja = jar[r];
         wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
       }
-      const int nact = build_active(act, jar, nefc, lane);
+      unsigned long long sig_f[4] = {0, 0, 0, 0};
+      bool same_f;
+      const int nact = build_active(act, jar, nefc, lane, sig_f, &same_f);
       sync();
-      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, S + L.red, lane);
+      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, lane);
       SUBSTAMP(8);
     }
     STAMP(9);
@@ -2333,14 +2368,19 @@ static StepFn step_fn(int nv, int ph) {
   return phase_fn_nr<64>(ph);
 }
 
-// Diagnostic: MJX355_LDS_PAD=<bytes> adds unused dynamic LDS per world, to measure how
-// throughput depends on resident worlds per CU.
+// Diagnostic: MJX355_LDS_PAD=<bytes> (all phases) or MJX355_LDS_PAD<ph>=<bytes> (phase 0/1/2)
+// adds unused dynamic LDS per world, to measure how throughput depends on resident worlds
+// per CU.
 static size_t lds_bytes(const Params& host, int ph) {
-  static const long pad = [] {
+  static const long pad[3] = {[] { const char* e = getenv("MJX355_LDS_PAD0"); return e ? atol(e) : 0L; }(),
+                              [] { const char* e = getenv("MJX355_LDS_PAD1"); return e ? atol(e) : 0L; }(),
+                              [] { const char* e = getenv("MJX355_LDS_PAD2"); return e ? atol(e) : 0L; }()};
+  static const long pad_all = [] {
     const char* e = getenv("MJX355_LDS_PAD");
     return e ? atol(e) : 0L;
   }();
-  return (size_t)host.LP[ph].total * 4 + (size_t)(pad > 0 ? pad : 0);
+  const long p = pad_all + pad[ph];
+  return (size_t)host.LP[ph].total * 4 + (size_t)(p > 0 ? p : 0);
 }
 
 hipError_t prepare_step(const Params& host) {
