@@ -16,8 +16,9 @@ three phases of one substep); algorithmic bytes per env-step
 B_env = 4*[dec*(2nq+5nv+2nu+ns+1) + 16*nbody + 72], per launch
 B_env/dec per world; achieved = bytes/launch / mean launch time (HIP events on the
 launch stream); peak 8 TB/s (MI355X_MICROARCH.md).  `traffic` = HBM bytes per launch from
-the committed PMC measurement profiles/r01_hbm_traffic.json (FETCH_SIZE x2 + WRITE_SIZE,
-separate rocprofv3 passes) when it was taken on this task / num_envs / nv, else null.
+the committed PMC measurements profiles/*_hbm_traffic.json (FETCH_SIZE x2 + WRITE_SIZE,
+separate rocprofv3 passes, scripts/profile_round.sh) when one was taken on this task /
+num_envs / nv (latest round first), else null.
 cpu_baseline: the fp64 CPU oracle (oracle/liboracle.so, "port"), OpenMP over worlds on
 the box's host cores, bounded sample.
 """
@@ -46,15 +47,16 @@ def b_env(m, dec):
 
 
 def measured_traffic(task, num_envs, nv):
-  path = os.path.join(ROOT, "profiles", "r01_hbm_traffic.json")
-  try:
-    with open(path) as fh:
-      t = json.load(fh)
-  except (OSError, ValueError):
-    return None
-  if (t.get("task"), t.get("num_envs"), t.get("nv")) != (task, num_envs, nv):
-    return None
-  return float(t["traffic_bytes_per_launch"])
+  import glob
+  for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
+    try:
+      with open(path) as fh:
+        t = json.load(fh)
+    except (OSError, ValueError):
+      continue
+    if (t.get("task"), t.get("num_envs"), t.get("nv")) == (task, num_envs, nv):
+      return float(t["traffic_bytes_per_launch"])
+  return None
 
 
 def cpu_baseline(model, dec, budget_s=12.0):
