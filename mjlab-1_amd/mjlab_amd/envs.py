@@ -217,20 +217,27 @@ class ManagerBasedRlEnv:
     self._static_action = torch.zeros(self.num_envs, self.action_manager.total_action_dim,
                                       device=self.device)
 
-  def _capture(self) -> None:
+  def _capture(self, action: torch.Tensor):
+    """Run one real sync-free step (it also warms the allocator and lazy tensors), then
+    record the step into a HIP graph.  Recording executes nothing, so the env advances
+    exactly one step per call, as in eager mode."""
     if self._fused is not None:
       self._fused.upload()  # command ranges may have changed (curriculum)
+    self._static_action.copy_(action)
     s = torch.cuda.Stream(device=self.device)
     s.wait_stream(torch.cuda.current_stream(self.device))
     with torch.cuda.stream(s):
-      for _ in range(2):  # warm up allocator + lazy tensors outside the capture
-        self._step_sync_free(self._static_action)
+      out = tuple(t.clone() for t in self._step_sync_free(self._static_action)[1:])
+      obs = {k: v.clone() for k, v in self.obs_buf.items()}
     torch.cuda.current_stream(self.device).wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
       self._graph_out = self._step_sync_free(self._static_action)
     self._graph = g
     self._graph_key_captured = self._graph_key()
+    self.obs_buf = obs
+    self.reward_buf, self.reset_terminated, self.reset_time_outs = out
+    return (obs, *out)
 
   def step(self, action: torch.Tensor):
     if getattr(self, "sync_free", False):
@@ -244,8 +251,7 @@ class ManagerBasedRlEnv:
         out = self._step_sync_free(action.to(self.device).contiguous())
         return (*out, self.extras)
       if self._graph is None or self._graph_key() != self._graph_key_captured:
-        self._static_action.copy_(action)
-        self._capture()
+        return (*self._capture(action), self.extras)
       self._static_action.copy_(action)
       self._graph.replay()
       self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs = self._graph_out
@@ -478,9 +484,15 @@ def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   return cfg
 
 
+def _tracking_g1(play: bool = False):
+  from .tracking import unitree_g1_flat_tracking_env_cfg
+  return unitree_g1_flat_tracking_env_cfg(play=play)
+
+
 TASKS = {
   "Mjlab-Velocity-Flat-Unitree-G1": unitree_g1_flat_env_cfg,
   "Mjlab-Velocity-Flat-Unitree-Go1": unitree_go1_flat_env_cfg,
+  "Mjlab-Tracking-Flat-Unitree-G1": _tracking_g1,
 }
 
 

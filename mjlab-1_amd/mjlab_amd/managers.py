@@ -575,7 +575,10 @@ class CommandTerm(ManagerTermBase):
     self._update_metrics()
     self.time_left -= dt
     if getattr(self._env, "sync_free", False):
-      self._resample_masked(self.time_left <= 0.0)
+      # a resampling period of >= 1e8 s (the tracking command's 1e9) never elapses: skip
+      # the masked resample instead of recording a no-op into the step graph
+      if self.cfg.resampling_time_range[0] < 1e8:
+        self._resample_masked(self.time_left <= 0.0)
     else:
       ids = (self.time_left <= 0.0).nonzero().flatten()
       if len(ids) > 0:

@@ -90,3 +90,44 @@ def yaw_quat(quat: torch.Tensor) -> torch.Tensor:
   out[..., 0] = torch.cos(yaw / 2)
   out[..., 3] = torch.sin(yaw / 2)
   return out
+
+
+def quat_conjugate(q: torch.Tensor) -> torch.Tensor:
+  return torch.cat((q[..., 0:1], -q[..., 1:]), dim=-1)
+
+
+def quat_inv(q: torch.Tensor, eps: float = 1e-9) -> torch.Tensor:
+  """`math.py:261-271`: conjugate / |q|^2."""
+  return quat_conjugate(q) / q.pow(2).sum(dim=-1, keepdim=True).clamp(min=eps)
+
+
+def quat_unique(q: torch.Tensor) -> torch.Tensor:
+  return torch.where(q[..., 0:1] < 0, -q, q)
+
+
+def axis_angle_from_quat(quat: torch.Tensor, eps: float = 1.0e-6) -> torch.Tensor:
+  """`math.py:478-506`: log map, shortest arc (w >= 0), Taylor branch near zero."""
+  quat = quat * (1.0 - 2.0 * (quat[..., 0:1] < 0.0))
+  mag = torch.linalg.norm(quat[..., 1:], dim=-1)
+  half = torch.atan2(mag, quat[..., 0])
+  angle = 2.0 * half
+  s = torch.where(angle.abs() > eps, torch.sin(half) / angle, 0.5 - angle * angle / 48)
+  return quat[..., 1:4] / s.unsqueeze(-1)
+
+
+def quat_box_minus(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  """`math.py:590-604`: log(q1 * conj(q2))."""
+  return axis_angle_from_quat(quat_mul(q1, quat_conjugate(q2)))
+
+
+def quat_error_magnitude(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  """`math.py:688-699`: |box_minus(q1, q2)| (rotation angle between the two)."""
+  return torch.norm(quat_box_minus(q1, q2), dim=-1)
+
+
+def subtract_frame_transforms(t01, q01, t02=None, q02=None):
+  """`math.py:832-863`: T12 = T01^-1 * T02."""
+  q10 = quat_inv(q01)
+  q12 = quat_mul(q10, q02) if q02 is not None else q10
+  t12 = quat_apply(q10, t02 - t01) if t02 is not None else quat_apply(q10, -t01)
+  return t12, q12

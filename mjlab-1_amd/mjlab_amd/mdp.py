@@ -441,40 +441,114 @@ reset_joints_by_offset.masked = _reset_joints_by_offset_masked
 push_by_setting_velocity.masked = _push_by_setting_velocity_masked
 
 
-def randomize_field(env, env_ids, field: str, ranges, operation: str = "abs",
-                    distribution: str = "uniform", asset_cfg=_ROBOT, axes=None):
-  """Domain randomization of one model field over the entity's elements
-  (`envs/mdp/events.py:264-289,519-706`); the field must have been expanded."""
+# `envs/mdp/events.py:264-289`: entity type, address use and default axes per field.
+FIELD_SPECS = {
+  "dof_armature": ("dof", None, None), "dof_frictionloss": ("dof", None, None),
+  "dof_damping": ("dof", None, None),
+  "jnt_range": ("joint", None, None), "jnt_stiffness": ("joint", None, None),
+  "body_mass": ("body", None, None), "body_ipos": ("body", [0, 1, 2], None),
+  "body_iquat": ("body", [0, 1, 2, 3], None), "body_inertia": ("body", None, None),
+  "body_pos": ("body", [0, 1, 2], None), "body_quat": ("body", [0, 1, 2, 3], None),
+  "geom_friction": ("geom", [0], [0, 1, 2]), "geom_pos": ("geom", [0, 1, 2], None),
+  "geom_quat": ("geom", [0, 1, 2, 3], None), "geom_rgba": ("geom", [0, 1, 2, 3], None),
+  "site_pos": ("site", [0, 1, 2], None), "site_quat": ("site", [0, 1, 2, 3], None),
+  "qpos0": ("qpos", None, None),
+}
+
+
+def _sample_distribution(distribution, lo, hi, shape, device):
+  if distribution == "uniform":
+    return sample_uniform(lo, hi, shape, device)
+  if distribution == "log_uniform":
+    return torch.exp(sample_uniform(math.log(lo), math.log(hi), shape, device))
+  if distribution == "gaussian":
+    return torch.randn(shape, device=device) * hi + lo
+  raise ValueError(f"Unknown distribution: {distribution}")
+
+
+def randomize_field(env, env_ids, field: str, ranges, distribution: str = "uniform",
+                    operation: str = "abs", asset_cfg=None, axes=None):
+  """Unified model-field randomization (`envs/mdp/events.py:292-354`).  `ranges` is
+  (lo, hi) for every target axis or {axis: (lo, hi)}; "add"/"scale" start from the
+  stored default (no accumulation across resets), "abs" keeps non-target axes.  The
+  field must have been expanded (EventManager does that for domain_randomization terms)."""
+  if field not in FIELD_SPECS:
+    raise ValueError(f"Unknown field '{field}'. Supported fields: {list(FIELD_SPECS.keys())}")
+  etype, default_axes, valid_axes = FIELD_SPECS[field]
+  asset_cfg = asset_cfg or _ROBOT
   a = env.scene[asset_cfg.name]
   if env_ids is None:
     env_ids = torch.arange(env.num_envs, device=env.device)
+  env_ids = env_ids.to(env.device, dtype=torch.long)
   t = getattr(env.sim.model, field)
-  if field.startswith("geom_"):
-    ids = a.indexing.geom_ids[asset_cfg.geom_ids]
-  elif field.startswith("body_"):
-    ids = a.indexing.body_ids[asset_cfg.body_ids]
-  elif field.startswith("dof_"):
-    ids = a.indexing.joint_v_adr[asset_cfg.joint_ids]
+  ix = a.indexing
+  ids = {"dof": lambda: ix.joint_v_adr[asset_cfg.joint_ids],
+         "qpos": lambda: ix.joint_q_adr[asset_cfg.joint_ids],
+         "joint": lambda: ix.joint_ids[asset_cfg.joint_ids],
+         "body": lambda: ix.body_ids[asset_cfg.body_ids],
+         "geom": lambda: ix.geom_ids[asset_cfg.geom_ids],
+         "site": lambda: ix.site_ids[asset_cfg.site_ids]}[etype]()
+  field_ndim = t.dim() - 1
+  if axes is not None:
+    target = list(axes)
+  elif isinstance(ranges, dict):
+    target = list(ranges.keys())
+  elif default_axes is not None:
+    target = list(default_axes)
   else:
-    raise NotImplementedError(field)
-  if axes is None:
-    axes = [0] if t.dim() == 3 else None
-  lo, hi = ranges if isinstance(ranges, tuple) else tuple(ranges)
-  shape = (len(env_ids), len(ids)) + ((len(axes),) if axes is not None else ())
-  if distribution == "uniform":
-    vals = sample_uniform(lo, hi, shape, env.device)
+    target = list(range(t.shape[-1])) if field_ndim > 1 else [0]
+  if valid_axes is not None and set(target) - set(valid_axes):
+    raise ValueError(f"Invalid axes {set(target) - set(valid_axes)} for field. Valid axes: {valid_axes}")
+  if isinstance(ranges, dict):
+    missing = set(target) - set(ranges.keys())
+    if missing:
+      raise ValueError(f"Missing ranges for axes {missing} in field '{field}'. Required axes: {target}")
+    axis_ranges = {ax: ranges[ax] for ax in target}
+  elif isinstance(ranges, (tuple, list)):
+    axis_ranges = {ax: tuple(ranges) for ax in target}
   else:
-    vals = torch.exp(sample_uniform(math.log(lo), math.log(hi), shape, env.device))
-  e = env_ids[:, None]
-  if axes is None:
-    base = env.sim.get_default_field(field)[ids]
-    cur = vals if operation == "abs" else (base * vals if operation == "scale" else base + vals)
-    t[e, ids] = cur
+    raise TypeError(f"ranges must be tuple or dict, got {type(ranges)}")
+  eg, ig = torch.meshgrid(env_ids, ids, indexing="ij")
+  cur = t[eg, ig]
+  if operation in ("scale", "add"):
+    base = env.sim.get_default_field(field)[ids].unsqueeze(0).expand_as(cur)
   else:
-    ax = torch.tensor(axes, device=env.device)
-    base = env.sim.get_default_field(field)[ids][:, ax]
-    cur = vals if operation == "abs" else (base * vals if operation == "scale" else base + vals)
-    t[e[..., None], ids[None, :, None], ax[None, None, :]] = cur
+    base = cur
+  if operation == "scale":
+    rnd = torch.ones_like(base)
+  elif operation == "add":
+    rnd = torch.zeros_like(base)
+  elif operation == "abs":
+    rnd = base.clone()
+  else:
+    raise ValueError(f"Unknown operation: {operation}")
+  for ax in target:
+    lo, hi = axis_ranges[ax]
+    if cur.dim() > 2:
+      rnd[..., ax] = _sample_distribution(distribution, lo, hi, cur.shape[:-1], env.device)
+    else:
+      rnd = _sample_distribution(distribution, lo, hi, cur.shape, env.device)
+  if operation == "add":
+    t[eg, ig] = base + rnd
+  elif operation == "scale":
+    t[eg, ig] = base * rnd
+  else:
+    t[eg, ig] = rnd
+
+
+def randomize_encoder_bias(env, env_ids, bias_range, asset_cfg=_ROBOT):
+  """`envs/mdp/events.py:709-745`: per-env joint encoder offsets (read by
+  joint_pos_rel(biased=True) and subtracted by the joint-position action)."""
+  a = env.scene[asset_cfg.name]
+  if env_ids is None:
+    env_ids = torch.arange(env.num_envs, device=env.device)
+  jid = asset_cfg.joint_ids
+  nj = a.num_joints if isinstance(jid, slice) else len(jid)
+  b = sample_uniform(bias_range[0], bias_range[1], (len(env_ids), nj), env.device)
+  if isinstance(jid, slice):
+    a.data.encoder_bias[env_ids] = b
+  else:
+    a.data.encoder_bias[env_ids[:, None], torch.as_tensor(jid, device=env.device)] = b
 
 
 # =========================================================================== commands

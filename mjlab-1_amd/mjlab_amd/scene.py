@@ -42,6 +42,7 @@ class EntityIndexing:
   free_joint_q_adr: torch.Tensor
   free_joint_v_adr: torch.Tensor
   site_body_ids: torch.Tensor
+  joint_ids: torch.Tensor | None = None
 
 
 class EntityData:
@@ -347,7 +348,8 @@ class Entity:
       joint_q_adr=t([m.jnt_qposadr[j] for j in self._jnt_gid]),
       joint_v_adr=t([m.jnt_dofadr[j] for j in self._jnt_gid]),
       free_joint_q_adr=t(fq), free_joint_v_adr=t(fv),
-      site_body_ids=t([m.site_bodyid[s] for s in self._site_gid]))
+      site_body_ids=t([m.site_bodyid[s] for s in self._site_gid]),
+      joint_ids=t(self._jnt_gid))
     key = np.asarray(m.key_qpos)
     root_state = np.zeros(13)
     if fq:

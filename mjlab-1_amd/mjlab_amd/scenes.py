@@ -72,8 +72,16 @@ def build_go1_velocity(xml_path: str) -> Model:
   return compile_scene([ent], contact_sensors=sensors, **VELOCITY_SIM)
 
 
+def build_g1_tracking(xml_path: str) -> Model:
+  """`tasks/tracking/config/g1/env_cfgs.py:22-33`: G1 (knees-bent init) on a plane with
+  the self-collision sensor only; sim options of `tracking_env_cfg.py:303-316`."""
+  sensors = [s for s in _g1_contact_sensors() if s.name == "self_collision"]
+  return compile_scene([_g1_entity(xml_path)], contact_sensors=sensors, **VELOCITY_SIM)
+
+
 SCENE_BUILDERS = {
   "g1_velocity": ("unitree_g1/xmls/g1.xml", build_g1_velocity),
+  "g1_tracking": ("unitree_g1/xmls/g1.xml", build_g1_tracking),
   "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
 }
 
