@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MJX_ABI_VERSION 1
+#define MJX_ABI_VERSION 2
 
 /* geom types (MuJoCo mjtGeom numbering) */
 enum { MJX_GEOM_PLANE = 0, MJX_GEOM_HFIELD = 1, MJX_GEOM_SPHERE = 2, MJX_GEOM_CAPSULE = 3,
@@ -48,7 +48,7 @@ enum { MJX_OBJ_NONE = 0, MJX_OBJ_BODY = 1, MJX_OBJ_XBODY = 2, MJX_OBJ_JOINT = 3,
 enum { MJX_REDUCE_NONE = 0, MJX_REDUCE_MINDIST = 1, MJX_REDUCE_MAXFORCE = 2,
        MJX_REDUCE_NETFORCE = 3 };
 enum { MJX_INT_EULER = 0, MJX_INT_IMPLICITFAST = 1 };
-#define MJX_MASK_WORDS 4 /* contact-sensor geom masks: 128 geoms */
+#define MJX_MASK_WORDS 16 /* contact-sensor geom masks: 512 geoms */
 
 /* Host-side compiled model (fp64 / int32).  Field names follow mjModel.  Array
  * widths per element are in the trailing comment.  Filled by the Python scene

@@ -67,6 +67,9 @@ struct mjxModel_ {
   std::map<std::string, std::vector<float>> host_float;
   std::map<std::string, std::pair<int64_t, int64_t>> float_dims;  // count, width
   std::map<std::string, std::pair<int64_t, int64_t>> int_dims;
+  // static world frames of heightfield geoms (terrain bodies are welded to the world)
+  std::vector<int> hf_static_geoms;
+  std::vector<float> hf_static_xpos, hf_static_xmat;
 };
 
 struct mjxSim_ {
@@ -190,6 +193,87 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     if (upload(anc.data(), sizeof(uint64_t) * anc.size(), &p)) { delete m; return -1; }
     m->dm.dof_ancmask = (const uint64_t*)p;
   }
+  {
+    // Heightfield broadphase tables.  The pair list is [regular pairs | hfield pairs], the
+    // hfield pairs grouped by hfield geom (the scene compiler emits them that way).
+    const int ng = desc->ngeom, np = desc->npair;
+    std::vector<int> geom_lds(ng > 0 ? ng : 1, -1), lds_geom;
+    for (int g = 0; g < ng; g++)
+      if (desc->geom_type[g] != 1) { geom_lds[g] = (int)lds_geom.size(); lds_geom.push_back(g); }
+    if (lds_geom.empty()) lds_geom.push_back(0);
+    d.ngeom_lds = 0;
+    for (int g = 0; g < ng; g++) d.ngeom_lds += desc->geom_type[g] != 1;
+    int nreg = 0;
+    while (nreg < np && desc->geom_type[desc->pair_geom1[nreg]] != 1 &&
+           desc->geom_type[desc->pair_geom2[nreg]] != 1) nreg++;
+    std::vector<int> hf_geom, hf_adr, partner;
+    std::vector<char> seen(ng > 0 ? ng : 1, 0);
+    for (int q = nreg; q < np; q++) {
+      const int g1 = desc->pair_geom1[q], g2 = desc->pair_geom2[q];
+      if (desc->geom_type[g1] != 1 || desc->geom_type[g2] == 1) {
+        delete m;
+        return fail("pair list: heightfield pairs (hfield first) must follow all regular pairs");
+      }
+      if (hf_geom.empty() || hf_geom.back() != g1) {
+        for (int h : hf_geom)
+          if (h == g1) { delete m; return fail("pair list: hfield pair blocks must be contiguous"); }
+        hf_geom.push_back(g1);
+        hf_adr.push_back(q);
+      }
+      if (!seen[g2]) { seen[g2] = 1; partner.push_back(g2); }
+    }
+    hf_adr.push_back(np);
+    d.npair = nreg;
+    d.npair_all = np;
+    d.nhfgeom = (int)hf_geom.size();
+    d.nhfpartner = (int)partner.size();
+    // static frames of every hfield geom (for D.geom_xpos / geom_xmat; kernels recompute)
+    for (int g = 0; g < ng; g++) {
+      if (desc->geom_type[g] != 1) continue;
+      int b = desc->geom_bodyid[g];
+      if (desc->body_weldid[b] != 0) {
+        delete m;
+        return fail("heightfield geoms must sit on bodies welded to the world");
+      }
+      // chain of static bodies up to the world: x = x_parent + R_parent p, q = q_parent q
+      double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, x[3] = {0, 0, 0};
+      std::vector<int> chain;
+      for (int c = b; c > 0; c = desc->body_parentid[c]) chain.push_back(c);
+      auto qm = [](const double* q, double* M) {
+        const double w = q[0], a = q[1], bq = q[2], c = q[3];
+        M[0] = 1 - 2 * (bq * bq + c * c); M[1] = 2 * (a * bq - w * c); M[2] = 2 * (a * c + w * bq);
+        M[3] = 2 * (a * bq + w * c); M[4] = 1 - 2 * (a * a + c * c); M[5] = 2 * (bq * c - w * a);
+        M[6] = 2 * (a * c - w * bq); M[7] = 2 * (bq * c + w * a); M[8] = 1 - 2 * (a * a + bq * bq);
+      };
+      auto step = [&](const double* pos, const double* quat) {
+        double Q[9], nx[3], nR[9];
+        qm(quat, Q);
+        for (int i = 0; i < 3; i++) nx[i] = x[i] + R[3 * i] * pos[0] + R[3 * i + 1] * pos[1] + R[3 * i + 2] * pos[2];
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++)
+            nR[3 * i + j] = R[3 * i] * Q[j] + R[3 * i + 1] * Q[3 + j] + R[3 * i + 2] * Q[6 + j];
+        for (int i = 0; i < 3; i++) x[i] = nx[i];
+        for (int i = 0; i < 9; i++) R[i] = nR[i];
+      };
+      for (auto it = chain.rbegin(); it != chain.rend(); ++it)
+        step(desc->body_pos + 3 * *it, desc->body_quat + 4 * *it);
+      step(desc->geom_pos + 3 * g, desc->geom_quat + 4 * g);
+      m->hf_static_geoms.push_back(g);
+      for (int i = 0; i < 3; i++) m->hf_static_xpos.push_back((float)x[i]);
+      for (int i = 0; i < 9; i++) m->hf_static_xmat.push_back((float)R[i]);
+    }
+    if (hf_geom.empty()) { hf_geom.push_back(0); partner.push_back(0); }
+    if (upload(geom_lds.data(), sizeof(int) * geom_lds.size(), &p)) { delete m; return -1; }
+    m->dm.geom_lds = (const int32_t*)p;
+    if (upload(lds_geom.data(), sizeof(int) * lds_geom.size(), &p)) { delete m; return -1; }
+    m->dm.lds_geom = (const int32_t*)p;
+    if (upload(hf_geom.data(), sizeof(int) * hf_geom.size(), &p)) { delete m; return -1; }
+    m->dm.hf_geom = (const int32_t*)p;
+    if (upload(hf_adr.data(), sizeof(int) * hf_adr.size(), &p)) { delete m; return -1; }
+    m->dm.hf_pairadr = (const int32_t*)p;
+    if (upload(partner.data(), sizeof(int) * partner.size(), &p)) { delete m; return -1; }
+    m->dm.hf_partner = (const int32_t*)p;
+  }
   if (upload(desc->sensor_geommask1, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask1 = (const uint32_t*)p;
   if (upload(desc->sensor_geommask2, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
@@ -285,6 +369,21 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   if (sync_params(s, nullptr)) { delete s; return -1; }
   e = mjx::prepare_step(host_params(s));
   if (e != hipSuccess) { delete s; return fail(std::string("prepare: ") + hipGetErrorString(e)); }
+  // heightfield geom frames are static: write them once for every world
+  for (size_t k = 0; k < model->hf_static_geoms.size(); k++) {
+    const int g = model->hf_static_geoms[k];
+    std::vector<float> px((size_t)nworld * 3), pm((size_t)nworld * 9);
+    for (int w = 0; w < nworld; w++) {
+      for (int i = 0; i < 3; i++) px[(size_t)w * 3 + i] = model->hf_static_xpos[3 * k + i];
+      for (int i = 0; i < 9; i++) pm[(size_t)w * 9 + i] = model->hf_static_xmat[9 * k + i];
+    }
+    e = hipMemcpy2D(s->dd.geom_xpos + 3 * g, sizeof(float) * 3 * d.ngeom, px.data(),
+                    sizeof(float) * 3, sizeof(float) * 3, nworld, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy2D(s->dd.geom_xmat + 9 * g, sizeof(float) * 9 * d.ngeom, pm.data(),
+                      sizeof(float) * 9, sizeof(float) * 9, nworld, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { delete s; return fail(std::string("hfield frames: ") + hipGetErrorString(e)); }
+  }
   // initial state: mj_resetData
   if (mjx::launch_reset(d, s->dm, s->dd, nullptr, nworld, nullptr) != hipSuccess) {
     delete s;

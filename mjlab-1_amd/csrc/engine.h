@@ -11,7 +11,7 @@
 namespace mjx {
 
 constexpr int kWave = 64;        // CDNA wavefront width
-constexpr int kMaskWords = 4;    // contact-sensor geom masks (128 geoms)
+constexpr int kMaskWords = 16;   // contact-sensor geom masks (512 geoms)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
@@ -19,6 +19,10 @@ constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (reg
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
   int nhfield, nhfielddata, nlevel, nchild, nmocap;
+  int ngeom_lds;  // geoms whose world frames phase A keeps in LDS (all but heightfields)
+  int npair_all;  // pair list length: [0, npair) regular pairs, [npair, npair_all) hfield pairs
+  int nhfgeom;    // heightfield geoms with candidate pairs (blocks of the hfield pair tail)
+  int nhfpartner; // distinct geoms paired with a heightfield (their union AABB culls hfields)
   int nconmax;  // contacts per world held in LDS
   int njmax;    // constraint rows per world held in LDS
 };
@@ -39,6 +43,15 @@ struct DModel {
 #undef X_FLT
   const uint64_t* dof_bodymask;
   const uint64_t* dof_ancmask;  // bit j set: dof j is dof i itself or an ancestor (host-derived)
+  // host-derived heightfield broadphase tables (capi.cpp): LDS frame slot per geom (-1 for
+  // hfields, whose static frames are computed on the fly), its inverse, hfield geoms with
+  // pairs, their pair blocks [hf_pairadr[i], hf_pairadr[i+1]) in the pair tail, and the
+  // distinct partner geoms
+  const int32_t* geom_lds;
+  const int32_t* lds_geom;
+  const int32_t* hf_geom;
+  const int32_t* hf_pairadr;
+  const int32_t* hf_partner;
   const uint32_t* sensor_geommask1;
   const uint32_t* sensor_geommask2;
 };

@@ -62,7 +62,7 @@ Lds make_lds(const Dims& d, int ph) {
     {&Lds::cinert, 10 * nb, A}, {&Lds::crb, 10 * nb, A}, {&Lds::cvel, 6 * nb, A | Cp},
     {&Lds::cacc, 6 * nb, A | Cp}, {&Lds::stlin, 3 * nb, A}, {&Lds::stang, 3 * nb, A},
     {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
-    {&Lds::gxpos, 3 * d.ngeom, A}, {&Lds::gxmat, 9 * d.ngeom, A},
+    {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
     {&Lds::M, nv * nv, A | B | Cp}, {&Lds::H, nv * nv, A | B | Cp},
     {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
@@ -129,8 +129,8 @@ Lds make_lds(const Dims& d, int ph) {
     // smooth solve) is dead before collision: M and H share the contact/row block too.
     if (g1.second >= nv * nv) L.M = L.H = g1.first;
     auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc, &Lds::xanchor, &Lds::xaxis});
-    const int gp = (3 * d.ngeom + 3) & ~3;
-    if (g2.second >= gp + 9 * d.ngeom) {
+    const int gp = (3 * d.ngeom_lds + 3) & ~3;
+    if (g2.second >= gp + 9 * d.ngeom_lds) {
       L.gxpos = g2.first;
       L.gxmat = g2.first + gp;
     }
@@ -237,6 +237,23 @@ __device__ __forceinline__ float wave_sum(float v) {
          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)) +
          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+}
+// min / max over the wave (same DPP pattern as wave_sum; all lanes must be active)
+__device__ __forceinline__ float wave_min(float v) {
+  v = fminf(v, dpp<0xB1>(v));
+  v = fminf(v, dpp<0x4E>(v));
+  v = fminf(v, dpp<0x141>(v));
+  v = fminf(v, dpp<0x140>(v));
+  const auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return fminf(fminf(rl(0), rl(16)), fminf(rl(32), rl(48)));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  const auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return fmaxf(fmaxf(rl(0), rl(16)), fmaxf(rl(32), rl(48)));
 }
 __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
   int x = v;
@@ -648,6 +665,92 @@ __device__ __forceinline__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* 
   }
   *pa = a0 + u * s;
   *pb = b0 + v * t;
+}
+
+
+// Heightfield frame (static body) and the sphere-vs-hfield narrowphase.  The surface is the
+// piecewise-linear interpolation of the elevation grid, two triangles per cell (p00 p10
+// p11 / p00 p11 p01); the contact is the deepest closest-point over the triangles of the
+// cells under the sphere footprint (oracle/oracle.c col_hfield_sphere, same arithmetic in
+// fp32).  Row r spans y, column c spans x, as MuJoCo lays out hfield data.
+struct HFrame { V3 p; float R[9]; };
+__device__ __forceinline__ HFrame hfield_frame(const DModel& m, const float* S, const Lds& L,
+                                               const float* gpos, const float* gquat, int g) {
+  HFrame f;
+  const int b = m.geom_bodyid[g];
+  const float* Rb = S + L.xmat + 9 * b;
+  f.p = v3(S + L.xpos + 3 * b) + mulv(Rb, v3(gpos + 3 * g));
+  float Rg[9];
+  qmat(Rg, q4(gquat + 4 * g));
+  mat3mul(f.R, Rb, Rg);
+  return f;
+}
+__device__ __forceinline__ int hfield_sphere(const ConOut& co, int key, int g1, int g2,
+                                             const HFrame& F, const float* hdata,
+                                             const float* hsize, int nr, int nc, V3 center,
+                                             float r, float margin, int* trunc) {
+  const V3 loc = mulTv(F.R, center - F.p);
+  const float sx = hsize[0], sy = hsize[1], sz = hsize[2];
+  const float dx = 2 * sx / (nc - 1), dy = 2 * sy / (nr - 1);
+  int c0 = (int)floorf((loc.x - r + sx) / dx), c1 = (int)floorf((loc.x + r + sx) / dx);
+  int r0 = (int)floorf((loc.y - r + sy) / dy), r1 = (int)floorf((loc.y + r + sy) / dy);
+  if (c1 < 0 || r1 < 0 || c0 > nc - 2 || r0 > nr - 2) return 0;
+  c0 = max(c0, 0); r0 = max(r0, 0);
+  c1 = min(c1, nc - 2); r1 = min(r1, nr - 2);
+  if ((c1 - c0 + 1) * (r1 - r0 + 1) > 64) { *trunc = 1; return 0; }  // footprint cap
+  float best = 1e30f;
+  V3 bestn = {0, 0, 1};
+  bool found = false;
+  for (int rr = r0; rr <= r1; rr++)
+    for (int cc = c0; cc <= c1; cc++) {
+      const float x0 = -sx + cc * dx, y0 = -sy + rr * dy;
+      const float* row0 = hdata + rr * nc + cc;
+      const V3 p00 = {x0, y0, row0[0] * sz}, p10 = {x0 + dx, y0, row0[1] * sz};
+      const V3 p01 = {x0, y0 + dy, row0[nc] * sz}, p11 = {x0 + dx, y0 + dy, row0[nc + 1] * sz};
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const V3 a = p00, b = k ? p11 : p10, c = k ? p01 : p11;
+        const V3 e1 = b - a, e2 = c - a;
+        V3 n = cross(e1, e2);
+        n = n * (1.0f / fmaxf(norm(n), MINVAL));
+        const float sd = dot(loc - a, n);
+        const V3 pp = loc - n * sd;
+        const V3 v2 = pp - a;
+        const float d00 = dot(e2, e2), d01 = dot(e2, e1), d11 = dot(e1, e1);
+        const float d20 = dot(v2, e2), d21 = dot(v2, e1);
+        const float den = d00 * d11 - d01 * d01;
+        const float u = (d11 * d20 - d01 * d21) / den, vv = (d00 * d21 - d01 * d20) / den;
+        V3 q;
+        if (u >= 0 && vv >= 0 && u + vv <= 1) {
+          q = pp;
+        } else {
+          float bd = 1e30f;
+          q = a;
+#pragma unroll
+          for (int e = 0; e < 3; e++) {
+            const V3 s0 = e == 0 ? a : (e == 1 ? b : c), s1 = e == 0 ? b : (e == 1 ? c : a);
+            const V3 ab = s1 - s0;
+            const float tt = clamp01(dot(loc - s0, ab) / fmaxf(dot(ab, ab), MINVAL));
+            const V3 cp = s0 + ab * tt;
+            const V3 df = loc - cp;
+            const float dd = dot(df, df);
+            if (dd < bd) { bd = dd; q = cp; }
+          }
+        }
+        const V3 diff = loc - q;
+        float dist = norm(diff);
+        V3 nn;
+        if (dist < MINVAL || sd < 0) { nn = n; dist = sd; }
+        else { nn = diff * (1.0f / dist); }
+        dist -= r;
+        if (dist < best) { best = dist; bestn = nn; found = true; }
+      }
+    }
+  if (!found || best > margin) return 0;
+  const V3 nw = mulv(F.R, bestn);
+  const V3 pw = mulv(F.R, loc - bestn * (r + 0.5f * best)) + F.p;
+  append(co, key, g1, g2, best, pw, nw);
+  return 1;
 }
 
 // --------------------------------------------------------------------------- impedance
@@ -1334,13 +1437,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     {
       const float* gpos = MF(geom_pos);
       const float* gquat = MF(geom_quat);
-      for (int g = lane; g < d.ngeom; g += kWave) {
+      for (int sl = lane; sl < d.ngeom_lds; sl += kWave) {
+        const int g = m.lds_geom[sl];
         int b = m.geom_bodyid[g];
         const float* R = S + L.xmat + 9 * b;
-        st3(S + L.gxpos + 3 * g, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
+        st3(S + L.gxpos + 3 * sl, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
         float Rg[9];
         qmat(Rg, q4(gquat + 4 * g));
-        mat3mul(S + L.gxmat + 9 * g, R, Rg);
+        mat3mul(S + L.gxmat + 9 * sl, R, Rg);
       }
     }
     sync();
@@ -1353,8 +1457,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int p = lane; p < d.npair; p += kWave) {
         int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
         int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        const int l1 = m.geom_lds[g1], l2 = m.geom_lds[g2];  // LDS frame slots
         float margin = fmaxf(gmargin[g1], gmargin[g2]);
-        V3 p1 = v3(S + L.gxpos + 3 * g1), p2 = v3(S + L.gxpos + 3 * g2);
+        V3 p1 = v3(S + L.gxpos + 3 * l1), p2 = v3(S + L.gxpos + 3 * l2);
         float r1 = grb[g1], r2 = grb[g2];
         if (r1 > 0 && r2 > 0 && t1 != GEOM_HFIELD) {
           if (norm(p2 - p1) > r1 + r2 + margin) continue;
@@ -1363,19 +1468,19 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         const float* s2 = gsize + 3 * g2;
         int key = p * 8;
         if (t1 == GEOM_PLANE) {
-          const float* Rp = S + L.gxmat + 9 * g1;
+          const float* Rp = S + L.gxmat + 9 * l1;
           V3 n = {Rp[2], Rp[5], Rp[8]};
           if (t2 == GEOM_SPHERE) {
             plane_sphere(co, key, g1, g2, p1, n, p2, s2[0], margin);
           } else if (t2 == GEOM_CAPSULE) {
-            const float* R2 = S + L.gxmat + 9 * g2;
+            const float* R2 = S + L.gxmat + 9 * l2;
             V3 ax = {R2[2], R2[5], R2[8]};
             int k = key;
             k += plane_sphere(co, k, g1, g2, p1, n, p2 + ax * s2[1], s2[0], margin);
             plane_sphere(co, k, g1, g2, p1, n, p2 - ax * s2[1], s2[0], margin);
           } else if (t2 == GEOM_BOX) {
             float dist = dot(p2 - p1, n);
-            const float* R2 = S + L.gxmat + 9 * g2;
+            const float* R2 = S + L.gxmat + 9 * l2;
             int cnt = 0;
             for (int i = 0; i < 8 && cnt < 4; i++) {
               V3 v = {(i & 1) ? s2[0] : -s2[0], (i & 2) ? s2[1] : -s2[1], (i & 4) ? s2[2] : -s2[2]};
@@ -1391,14 +1496,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
           sphere_sphere(co, key, g1, g2, p1, s1[0], p2, s2[0], margin);
         } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
-          const float* R2 = S + L.gxmat + 9 * g2;
+          const float* R2 = S + L.gxmat + 9 * l2;
           V3 ax = {R2[2], R2[5], R2[8]};
           V3 pa, pb;
           seg_seg(p1, p1, p2 + ax * s2[1], p2 - ax * s2[1], &pa, &pb);
           sphere_sphere(co, key, g1, g2, p1, s1[0], pb, s2[0], margin);
         } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
-          const float* R1 = S + L.gxmat + 9 * g1;
-          const float* R2 = S + L.gxmat + 9 * g2;
+          const float* R1 = S + L.gxmat + 9 * l1;
+          const float* R2 = S + L.gxmat + 9 * l2;
           V3 a1 = {R1[2], R1[5], R1[8]}, a2 = {R2[2], R2[5], R2[8]};
           V3 pa, pb;
           seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
@@ -1406,6 +1511,75 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         } else {
           atomicOr(&ints[3], 4);
         }
+      }
+      // heightfield pairs: the union AABB of the hfield partners (bounding spheres) culls
+      // the hfield geoms (lane per hfield), then lanes take the pairs of each overlapping
+      // hfield block.  A terrain of many sub-terrain hfields costs ~1 block per world.
+      if (d.nhfgeom > 0) {
+        float lo0 = 1e30f, lo1 = 1e30f, lo2 = 1e30f, hi0 = -1e30f, hi1 = -1e30f, hi2 = -1e30f;
+        for (int i = lane; i < d.nhfpartner; i += kWave) {
+          const int g = m.hf_partner[i];
+          const V3 c = v3(S + L.gxpos + 3 * m.geom_lds[g]);
+          const float r = grb[g] + gmargin[g];
+          lo0 = fminf(lo0, c.x - r); lo1 = fminf(lo1, c.y - r); lo2 = fminf(lo2, c.z - r);
+          hi0 = fmaxf(hi0, c.x + r); hi1 = fmaxf(hi1, c.y + r); hi2 = fmaxf(hi2, c.z + r);
+        }
+        lo0 = wave_min(lo0); lo1 = wave_min(lo1); lo2 = wave_min(lo2);
+        hi0 = wave_max(hi0); hi1 = wave_max(hi1); hi2 = wave_max(hi2);
+        const float* gpos = MF(geom_pos);
+        const float* gquat = MF(geom_quat);
+        const float* hsz_all = MF(hfield_size);
+        const float* hdat_all = MF(hfield_data);
+        int trunc = 0;
+        for (int base = 0; base < d.nhfgeom; base += kWave) {
+          bool act = false;
+          const int i = base + lane;
+          if (i < d.nhfgeom) {
+            const int g = m.hf_geom[i];
+            const HFrame F = hfield_frame(m, S, L, gpos, gquat, g);
+            const float* hs = hsz_all + 4 * m.geom_dataid[g];
+            // local box [-sx, sx] x [-sy, sy] x [-base, z_max] -> world AABB
+            const float ex = hs[0], ey = hs[1], ez = 0.5f * (hs[2] + hs[3]);
+            const V3 cw = F.p + mulv(F.R, V3{0, 0, 0.5f * (hs[2] - hs[3])});
+            const float wx = fabsf(F.R[0]) * ex + fabsf(F.R[1]) * ey + fabsf(F.R[2]) * ez;
+            const float wy = fabsf(F.R[3]) * ex + fabsf(F.R[4]) * ey + fabsf(F.R[5]) * ez;
+            const float wz = fabsf(F.R[6]) * ex + fabsf(F.R[7]) * ey + fabsf(F.R[8]) * ez;
+            act = cw.x - wx <= hi0 && cw.x + wx >= lo0 && cw.y - wy <= hi1 &&
+                  cw.y + wy >= lo1 && cw.z - wz <= hi2 && cw.z + wz >= lo2;
+          }
+          unsigned long long bal = __ballot(act);
+          while (bal) {
+            const int j = base + __ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+            const int hg = m.hf_geom[j];
+            const HFrame F = hfield_frame(m, S, L, gpos, gquat, hg);
+            const int hid = m.geom_dataid[hg];
+            const float* hs = hsz_all + 4 * hid;
+            const float* hd = hdat_all + m.hfield_adr[hid];
+            const int nr = m.hfield_nrow[hid], nc = m.hfield_ncol[hid];
+            for (int p = m.hf_pairadr[j] + lane; p < m.hf_pairadr[j + 1]; p += kWave) {
+              const int g2 = m.pair_geom2[p];
+              const int t2 = m.geom_type[g2];
+              const int l2 = m.geom_lds[g2];
+              const V3 p2 = v3(S + L.gxpos + 3 * l2);
+              const float* s2 = gsize + 3 * g2;
+              const float margin = fmaxf(gmargin[hg], gmargin[g2]);
+              const int key = p * 8;
+              if (t2 == GEOM_SPHERE) {
+                hfield_sphere(co, key, hg, g2, F, hd, hs, nr, nc, p2, s2[0], margin, &trunc);
+              } else if (t2 == GEOM_CAPSULE) {
+                const float* R2 = S + L.gxmat + 9 * l2;
+                const V3 ax = {R2[2], R2[5], R2[8]};
+                int k = key;
+                k += hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 + ax * s2[1], s2[0], margin, &trunc);
+                hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 - ax * s2[1], s2[0], margin, &trunc);
+              } else {
+                atomicOr(&ints[3], 4);
+              }
+            }
+          }
+        }
+        if (trunc) atomicOr(&ints[3], 4);
       }
     }
     sync();
@@ -1779,9 +1953,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.ximat[wb * 9 + i] = S[L.ximat + i];
       }
       for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
-      size_t wg = (size_t)w * d.ngeom;
-      for (int i = lane; i < 3 * d.ngeom; i += kWave) D.geom_xpos[wg * 3 + i] = S[L.gxpos + i];
-      for (int i = lane; i < 9 * d.ngeom; i += kWave) D.geom_xmat[wg * 9 + i] = S[L.gxmat + i];
+      size_t wg = (size_t)w * d.ngeom;  // heightfield frames are static (set at sim creation)
+      for (int i = lane; i < 3 * d.ngeom_lds; i += kWave)
+        D.geom_xpos[(wg + m.lds_geom[i / 3]) * 3 + i % 3] = S[L.gxpos + i];
+      for (int i = lane; i < 9 * d.ngeom_lds; i += kWave)
+        D.geom_xmat[(wg + m.lds_geom[i / 9]) * 9 + i % 9] = S[L.gxmat + i];
       size_t ws = (size_t)w * d.nsite;
       for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
       for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];

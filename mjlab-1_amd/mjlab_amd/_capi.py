@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _I = ctypes.POINTER(ctypes.c_int32)
 _D = ctypes.POINTER(ctypes.c_double)
 _U64 = ctypes.POINTER(ctypes.c_uint64)

@@ -65,7 +65,8 @@ def lib() -> ctypes.CDLL:
       continue  # bound by mjlab_amd.fused
     if name not in ("mjx_last_error", "mjx_field_name", "mjx_model_desc_size"):
       getattr(L, name).restype = ci
-  if L.mjx_abi_version() != 1:
+  from ._capi import ABI_VERSION
+  if L.mjx_abi_version() != ABI_VERSION:
     raise MjxError("libmjx355 ABI version mismatch")
   if L.mjx_model_desc_size() != ctypes.sizeof(ModelDesc):
     raise MjxError("mjxModelDesc layout mismatch between include/mjx355.h and _capi.py")

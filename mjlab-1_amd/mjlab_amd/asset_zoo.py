@@ -79,6 +79,21 @@ G1_HOME = dict(
   },
 )
 
+# `tasks/jump/config/g1/env_cfgs.py:19-46` (first-match pattern resolution, so the
+# ".*_shoulder_roll_joint" entry wins over the later left/right ones, as resolve_expr does)
+G1_JUMP_CROUCH = dict(
+  pos=(0.0, 0.0, 0.55),
+  joint_pos={
+    ".*_hip_pitch_joint": -0.6, ".*_knee_joint": 1.2, ".*_ankle_pitch_joint": -0.6,
+    ".*_hip_roll_joint": 0.0, ".*_hip_yaw_joint": 0.0, ".*_ankle_roll_joint": 0.0,
+    "waist_yaw_joint": 0.0, "waist_roll_joint": 0.0, "waist_pitch_joint": 0.15,
+    ".*_shoulder_pitch_joint": -0.5, ".*_shoulder_roll_joint": 0.0,
+    "left_shoulder_roll_joint": 0.3, "right_shoulder_roll_joint": -0.3,
+    ".*_shoulder_yaw_joint": 0.0, ".*_elbow_joint": 0.8, ".*_wrist_pitch_joint": 0.0,
+    ".*_wrist_roll_joint": 0.0, ".*_wrist_yaw_joint": 0.0,
+  },
+)
+
 GO1_ROTOR_INERTIA = 0.000111842
 GO1_HIP_ARMATURE = GO1_ROTOR_INERTIA * 6 ** 2
 GO1_KNEE_ARMATURE = GO1_ROTOR_INERTIA * 9 ** 2

@@ -43,7 +43,7 @@ CONTACT_FIELD_DIM = {"found": 1, "force": 3, "torque": 3, "dist": 1, "pos": 3, "
 CONTACT_FIELD_BIT = {"found": 0, "force": 1, "torque": 2, "dist": 3, "pos": 4, "normal": 5,
                      "tangent": 6}
 CONTACT_REDUCE = {"none": 0, "mindist": 1, "maxforce": 2, "netforce": 3}
-MASK_WORDS = 4  # contact-sensor geom masks: up to 128 geoms
+MASK_WORDS = 16  # contact-sensor geom masks: up to 512 geoms
 
 MINVAL = 1e-15
 
@@ -544,6 +544,10 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
         continue
       a, b = (i, j) if ti <= tj else (j, i)
       pairs.append((a, b))
+  # heightfield pairs last, grouped by hfield geom (the engine's hfield broadphase walks
+  # them as per-hfield blocks; capi.cpp checks the layout)
+  hf = GEOM_TYPES["hfield"]
+  pairs.sort(key=lambda pr: (geoms[pr[0]]["type"] == hf, pr[0] if geoms[pr[0]]["type"] == hf else 0))
   m.npair = len(pairs)
   A["pair_geom1"] = np.array([p[0] for p in pairs], np.int32)
   A["pair_geom2"] = np.array([p[1] for p in pairs], np.int32)
@@ -559,8 +563,9 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     adr.append(acc)
     acc += h.data.size
   A["hfield_adr"] = np.array(adr, np.int32)
-  A["hfield_data"] = (np.concatenate([h.data.reshape(-1) for h in hfields])
-                      if hfields else np.zeros(0))
+  # float32 like the reference's hfield userdata (heightfield_terrains.py:220)
+  A["hfield_data"] = (np.concatenate([np.asarray(h.data, np.float32).reshape(-1) for h in hfields])
+                      if hfields else np.zeros(0, np.float32))
   m.nhfielddata = acc
 
   # sensors

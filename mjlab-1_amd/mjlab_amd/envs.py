@@ -489,10 +489,23 @@ def _tracking_g1(play: bool = False):
   return unitree_g1_flat_tracking_env_cfg(play=play)
 
 
+def _jump_g1(play: bool = False):
+  from .jump import unitree_g1_jump_env_cfg
+  return unitree_g1_jump_env_cfg(play=play)
+
+
+def _jump_g1_hfield(play: bool = False):
+  """Config 5: the jump cfg on the seeded heightfield terrain grid."""
+  from .jump import unitree_g1_jump_env_cfg
+  return unitree_g1_jump_env_cfg(play=play, scene_name="g1_jump_hfield")
+
+
 TASKS = {
   "Mjlab-Velocity-Flat-Unitree-G1": unitree_g1_flat_env_cfg,
   "Mjlab-Velocity-Flat-Unitree-Go1": unitree_go1_flat_env_cfg,
   "Mjlab-Tracking-Flat-Unitree-G1": _tracking_g1,
+  "Mjlab-Jump-Flat-Unitree-G1": _jump_g1,
+  "Mjlab-Jump-Hfield-Unitree-G1": _jump_g1_hfield,
 }
 
 

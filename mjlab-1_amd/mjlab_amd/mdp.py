@@ -224,6 +224,26 @@ def joint_pos_limits(env, asset_cfg=_ROBOT):
   return torch.sum(out, dim=1)
 
 
+def is_alive(env):
+  """`envs/mdp/rewards.py:22-24`."""
+  return (~env.termination_manager.terminated).float()
+
+
+def is_terminated(env):
+  return env.termination_manager.terminated.float()
+
+
+def joint_torques_l2(env, asset_cfg=_ROBOT):
+  """`envs/mdp/rewards.py:32-37` (all actuators, whatever asset_cfg selects)."""
+  return torch.sum(torch.square(env.scene[asset_cfg.name].data.actuator_force), dim=1)
+
+
+def action_acc_l2(env):
+  """`envs/mdp/rewards.py:63-70`."""
+  am = env.action_manager
+  return torch.sum(torch.square(am.action - 2 * am.prev_action + am.prev_prev_action), dim=1)
+
+
 def action_rate_l2(env):
   return torch.sum(torch.square(env.action_manager.action - env.action_manager.prev_action), dim=1)
 

@@ -583,6 +583,14 @@ class Scene:
           slots.append((prim, fld, int(adr[i]), int(dim[i])))
       self._sensors[cname] = ContactSensor(cname, slots, spec["fields"], spec.get("num_slots", 1),
                                            spec.get("track_air_time", False))
+    if "terrain_origins" in mj_model.arrays:
+      # generator terrain: curriculum origins over the sub-terrain spawn points
+      # (terrain_importer.py:224-244), drawn from torch's global RNG like the reference
+      from .terrains import curriculum_env_origins
+      o, lv, ty = curriculum_env_origins(mj_model.arrays["terrain_origins"], num_envs)
+      self.env_origins = o.to(device)
+      self.terrain_levels, self.terrain_types = lv.to(device), ty.to(device)
+      return
     # env origins on a grid (terrain_importer.py:246-261)
     rows = int(np.ceil(num_envs / int(np.sqrt(num_envs))))
     cols = int(np.ceil(num_envs / rows))

@@ -79,9 +79,34 @@ def build_g1_tracking(xml_path: str) -> Model:
   return compile_scene([_g1_entity(xml_path)], contact_sensors=sensors, **VELOCITY_SIM)
 
 
+def _g1_jump_sensors():
+  """`tasks/jump/config/g1/env_cfgs.py:66-79`: feet vs terrain only."""
+  return [s for s in _g1_contact_sensors(self_collision=False)]
+
+
+def build_g1_jump(xml_path: str) -> Model:
+  """`Mjlab-Jump-Flat-Unitree-G1`: crouch keyframe, plane, dt 0.002."""
+  return compile_scene([_g1_entity(xml_path, init=az.G1_JUMP_CROUCH)],
+                       contact_sensors=_g1_jump_sensors(), **JUMP_SIM)
+
+
+def build_g1_jump_hfield(xml_path: str) -> Model:
+  """Config 5: the jump scene re-terrained onto the seeded 10 x 20 grid of
+  heightfield sub-terrains (terrains.hf_rough_terrains_cfg); spawn origins are stored
+  with the model (`terrain_origins`, [rows, cols, 3])."""
+  from .terrains import TerrainGenerator, hf_rough_terrains_cfg
+  hfields, origins = TerrainGenerator(hf_rough_terrains_cfg(seed=0)).generate()
+  m = compile_scene([_g1_entity(xml_path, init=az.G1_JUMP_CROUCH)], terrain="hfield",
+                    hfields=hfields, contact_sensors=_g1_jump_sensors(), **JUMP_SIM)
+  m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  return m
+
+
 SCENE_BUILDERS = {
   "g1_velocity": ("unitree_g1/xmls/g1.xml", build_g1_velocity),
   "g1_tracking": ("unitree_g1/xmls/g1.xml", build_g1_tracking),
+  "g1_jump": ("unitree_g1/xmls/g1.xml", build_g1_jump),
+  "g1_jump_hfield": ("unitree_g1/xmls/g1.xml", build_g1_jump_hfield),
   "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
 }
 
