@@ -10,6 +10,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/mjx355.h"
@@ -79,7 +80,7 @@ struct mjxSim_ {
   mjx::DModel dm;  // per-sim copy: expanded fields point to per-world buffers
   mjx::DData dd;
   mjx::Lds lds_ph[3];  // per-phase LDS carves
-  int gC = 0, gstride = 0;
+  int gC = 0, gF = 0, gstride = 0;
   float* gscr = nullptr;
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
@@ -98,6 +99,7 @@ static mjx::Params host_params(const mjxSim_* s) {
   for (int i = 0; i < 3; i++) p.LP[i] = s->lds_ph[i];
   p.gscr = s->gscr;
   p.gC = s->gC;
+  p.gF = s->gF;
   p.gstride = s->gstride;
   return p;
 }
@@ -311,7 +313,11 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
     }
   }
   s->gC = (s->lds_ph[1].pack_len + 63) & ~63;
-  s->gstride = s->gC + ((s->lds_ph[2].pack_len + 63) & ~63);
+  s->gF = s->gC + ((s->lds_ph[2].pack_len + 63) & ~63);
+  {
+    const int nvp = (s->d.nv + 3) & ~3;
+    s->gstride = s->gF + ((nvp * nvp + 63) & ~63);
+  }
   const mjx::Dims& d = s->d;
   // data arena: one allocation, 256-B aligned sub-buffers
   size_t off = 0;
@@ -327,6 +333,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_FLT
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
+  reserve("__wstats", sizeof(int32_t) * 8 * (size_t)nworld);
   reserve("__prof", sizeof(unsigned long long) * 32);
   hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
@@ -351,6 +358,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_FLT
 #undef X_INT
   s->dd.stats = (int32_t*)(base + offs[k++].second);
+  s->dd.wstats = (int32_t*)(base + offs[k++].second);
   s->dd.prof = (unsigned long long*)(base + offs[k++].second);
   s->stats = s->dd.stats;
   // model fields visible as "model.<name>"
@@ -527,8 +535,19 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
 
 int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {
   if (!s || !out) return fail("null argument");
-  HIPCHK(hipMemcpyAsync(out, s->stats, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  // per-world counters -> totals: [0] max contacts, [1] max rows, [2..4] overflow /
+  // row-overflow / unsupported-pair events, [5] max Newton iterations
+  std::vector<int32_t> ws((size_t)s->nworld * 8);
+  HIPCHK(hipMemcpyAsync(ws.data(), s->dd.wstats, sizeof(int32_t) * ws.size(), hipMemcpyDeviceToHost,
+                        (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  int32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int w = 0; w < s->nworld; w++) {
+    const int32_t* x = ws.data() + 8 * (size_t)w;
+    r[0] = std::max(r[0], x[0]); r[1] = std::max(r[1], x[1]); r[5] = std::max(r[5], x[5]);
+    r[2] += x[2]; r[3] += x[3]; r[4] += x[4];
+  }
+  for (int i = 0; i < 8; i++) out[i] = r[i];
   return 0;
 }
 

@@ -63,7 +63,8 @@ struct DData {
   MJX_DATA_INT_FIELDS(X_INT)
 #undef X_FLT
 #undef X_INT
-  int32_t* stats;  // [8] global counters (atomics)
+  int32_t* stats;   // [8] reduced engine counters (filled by mjx_sim_stats)
+  int32_t* wstats;  // [nworld][8] per-world counters (no cross-world atomics in the kernels)
   unsigned long long* prof;  // [32] stage cycle sums (diagnostic -DMJX_STAMPS build)
 };
 
@@ -96,8 +97,10 @@ struct Params {
   DModel m;
   DData D;
   Lds LP[3];     // per-phase LDS carves (A, B, C)
-  float* gscr;   // per-world hand-off scratch: [B pack | C pack], gstride floats per world
+  float* gscr;   // per-world hand-off scratch: [B pack | C pack | F], gstride floats per world
   int gC;        // offset of the C pack inside a world's scratch
+  int gF;        // offset of F: the implicit-integration factor (nvp x nvp rows), read by
+                 // phase C straight from global memory (not staged in LDS)
   int gstride;
 };
 

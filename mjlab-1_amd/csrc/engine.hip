@@ -64,11 +64,11 @@ Lds make_lds(const Dims& d, int ph) {
     {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
     {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
-    {&Lds::M, nv * nv, A | B | Cp}, {&Lds::H, nv * nv, A | B | Cp},
+    {&Lds::M, nv * nv, A | B}, {&Lds::H, nv * nv, A | B},
     {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
     {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
     {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
-    {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, Cp},
+    {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
     {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
     {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, A | Cp},
@@ -77,7 +77,7 @@ Lds make_lds(const Dims& d, int ph) {
     {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
     {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
     {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
-    {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, Cp},
+    {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, 0},
     {&Lds::red, 5 * kWave, B},
   };
   static int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
@@ -85,7 +85,7 @@ Lds make_lds(const Dims& d, int ph) {
   static int Lds::* const packC[] = {
       &Lds::cdof, &Lds::cdofdot, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
       &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
-      &Lds::con_frame, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::M, &Lds::qfrc_smooth,
+      &Lds::con_frame, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
       // written by phase B:
       &Lds::ints, &Lds::x, &Lds::qfrc_con, &Lds::efc_force};
   constexpr int kAbsent = 1 << 24;
@@ -108,7 +108,6 @@ Lds make_lds(const Dims& d, int ph) {
     L.red = L.M;
     L.efc_Js = L.efc_aref;
   }
-  if (ph == 2) L.H = L.M;  // integrate factors M + h D in place (M is dead afterwards)
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
     // collision, contacts, rows.  Two aliases follow from it:
@@ -1005,6 +1004,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
   float* gc = gw + P->gC;
+  float* gf = gw + P->gF;  // implicit-integration factor (phase A writes, phase C reads)
   (void)LB; (void)LC; (void)gc;
   const int lane = threadIdx.x;
   int* Si = reinterpret_cast<int*>(S);
@@ -1265,9 +1265,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       S[L.M + i * nvp + i] += Dr.arm;
     }
     sync();
-    // M to the B and C packs now: its LDS slot is reused (in place factor, then contacts)
+    // M to the B pack now: its LDS slot is reused (in place factor, then contacts).  Phase C
+    // gets the implicit-integration factor of M + h D instead (below, scratch region F).
     cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
-    cp4(gc + LC.M, S + L.M, nvp * nvp, lane);
     STAMP(2);
     // =========================================================== velocity stage
     if (lane < 6) S[L.cvel + lane] = 0;
@@ -1384,6 +1384,33 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     sync();
     STAMP(6);
+    if (integrate) {
+      // implicitfast / Euler: factor M + h diag(dof damping - gear^2 biasprm2) here, where M
+      // and the (clamped) actuator forces are at hand, into the scratch region F; phase C then
+      // runs only the two triangular solves.  The actuator term is dropped for an actuator
+      // whose force is at its forcerange limit (zero derivative), as in mj_implicit.
+      float act_d = 0.f;
+      if (o.integrator == 1 && lane < nu && Ar.b2 != 0.f) {
+        bool skip = false;
+        if (Ar.forcelim) {
+          const float fo = S[L.act_force + lane];
+          skip = fo <= Ar.fr0 || fo >= Ar.fr1;
+        }
+        if (!skip) act_d = -h * Ar.gear * Ar.gear * Ar.b2;
+      }
+      float da = lane < nv ? h * Dr.damp : 0.f;
+      for (int u = 0; u < nu; u++) {  // scatter actuator terms onto their dofs
+        const float cu = rl(act_d, u);
+        if (lane == __builtin_amdgcn_readlane(Ar.dof, u)) da += cu;
+      }
+      float A[NR];
+      rows_load<NR>(A, S + L.M, nvp, lane);
+#pragma unroll
+      for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
+      float rd;
+      rows_chol<NR>(A, rd, nvp, lane);
+      rows_store_strict<NR>(A, rd, gf, nvp, lane);
+    }
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
     spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, nvp, lane);
     STAMP(7);
@@ -2266,16 +2293,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       const bool in = i < nv;
       S[L.qvel + i] = in ? D.qvel[(size_t)w * nv + i] : 0.f;
       S[L.qacc_ws + i] = in ? D.qacc_warmstart[(size_t)w * nv + i] : 0.f;
-      S[L.vtmp + i] = 0.f;
     }
     for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
     float time = D.time[w];
     const BodyLite B = load_body_lite(m, d, min(lane, nb - 1));
     const bool bl = lane < nb;
-    const ActRec Ar = load_act(m, MF(actuator_gear), MF(actuator_gainprm), MF(actuator_biasprm),
-                               MF(actuator_forcerange), MF(actuator_ctrlrange),
-                               min(lane, max(nu - 1, 0)));
-    const float damp_l = MF(dof_damping)[min(lane, max(nv - 1, 0))];
     lds_dma_wait();
     sync();
     const int nefc = ints[1];
@@ -2425,13 +2447,12 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.contact_force[(wc + c) * 3 + 1] = f.y;
         D.contact_force[(wc + c) * 3 + 2] = f.z;
       }
-      if (lane == 0) {
-        atomicMax(&D.stats[0], ints[0]);
-        atomicMax(&D.stats[1], nefc);
-        if (ints[3] & 1) atomicAdd(&D.stats[2], 1);
-        if (ints[3] & 2) atomicAdd(&D.stats[3], 1);
-        if (ints[3] & 4) atomicAdd(&D.stats[4], 1);
-        atomicMax(&D.stats[5], niter_last);
+      if (lane < 6) {  // per-world counters: [0,1,5] running max, [2..4] event counts
+        int* ws = D.wstats + 8 * (size_t)w;
+        const int v = lane == 0 ? ints[0] : lane == 1 ? nefc : lane == 5 ? niter_last
+                    : (ints[3] >> (lane - 2)) & 1;
+        const int old = ws[lane];
+        ws[lane] = (lane >= 2 && lane <= 4) ? old + v : max(old, v);
       }
     }
     STAMP(12);
@@ -2443,22 +2464,17 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // =========================================================== implicitfast / Euler
     sync();
     {
-      for (int i = lane; i < nvp; i += kWave) S[L.hdiag + i] = i < nv ? h * damp_l : 0.f;
-      sync();
       SUBSTAMP(9);
-      if (o.integrator == 1 && lane < nu) {
-        bool skip = Ar.b2 == 0.f;
-        if (Ar.forcelim) {
-          const float fo = S[L.act_force + lane];
-          skip = skip || fo <= Ar.fr0 || fo >= Ar.fr1;
-        }
-        if (!skip) atomicAdd(S + L.hdiag + Ar.dof, -h * Ar.gear * Ar.gear * Ar.b2);
-      }
-      for (int i = lane; i < nvp; i += kWave) S[L.vtmp + i] = S[L.qfrc_smooth + i] + S[L.qfrc_con + i];
-      sync();
+      // (M + h D) qacc' = qfrc_smooth + qfrc_constraint with the factor phase A stored in
+      // the world's scratch (rows and columns come straight from global memory)
       SUBSTAMP(10);
-      spd_factor_solve<NR>(S + L.M, S + L.hdiag, S + L.H, S + L.vtmp, nvp, lane);
-      for (int i = lane; i < nv; i += kWave) S[L.qvel + i] += h * S[L.vtmp + i];
+      {
+        float A[NR], rd;
+        rows_load_factor<NR>(A, rd, gf, nvp, lane);
+        const float f = lane < nvp ? S[L.qfrc_smooth + lane] + S[L.qfrc_con + lane] : 0.f;
+        const float acc = rows_solve<NR>(A, rd, gf, f, nvp, lane);
+        if (lane < nv) S[L.qvel + lane] += h * acc;
+      }
       sync();
       SUBSTAMP(11);
       for (int k = lane; k < d.njnt; k += kWave) {

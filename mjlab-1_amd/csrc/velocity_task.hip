@@ -160,10 +160,11 @@ __global__ void k_substep(const mjxTaskDesc* __restrict__ T) {
   t.last_time[e] = now;
 }
 
-__global__ void k_post(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
-  const mjxTaskDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= t.nworld) return;
+// Per-env terminations, rewards and reset bookkeeping.  Cross-env accumulators go to the
+// block's LDS copy of Acc (ds_add_f32) and are flushed with one global atomic per field and
+// block: thousands of lanes adding into the same few global addresses serialise at the
+// memory side (MI355X_MICROARCH.md, float atomics: one target row is ~14x slower).
+__device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, Acc* __restrict__ acc) {
   const int64_t len = t.episode_length[e] + 1;
   t.episode_length[e] = len;
   const Root r = root_state(t, e);
@@ -337,6 +338,21 @@ __global__ void k_post(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc)
     t.metric_err_xy[e] = 0.f;
     t.metric_err_yaw[e] = 0.f;
   }
+}
+
+__global__ void k_post(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
+  const mjxTaskDesc& t = *T;
+  __shared__ Acc sh;
+  float* shf = reinterpret_cast<float*>(&sh);
+  constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
+  for (int i = threadIdx.x; i < kAccN; i += blockDim.x) shf[i] = 0.f;
+  __syncthreads();
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < t.nworld) post_env(t, e, &sh);
+  __syncthreads();
+  float* gf = reinterpret_cast<float*>(acc);
+  for (int i = threadIdx.x; i < kAccN; i += blockDim.x)
+    if (shf[i] != 0.f) atomicAdd(gf + i, shf[i]);
 }
 
 __device__ __forceinline__ void resample_command(const mjxTaskDesc& t, int e, uint64_t step,
