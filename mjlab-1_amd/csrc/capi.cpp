@@ -79,7 +79,17 @@ struct mjxSim_ {
   mjx::Dims d;
   mjx::DModel dm;  // per-sim copy: expanded fields point to per-world buffers
   mjx::DData dd;
-  mjx::Lds lds_ph[3];  // per-phase LDS carves
+  mjx::Lds lds_ph[3 + mjx::kRowClasses];  // per-phase LDS carves ([3 + k]: Newton row class k)
+  int nrowclass = 0;
+  int row_cap[mjx::kRowClasses] = {};
+  mjx::SideStream side{};  // streams of the Newton row classes (when classes are used)
+  ~mjxSim_() {
+    if (side.fork) (void)hipEventDestroy(side.fork);
+    for (int k = 0; k < mjx::kRowClasses; k++) {
+      if (side.join[k]) (void)hipEventDestroy(side.join[k]);
+      if (side.stream[k]) (void)hipStreamDestroy(side.stream[k]);
+    }
+  }
   int gC = 0, gF = 0, gstride = 0;
   float* gscr = nullptr;
   void* arena = nullptr;
@@ -96,7 +106,9 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.o = s->model->o;
   p.m = s->dm;
   p.D = s->dd;
-  for (int i = 0; i < 3; i++) p.LP[i] = s->lds_ph[i];
+  for (int i = 0; i < 3 + mjx::kRowClasses; i++) p.LP[i] = s->lds_ph[i];
+  p.nrowclass = s->nrowclass;
+  for (int k = 0; k < mjx::kRowClasses; k++) p.row_cap[k] = s->row_cap[k];
   p.gscr = s->gscr;
   p.gC = s->gC;
   p.gF = s->gF;
@@ -312,6 +324,20 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
   }
+  s->nrowclass = mjx::choose_row_classes(s->d, s->row_cap);
+  for (int k = 0; k < mjx::kRowClasses; k++) {
+    mjx::Dims ds = s->d;
+    ds.njmax = k < s->nrowclass ? s->row_cap[k] : s->d.njmax;
+    s->lds_ph[3 + k] = mjx::make_lds(ds, 1);
+  }
+  if (s->nrowclass > 0) {
+    hipError_t e = hipEventCreateWithFlags(&s->side.fork, hipEventDisableTiming);
+    for (int k = 0; k < s->nrowclass && e == hipSuccess; k++) {
+      e = hipStreamCreateWithFlags(&s->side.stream[k], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[k], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) { delete s; return fail(std::string("side streams: ") + hipGetErrorString(e)); }
+  }
   s->gC = (s->lds_ph[1].pack_len + 63) & ~63;
   s->gF = s->gC + ((s->lds_ph[2].pack_len + 63) & ~63);
   {
@@ -417,7 +443,7 @@ int mjx_step(mjxSim* s, int nsubstep, void* stream) {
   if (!s) return fail("null sim");
   if (nsubstep < 1) return fail("nsubstep must be >= 1");
   hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, nsubstep, 1, nullptr,
-                                  (hipStream_t)stream);
+                                  (hipStream_t)stream, &s->side);
   if (e != hipSuccess) return fail(std::string("step launch: ") + hipGetErrorString(e));
   return 0;
 }
@@ -427,7 +453,7 @@ int mjx_forward(mjxSim* s, void* stream) { return mjx_forward_masked(s, nullptr,
 int mjx_forward_masked(mjxSim* s, const uint8_t* mask, void* stream) {
   if (!s) return fail("null sim");
   hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, 1, 0, mask,
-                                  (hipStream_t)stream);
+                                  (hipStream_t)stream, &s->side);
   if (e != hipSuccess) return fail(std::string("forward launch: ") + hipGetErrorString(e));
   return 0;
 }

@@ -15,6 +15,7 @@ constexpr int kMaskWords = 16;   // contact-sensor geom masks (512 geoms)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
+constexpr int kRowClasses = 2;   // Newton row classes below the full capacity
 
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
@@ -96,7 +97,12 @@ struct Params {
   Opt o;
   DModel m;
   DData D;
-  Lds LP[3];     // per-phase LDS carves (A, B, C)
+  // Per-phase LDS carves: [0] A, [1] B at full row capacity, [2] C, [3 + k] B for Newton row
+  // class k.  Worlds whose nefc fits class k's capacity run Newton in its smaller carve (more
+  // resident worlds per CU); classes run concurrently (launch_step).
+  Lds LP[3 + kRowClasses];
+  int nrowclass;                 // row classes in use (0 = every world in LP[1])
+  int row_cap[kRowClasses];      // ascending row capacities of the classes
   float* gscr;   // per-world hand-off scratch: [B pack | C pack | F], gstride floats per world
   int gC;        // offset of the C pack inside a world's scratch
   int gF;        // offset of F: the implicit-integration factor (nvp x nvp rows), read by
@@ -107,8 +113,17 @@ struct Params {
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.
 hipError_t prepare_step(const Params& host);  // one-time kernel attributes (not capturable)
+// Side streams for the Newton row classes beyond the first: forked from and joined back
+// into the launch stream every substep (graph-capturable fork/join).
+struct SideStream {
+  hipStream_t stream[kRowClasses];
+  hipEvent_t fork, join[kRowClasses];
+};
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
-                       int integrate, const uint8_t* mask, hipStream_t stream);
+                       int integrate, const uint8_t* mask, hipStream_t stream,
+                       const SideStream* side);
+// Newton row classes (capacities ascending into caps[]); returns how many are used.
+int choose_row_classes(const Dims& d, int (&caps)[kRowClasses]);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
                         int nworld, hipStream_t stream);
 

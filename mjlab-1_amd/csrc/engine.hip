@@ -17,6 +17,7 @@
 // stage by stage, restated in oracle/oracle.c (the parity checker).
 #include <float.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <initializer_list>
 #include <utility>
 #include <math.h>
@@ -996,7 +997,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const Opt& o = P->o;
   const DModel& m = P->m;
   const DData& D = P->D;
-  const Lds& L = P->LP[PH];
+  // phase B: `integrate` carries the Newton row class (0 = full capacity, k > 0 = LP[2 + k])
+  const Lds& L = P->LP[PH == 1 && integrate > 0 ? 2 + integrate : PH];
   const Lds& LB = P->LP[1];
   const Lds& LC = P->LP[2];
   const int w = blockIdx.x;
@@ -2043,7 +2045,22 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // ----------------------------------------------------------- phase B (Newton)
     {
       const int nefc_in = reinterpret_cast<const int*>(gw)[LB.ints + 1];
+      // row classes (launch_step): class k > 0 takes row_cap[k-2] < nefc <= row_cap[k-1],
+      // class 0 the worlds above every class capacity (all of them without classes)
+      const int cls = integrate;
+      const int nc = P->nrowclass;
+      const int lo = cls == 0 ? (nc > 0 ? P->row_cap[nc - 1] : -1) : (cls > 1 ? P->row_cap[cls - 2] : -1);
+      if (nefc_in <= lo || (cls > 0 && nefc_in > P->row_cap[cls - 1])) return;
+      if (cls == 0) {
         cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
+      } else {
+        // the pack is laid out with the full-capacity carve LB: [ints M qacc_smooth
+        // qfrc_smooth efc_aref] sit at the same offsets in both, efc_D and efc_J move
+        const int nr4 = (nefc_in + 3) & ~3;
+        cp_pack(S, gw, LB.efc_aref + nr4, lane);
+        cp_pack(S + L.efc_D, gw + LB.efc_D, nr4, lane);
+        cp_pack(S + L.efc_J, gw + LB.efc_J, nefc_in * nvp, lane);
+      }
     }
     const Tiles T = make_tiles(nvp, lane);
     for (int i = lane; i < nvp; i += kWave) {
@@ -2571,16 +2588,17 @@ static size_t lds_bytes(const Params& host, int ph) {
     const char* e = getenv("MJX355_LDS_PAD");
     return e ? atol(e) : 0L;
   }();
-  const long p = pad_all + pad[ph];
+  const long p = pad_all + pad[ph >= 3 ? 1 : ph];
   return (size_t)host.LP[ph].total * 4 + (size_t)(p > 0 ? p : 0);
 }
 
 hipError_t prepare_step(const Params& host) {
+  size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
+  for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
   for (int ph = 0; ph < 3; ph++) {
-    size_t shmem = lds_bytes(host, ph);
-    if (shmem > 64 * 1024) {
+    if (shmem[ph] > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)step_fn(host.d.nv, ph),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem[ph]);
       if (e != hipSuccess) return e;
     }
   }
@@ -2588,15 +2606,81 @@ hipError_t prepare_step(const Params& host) {
 }
 
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
-                       int integrate, const uint8_t* mask, hipStream_t stream) {
+                       int integrate, const uint8_t* mask, hipStream_t stream,
+                       const SideStream* side) {
   if (nworld <= 0) return hipSuccess;
+  const StepFn fA = step_fn(host.d.nv, 0), fB = step_fn(host.d.nv, 1), fC = step_fn(host.d.nv, 2);
+  const int nc = host.nrowclass;
+  if (nc > 0 && !side) return hipErrorInvalidValue;
   for (int sub = 0; sub < nsubstep; sub++) {
     const int last = sub == nsubstep - 1;
-    for (int ph = 0; ph < 3; ph++)
-      hipLaunchKernelGGL(step_fn(host.d.nv, ph), dim3(nworld), dim3(kWave), lds_bytes(host, ph),
-                         stream, dev, nworld, last, integrate, mask);
+    hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(host, 0), stream, dev, nworld,
+                       last, integrate, mask);
+    if (nc > 0) {
+      // Newton by row class, concurrently: the full-capacity class (few worlds, long
+      // per-world latency) first on a side stream so its blocks dispatch first, the middle
+      // classes on further side streams, the smallest (most worlds) on the launch stream
+      hipError_t e = hipEventRecord(side->fork, stream);
+      if (e != hipSuccess) return e;
+      for (int k = 0; k < nc; k++) {
+        const int cls = k == 0 ? 0 : nc + 1 - k;  // 0, then nc, nc-1, ..., 2
+        e = hipStreamWaitEvent(side->stream[k], side->fork, 0);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fB, dim3(nworld), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
+                           side->stream[k], dev, nworld, last, cls, mask);
+      }
+      hipLaunchKernelGGL(fB, dim3(nworld), dim3(kWave), lds_bytes(host, 3), stream, dev, nworld,
+                         last, 1, mask);
+      for (int k = 0; k < nc; k++) {
+        e = hipEventRecord(side->join[k], side->stream[k]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join[k], 0);
+        if (e != hipSuccess) return e;
+      }
+    } else {
+      hipLaunchKernelGGL(fB, dim3(nworld), dim3(kWave), lds_bytes(host, 1), stream, dev, nworld,
+                         last, 0, mask);
+    }
+    hipLaunchKernelGGL(fC, dim3(nworld), dim3(kWave), lds_bytes(host, 2), stream, dev, nworld,
+                       last, integrate, mask);
   }
   return hipGetLastError();
+}
+
+int choose_row_classes(const Dims& d, int (&caps)[kRowClasses]) {
+  for (int k = 0; k < kRowClasses; k++) caps[k] = 0;
+  int n = 0;
+  if (const char* e = getenv("MJX355_ROW_CLASSES")) {  // diagnostic: "44,80" or "" (none)
+    for (const char* c = e; *c && n < kRowClasses;) {
+      const int v = atoi(c);
+      if (v > 0 && v < d.njmax && (n == 0 || v > caps[n - 1])) caps[n++] = v;
+      while (*c && *c != ',') c++;
+      if (*c == ',') c++;
+    }
+    return n;
+  }
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, (const void*)step_fn(d.nv, 1)) != hipSuccess) return 0;
+  // wave64 on gfx950: 512 VGPRs per SIMD lane (granule 8), 4 SIMDs per CU
+  const int regs = (fa.numRegs + 7) & ~7;
+  const int top = 4 * (regs > 0 ? std::min(8, 512 / regs) : 8);  // register-bound worlds/CU
+  // largest row capacity (multiple of 4) whose phase-B carve lets `w` worlds share a CU
+  auto cap_for = [&](int w) {
+    Dims ds = d;
+    for (int r = (d.njmax - 1) & ~3; r >= 8; r -= 4) {
+      ds.njmax = r;
+      if ((size_t)make_lds(ds, 1).total * 4 <= (size_t)160 * 1024 / w) return r;
+    }
+    return 0;
+  };
+  if ((size_t)make_lds(d, 1).total * 4 <= (size_t)160 * 1024 / top) return 0;  // no need
+  // class 1 at the register-bound residency, class 2 at two thirds of it (when that still
+  // beats the full carve by a margin: measured, a class at <= 5 worlds/CU does not pay)
+  for (int w : {top, (2 * top) / 3}) {
+    if (w < 8) continue;
+    const int r = cap_for(w);
+    if (r > 0 && (n == 0 || r > caps[n - 1]) && n < kRowClasses) caps[n++] = r;
+  }
+  return n;
 }
 
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
