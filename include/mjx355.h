@@ -145,7 +145,7 @@ int mjx_field_is_expanded(const mjxSim* sim, const char* name);
 /* Diagnostics: per-sim counters (max contacts/rows seen, overflow events) as
  * int32[8] written to host `out`; synchronises the stream. */
 int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);
-/* Diagnostics: per-stage cycle sums uint64[32] (non-zero only in the -DMJX_STAMPS build). */
+/* Diagnostics: per-stage cycle sums uint64[48] (non-zero only in the -DMJX_STAMPS build). */
 int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
 
 #ifdef __cplusplus

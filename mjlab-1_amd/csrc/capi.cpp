@@ -360,7 +360,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
   reserve("__wstats", sizeof(int32_t) * 8 * (size_t)nworld);
-  reserve("__prof", sizeof(unsigned long long) * 32);
+  reserve("__prof", sizeof(unsigned long long) * 48);
   hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
   e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->gstride);
@@ -554,7 +554,7 @@ int mjx_expand_field(mjxSim* s, const char* cname, void* stream) {
 
 int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
   if (!s || !out) return fail("null argument");
-  HIPCHK(hipMemcpyAsync(out, s->dd.prof, sizeof(uint64_t) * 32, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipMemcpyAsync(out, s->dd.prof, sizeof(uint64_t) * 48, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }

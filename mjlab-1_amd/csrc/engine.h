@@ -66,7 +66,7 @@ struct DData {
 #undef X_INT
   int32_t* stats;   // [8] reduced engine counters (filled by mjx_sim_stats)
   int32_t* wstats;  // [nworld][8] per-world counters (no cross-world atomics in the kernels)
-  unsigned long long* prof;  // [32] stage cycle sums (diagnostic -DMJX_STAMPS build)
+  unsigned long long* prof;  // [48] stage cycle sums (diagnostic -DMJX_STAMPS build)
 };
 
 // Per-world LDS carve (offsets in 4-byte words).

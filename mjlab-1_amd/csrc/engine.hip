@@ -302,7 +302,7 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
 #define STAMP_FLUSH()                                                            \
   do {                                                                           \
     if (lane == 0)                                                               \
-      for (int k_ = 0; k_ < 32; k_++)                                            \
+      for (int k_ = 0; k_ < 48; k_++)                                            \
         if (stamp_acc[k_]) atomicAdd((unsigned long long*)&D.prof[k_], stamp_acc[k_]); \
   } while (0)
 #else
@@ -810,6 +810,12 @@ __device__ __forceinline__ void cp_pack(float* __restrict__ dst, const float* __
       __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + 4 * lane), (lds_void_t)(dst + i0),
                                        16, 0, 0);
 }
+// Global -> LDS copy of n floats (any alignment) by 4-byte LDS-DMA, lane per float.
+__device__ __forceinline__ void dma_row(float* dst, const float* src, int n, int lane) {
+  for (int i0 = 0; i0 < n; i0 += kWave)
+    if (i0 + lane < n)
+      __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + lane), (lds_void_t)(dst + i0), 4, 0, 0);
+}
 __device__ __forceinline__ void lds_dma_wait() {
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
@@ -1019,9 +1025,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
 #ifdef MJX_STAMPS
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
   unsigned long long sub_prev = stamp_prev;
-  unsigned long long stamp_acc[32];
+  unsigned long long stamp_acc[48];
 #pragma unroll
-  for (int k_ = 0; k_ < 32; k_++) stamp_acc[k_] = 0;
+  for (int k_ = 0; k_ < 48; k_++) stamp_acc[k_] = 0;
 #endif
   const float* body_pos = MF(body_pos);
   const float* body_quat = MF(body_quat);
@@ -1037,28 +1043,27 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
 
   if constexpr (PH == 0) {
     // ----------------------------------------------------------- phase A
+    // Preamble: every independent global read is in flight before the first wait -- state
+    // rows go straight into LDS (LDS-DMA), model records into registers, then one wait
+    // (copied loop by loop, each load-then-LDS-store would wait out a global latency).
     for (int i = lane; i < nvp; i += kWave) {
-      S[L.qvel + i] = 0.f; S[L.qfrc_applied + i] = 0.f; S[L.qfrc_bias + i] = 0.f;
-      S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f; S[L.qfrc_smooth + i] = 0.f;
-      S[L.qacc_smooth + i] = 0.f;
+      if (i >= nv) { S[L.qvel + i] = 0.f; S[L.qfrc_applied + i] = 0.f; }  // DMA fills i < nv
+      S[L.qfrc_bias + i] = 0.f; S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f;
+      S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f;
     }
-    sync();
-    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
-    for (int i = lane; i < nv; i += kWave) {
-      S[L.qvel + i] = D.qvel[(size_t)w * nv + i];
-      S[L.qfrc_applied + i] = D.qfrc_applied[(size_t)w * nv + i];
-    }
-    for (int i = lane; i < nu; i += kWave) S[L.ctrl + i] = D.ctrl[(size_t)w * nu + i];
-    int any_xfrc = 0;
-    for (int i = lane; i < 6 * nb; i += kWave) {
-      float v = D.xfrc_applied[(size_t)w * 6 * nb + i];
-      any_xfrc |= (v != 0.f);
-    }
-    any_xfrc = __any(any_xfrc);
+    dma_row(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
+    dma_row(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
+    dma_row(S + L.qfrc_applied, D.qfrc_applied + (size_t)w * nv, nv, lane);
+    dma_row(S + L.ctrl, D.ctrl + (size_t)w * nu, nu, lane);
+    SUBSTAMP(15);
     float* Jg = gw + LB.efc_J;
     const BodyPtrs BP{body_pos, body_quat, body_ipos, body_iquat, body_mass, body_inertia,
                       jnt_pos, jnt_axis, qpos0};
     const BodyRec B = load_body(m, d, BP, min(lane, nb - 1));
+#ifdef MJX_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SUBSTAMP(16);
     const bool bl = lane < nb;  // this lane holds a body record
     DofRec Dr;
     {
@@ -1072,10 +1077,19 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       Dr.jt = m.jnt_type[j]; Dr.qa = m.jnt_qposadr[j];
       Dr.arm = arm[i]; Dr.damp = damping[i]; Dr.stiff = jstiff[j]; Dr.qs = qspring[Dr.qa];
     }
+#ifdef MJX_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SUBSTAMP(17);
     const ActRec Ar = load_act(m, MF(actuator_gear), MF(actuator_gainprm), MF(actuator_biasprm),
                                MF(actuator_forcerange), MF(actuator_ctrlrange),
                                min(lane, max(nu - 1, 0)));
+    int any_xfrc = 0;
+    for (int i = lane; i < 6 * nb; i += kWave) any_xfrc |= D.xfrc_applied[(size_t)w * 6 * nb + i] != 0.f;
+    any_xfrc = __any(any_xfrc);
+    lds_dma_wait();
     sync();
+    SUBSTAMP(13);
     // =========================================================== kinematics (levels)
     if (lane == 0) {
       S[L.xpos + 0] = S[L.xpos + 1] = S[L.xpos + 2] = 0;
@@ -1124,6 +1138,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       sync();
     }
+    SUBSTAMP(14);
     if (bl) {
       const int b = B.b;
       float* R = S + L.xmat + 9 * b;
@@ -1967,7 +1982,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     STAMP(11);
     // outputs final after phase A
+#ifdef MJX_ABLATE_OUTPUTS
+    if (false) {
+#else
     if (last) {
+#endif
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 3 * nb; i += kWave) {
         D.xpos[wb * 3 + i] = S[L.xpos + i];
@@ -1982,11 +2001,21 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.ximat[wb * 9 + i] = S[L.ximat + i];
       }
       for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
-      size_t wg = (size_t)w * d.ngeom;  // heightfield frames are static (set at sim creation)
-      for (int i = lane; i < 3 * d.ngeom_lds; i += kWave)
-        D.geom_xpos[(wg + m.lds_geom[i / 3]) * 3 + i % 3] = S[L.gxpos + i];
-      for (int i = lane; i < 9 * d.ngeom_lds; i += kWave)
-        D.geom_xmat[(wg + m.lds_geom[i / 9]) * 9 + i % 9] = S[L.gxmat + i];
+      // lane per geom: one model-index load per lane up front, not one per element (a
+      // dependent global load in every iteration of an element loop serialises on latency);
+      // heightfield frames are static (set at sim creation)
+      size_t wg = (size_t)w * d.ngeom;
+      for (int i = lane; i < d.ngeom_lds; i += kWave) {
+        const size_t g = wg + m.lds_geom[i];
+        const float* xp = S + L.gxpos + 3 * i;
+        const float* xm = S + L.gxmat + 9 * i;
+        float* op = D.geom_xpos + g * 3;
+        float* om = D.geom_xmat + g * 9;
+#pragma unroll
+        for (int t = 0; t < 3; t++) op[t] = xp[t];
+#pragma unroll
+        for (int t = 0; t < 9; t++) om[t] = xm[t];
+      }
       size_t ws = (size_t)w * d.nsite;
       for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
       for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];
@@ -2015,6 +2044,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
+    STAMP(12);
     // hand-off: B pack (J rows already written) and the A part of the C pack
     const int C = d.nconmax;
     const int C4 = (C + 3) & ~3;
@@ -2619,7 +2649,9 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     if (nc > 0) {
       // Newton by row class, concurrently: the full-capacity class (few worlds, long
       // per-world latency) first on a side stream so its blocks dispatch first, the middle
-      // classes on further side streams, the smallest (most worlds) on the launch stream
+      // classes on further side streams, the smallest (most worlds) on the launch stream.
+      // Measured: forking the side classes after the smallest makes the full class the tail
+      // (B span 240 -> 255 us, G1).
       hipError_t e = hipEventRecord(side->fork, stream);
       if (e != hipSuccess) return e;
       for (int k = 0; k < nc; k++) {

@@ -265,7 +265,7 @@ class Simulation:
 
   def profile(self) -> list[int]:
     """Per-stage cycle sums (diagnostic MJX_STAMPS build only)."""
-    out = (ctypes.c_uint64 * 32)()
+    out = (ctypes.c_uint64 * 48)()
     check(lib().mjx_sim_profile(self._sim, out, _stream_handle(self._torch_device)))
     return list(out)
 

@@ -27,7 +27,8 @@ for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
   SUB = ["  nt: warmstart", "  nt: grad (active, J^T w)", "  nt: H assembly", "  nt: cholesky",
          "  nt: solve", "  nt: M s, J s, dots", "  nt: line search", "  nt: update+cost",
          "  nt: final forces", "  int: damping", "  int: actuator bias", "  int: factor+solve",
-         "  int: joints"]
+         "  int: joints", "  A: preamble rest (act)", "  A: kinematics levels", "  A: pre: state+xfrc",
+         "  A: pre: body recs", "  A: pre: dof recs"]
   for i, n in enumerate(SUB):
     print(f"  {n:22s} {d[16 + i] / nsub:10.0f}  {100 * d[16 + i] / max(tot, 1):5.1f}%")
   print("  stats", env.sim.stats(), "mean niter", float(env.sim.field("solver_niter").float().mean()))
