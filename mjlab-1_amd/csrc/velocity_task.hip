@@ -117,13 +117,16 @@ __device__ __forceinline__ float command_active(const float* c, float thr) {
 }
 
 // ----------------------------------------------------------------------------- kernels
+// Thread per (env, joint): a thread-per-env loop serialises every iteration on a global
+// load, since its stores may alias the next iteration's loads.
 __global__ void k_action(const mjxTaskDesc* __restrict__ T, const float* __restrict__ a) {
   const mjxTaskDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) *t.step_counter += 1;  // later kernels of this env step read the new value
-  if (e >= t.nworld) return;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx == 0) *t.step_counter += 1;  // later kernels of this env step read the new value
   const int nj = t.njoint;
-  for (int k = 0; k < nj; k++) {
+  if (idx >= t.nworld * nj) return;
+  const int e = idx / nj, k = idx - e * nj;
+  {
     const size_t i = (size_t)e * nj + k;
     const float raw = a[i];
     t.prev_prev_action[i] = t.prev_action[i];
@@ -164,38 +167,83 @@ __global__ void k_substep(const mjxTaskDesc* __restrict__ T) {
 // block's LDS copy of Acc (ds_add_f32) and are flushed with one global atomic per field and
 // block: thousands of lanes adding into the same few global addresses serialise at the
 // memory side (MI355X_MICROARCH.md, float atomics: one target row is ~14x slower).
-__device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, Acc* __restrict__ acc) {
+// Joint sums of the per-joint reward terms, reduced over the env's wave (lane per joint):
+// pose deviation under each std table, soft-limit violation, action rate.  A thread-per-env
+// loop pays two dependent global loads (joint index, then qpos) per joint.
+struct JointSums { float pose[3], lim, rate; };
+__device__ __forceinline__ float wave_add(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ JointSums joint_sums(const mjxTaskDesc& t, int e, int lane) {
+  JointSums r{{0.f, 0.f, 0.f}, 0.f, 0.f};
+  const int nj = t.njoint;
+  for (int j = lane; j < nj; j += 64) {
+    const float q = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
+    const float d = q - t.default_joint_pos[j];
+    const float s0 = t.std_standing[j], s1 = t.std_walking[j], s2 = t.std_running[j];
+    r.pose[0] += d * d / (s0 * s0);
+    r.pose[1] += d * d / (s1 * s1);
+    r.pose[2] += d * d / (s2 * s2);
+    r.lim += fmaxf(t.soft_lo[j] - q, 0.f) + fmaxf(q - t.soft_hi[j], 0.f);
+    const float da = t.action[(size_t)e * nj + j] - t.prev_action[(size_t)e * nj + j];
+    r.rate += da * da;
+  }
+  for (int k = 0; k < 3; k++) r.pose[k] = wave_add(r.pose[k]);
+  r.lim = wave_add(r.lim);
+  r.rate = wave_add(r.rate);
+  return r;
+}
+
+// Called by every lane of the env's wave: lane k evaluates termination k and reward term k
+// (terms are independent; their loads overlap instead of queueing behind each other's
+// stores), the wave reduces the flags and the reward total.
+__device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, const JointSums& js,
+                                         const int lane, Acc* __restrict__ acc) {
   const int64_t len = t.episode_length[e] + 1;
-  t.episode_length[e] = len;
   const Root r = root_state(t, e);
   const float* sd = t.sensordata + (size_t)e * t.nsensordata;
+  if (lane == 0) t.episode_length[e] = len;
   // ---- terminations (termination_manager.py:87-97)
-  bool terminated = false, truncated = false;
-  for (int k = 0; k < t.ntermination; k++) {
+  bool tm_v = false;
+  {
+    const int k = lane;
     bool v = false;
-    switch (t.termination_kind[k]) {
+    switch (k < t.ntermination ? t.termination_kind[k] : -1) {
       case MJX_TM_TIME_OUT: v = len >= t.max_episode_length; break;
       case MJX_TM_BAD_ORIENT: v = fabsf(acosf(-r.grav_b.z)) > t.termination_p0[k]; break;  // NaN -> false, as torch
       case MJX_TM_ILLEGAL_CONTACT:
         for (int s = 0; s < t.nillegal; s++) v |= sd[t.illegal_found_adr[s]] > 0.f;
         break;
     }
-    t.term_dones[(size_t)k * t.nworld + e] = v;
-    if (t.termination_is_timeout[k]) truncated |= v; else terminated |= v;
+    if (k < t.ntermination) {
+      t.term_dones[(size_t)k * t.nworld + e] = v;
+      tm_v = v;
+    }
   }
+  const bool is_to = lane < t.ntermination && t.termination_is_timeout[lane];
+  const bool truncated = __ballot(tm_v && is_to) != 0ull;
+  const bool terminated = __ballot(tm_v && !is_to) != 0ull;
   const bool reset = terminated || truncated;
-  t.terminated[e] = terminated;
-  t.time_outs[e] = truncated;
-  t.reset_buf[e] = reset;
+  if (lane == 0) {
+    t.terminated[e] = terminated;
+    t.time_outs[e] = truncated;
+    t.reset_buf[e] = reset;
+  }
   // ---- rewards (reward_manager.py:77-91)
   const float dt = t.step_dt;
   const float* cmd = t.command + (size_t)e * 3;
   const int nj = t.njoint;
   float total = 0.f;
-  for (int k = 0; k < t.nreward; k++) {
-    const float w = t.reward_weight[k];
+  do {
+    const int k = lane;
+    const float w = k < t.nreward ? t.reward_weight[k] : 0.f;
     float* sr = t.step_reward + (size_t)e * t.nreward + k;
-    if (w == 0.f) { *sr = 0.f; continue; }
+    if (w == 0.f) {
+      if (k < t.nreward) *sr = 0.f;
+      break;
+    }
     const float p0 = t.reward_p0[k], p1 = t.reward_p1[k], p2 = t.reward_p2[k];
     float f = 0.f;
     switch (t.reward_kind[k]) {
@@ -215,12 +263,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, Acc*
       } break;
       case MJX_RW_POSE: {  // rewards.py:291-359 (p0 walking, p1 running threshold)
         const float speed = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) + fabsf(cmd[2]);
-        const float* std = speed < p0 ? t.std_standing : (speed < p1 ? t.std_walking : t.std_running);
-        float s = 0.f;
-        for (int j = 0; j < nj; j++) {
-          float d = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j];
-          s += d * d / (std[j] * std[j]);
-        }
+        const float s = js.pose[speed < p0 ? 0 : (speed < p1 ? 1 : 2)];
         f = expf(-s / (float)nj);
       } break;
       case MJX_RW_BODY_ANG_VEL: {  // rewards.py:98-107
@@ -233,18 +276,8 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, Acc*
         atomicAdd(&acc->metric_sum[MJX_MT_ANGMOM], sqrtf(f));
         atomicAdd(&acc->metric_cnt[MJX_MT_ANGMOM], 1.f);
       } break;
-      case MJX_RW_JOINT_POS_LIMITS: {  // envs/mdp/rewards.py:73-88
-        for (int j = 0; j < nj; j++) {
-          float q = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
-          f += fmaxf(t.soft_lo[j] - q, 0.f) + fmaxf(q - t.soft_hi[j], 0.f);
-        }
-      } break;
-      case MJX_RW_ACTION_RATE: {  // envs/mdp/rewards.py:56-60
-        for (int j = 0; j < nj; j++) {
-          float d = t.action[(size_t)e * nj + j] - t.prev_action[(size_t)e * nj + j];
-          f += d * d;
-        }
-      } break;
+      case MJX_RW_JOINT_POS_LIMITS: f = js.lim; break;  // envs/mdp/rewards.py:73-88
+      case MJX_RW_ACTION_RATE: f = js.rate; break;       // envs/mdp/rewards.py:56-60
       case MJX_RW_FEET_AIR_TIME: {  // rewards.py:123-152 (p0 min, p1 max, p2 cmd thr)
         float in_air_t = 0.f, in_air_n = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
@@ -317,38 +350,63 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, Acc*
     }
     float v = f * w * dt;
     if (!isfinite(v)) v = 0.f;  // nan_to_num
-    total += v;
+    total = v;
     float* es = t.episode_sums + (size_t)k * t.nworld + e;
-    *es += v;
+    const float es_new = *es + v;
     *sr = v / dt;
+    // ---- reset bookkeeping of this step's resets (reward manager log)
+    if (reset) {
+      atomicAdd(&acc->reward[k], es_new);
+      *es = 0.f;
+    } else {
+      *es = es_new;
+    }
+  } while (0);
+  // reward total in term order (sequential, as the reference's per-term accumulation)
+  {
+    float tot = 0.f;
+    for (int k = 0; k < t.nreward; k++) tot += __shfl(total, k);
+    if (lane == 0) t.reward_buf[e] = tot;
   }
-  t.reward_buf[e] = total;
-  // ---- reset bookkeeping of this step's resets (reward/termination/command manager logs)
-  if (reset) {
-    atomicAdd(&acc->count, 1.f);
-    for (int k = 0; k < t.nreward; k++) {
+  // zero-weight terms still hand their (unchanged) episode sums to the log on reset
+  for (int k = lane; k < t.nreward; k += 64) {
+    if (reset && t.reward_weight[k] == 0.f) {
       float* es = t.episode_sums + (size_t)k * t.nworld + e;
       atomicAdd(&acc->reward[k], *es);
       *es = 0.f;
     }
-    for (int k = 0; k < t.ntermination; k++)
-      if (t.term_dones[(size_t)k * t.nworld + e]) atomicAdd(&acc->term[k], 1.f);
-    atomicAdd(&acc->cmd[0], t.metric_err_xy[e]);
-    atomicAdd(&acc->cmd[1], t.metric_err_yaw[e]);
-    t.metric_err_xy[e] = 0.f;
-    t.metric_err_yaw[e] = 0.f;
+  }
+  // ---- reset bookkeeping (termination/command manager logs)
+  if (reset) {
+    if (lane < t.ntermination && tm_v) atomicAdd(&acc->term[lane], 1.f);
+    if (lane == 0) {
+      atomicAdd(&acc->count, 1.f);
+      atomicAdd(&acc->cmd[0], t.metric_err_xy[e]);
+      atomicAdd(&acc->cmd[1], t.metric_err_yaw[e]);
+      t.metric_err_xy[e] = 0.f;
+      t.metric_err_yaw[e] = 0.f;
+    }
   }
 }
 
-__global__ void k_post(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
+// Wave per env (kPostEnvs envs per block): the joint sums run lane-parallel, the rest of
+// the env's terms on lane 0.  Accumulators: block LDS copy, one global atomic per field
+// and block.
+constexpr int kPostEnvs = 16;
+__global__ __launch_bounds__(64 * kPostEnvs) void k_post(const mjxTaskDesc* __restrict__ T,
+                                                        Acc* __restrict__ acc) {
   const mjxTaskDesc& t = *T;
   __shared__ Acc sh;
   float* shf = reinterpret_cast<float*>(&sh);
   constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
   for (int i = threadIdx.x; i < kAccN; i += blockDim.x) shf[i] = 0.f;
   __syncthreads();
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < t.nworld) post_env(t, e, &sh);
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
+  if (e < t.nworld) {
+    const JointSums js = joint_sums(t, e, lane);
+    post_env(t, e, js, lane, &sh);
+  }
   __syncthreads();
   float* gf = reinterpret_cast<float*>(acc);
   for (int i = threadIdx.x; i < kAccN; i += blockDim.x)
@@ -483,41 +541,62 @@ __global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ a
     }
     t.push_time_left[e] = pt;
   }
-  // ---- observations (observation_manager.py:154-208; velocity_env_cfg.py observation terms)
-  const float* sd = t.sensordata + (size_t)e * t.nsensordata;
+}
+
+// ---- observations (observation_manager.py:154-208; velocity_env_cfg.py observation terms),
+// thread per (env, critic element) after k_observe has updated commands and pushes.  Policy
+// element i is the critic's element i (plus noise draw D_NOISE + i); the critic's extras follow.
+__global__ void k_obs(const mjxTaskDesc* __restrict__ T) {
+  const mjxTaskDesc& t = *T;
   const int nj = t.njoint;
-  float* po = t.obs_policy + (size_t)e * t.npolicy;
+  const int nput = 9 + 3 * nj + 3;  // elements shared by the policy and critic groups
+  const int nel = t.critic_extras ? nput + 6 * t.nfeet : nput;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= t.nworld * nel) return;
+  const int e = idx / nel, i = idx - e * nel;
+  const float* sd = t.sensordata + (size_t)e * t.nsensordata;
   float* co = t.obs_critic + (size_t)e * t.ncritic;
-  const bool noisy = t.corrupt_policy != 0;
-  uint32_t dn = D_NOISE;
-  auto put = [&](int& i, float val, float noise) {
+  if (i < nput) {
+    float val, noise = 0.f;
+    if (i < 3) {
+      val = sd[t.imu_lin_vel_adr + i]; noise = t.noise_lin_vel;
+    } else if (i < 6) {
+      val = sd[t.imu_ang_vel_adr + i - 3]; noise = t.noise_ang_vel;
+    } else if (i < 9) {
+      const V3 g = qapply_inv(t.xquat + ((size_t)e * t.nbody + t.root_body) * 4, V3{0.f, 0.f, -1.f});
+      val = i == 6 ? g.x : i == 7 ? g.y : g.z;
+      noise = t.noise_gravity;
+    } else if (i < 9 + nj) {
+      const int j = i - 9;
+      val = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j];
+      noise = t.noise_joint_pos;
+    } else if (i < 9 + 2 * nj) {
+      val = t.qvel[(size_t)e * t.nv + t.joint_v_adr[i - 9 - nj]]; noise = t.noise_joint_vel;
+    } else if (i < 9 + 3 * nj) {
+      val = t.action[(size_t)e * nj + i - 9 - 2 * nj];
+    } else {
+      val = t.command[(size_t)e * 3 + i - 9 - 3 * nj];
+    }
     co[i] = val;
-    po[i] = noisy && noise > 0.f ? val + uniform(-noise, noise, urand(seed, e, step, dn)) : val;
-    dn++;
-    i++;
-  };
-  int i = 0;
-  for (int k = 0; k < 3; k++) put(i, sd[t.imu_lin_vel_adr + k], t.noise_lin_vel);
-  for (int k = 0; k < 3; k++) put(i, sd[t.imu_ang_vel_adr + k], t.noise_ang_vel);
-  put(i, r.grav_b.x, t.noise_gravity);
-  put(i, r.grav_b.y, t.noise_gravity);
-  put(i, r.grav_b.z, t.noise_gravity);
-  for (int j = 0; j < nj; j++)
-    put(i, t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j], t.noise_joint_pos);
-  for (int j = 0; j < nj; j++) put(i, t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]], t.noise_joint_vel);
-  for (int j = 0; j < nj; j++) put(i, t.action[(size_t)e * nj + j], 0.f);
-  for (int k = 0; k < 3; k++) put(i, c[k], 0.f);
-  if (t.critic_extras) {
-    int ic = i;
-    for (int s = 0; s < t.nfeet; s++) co[ic++] = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
-    for (int s = 0; s < t.nfeet; s++) co[ic++] = t.cur_air[(size_t)e * t.nfeet + s];
-    for (int s = 0; s < t.nfeet; s++) co[ic++] = sd[t.feet_found_adr[s]] > 0.f ? 1.f : 0.f;
-    for (int s = 0; s < t.nfeet; s++)
-      for (int k = 0; k < 3; k++) {
-        float fv = sd[t.feet_force_adr[s] + k];
-        co[ic++] = copysignf(log1pf(fabsf(fv)), fv) * (fv != 0.f ? 1.f : 0.f);
-      }
+    const bool noisy = t.corrupt_policy != 0;
+    t.obs_policy[(size_t)e * t.npolicy + i] =
+        noisy && noise > 0.f ? val + uniform(-noise, noise, urand(t.seed, e, *t.step_counter, D_NOISE + i)) : val;
+    return;
   }
+  const int x = i - nput, nf = t.nfeet, s = x % nf, blk = x / nf;
+  float v;
+  if (blk == 0) {
+    v = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
+  } else if (blk == 1) {
+    v = t.cur_air[(size_t)e * nf + s];
+  } else if (blk == 2) {
+    v = sd[t.feet_found_adr[s]] > 0.f ? 1.f : 0.f;
+  } else {  // blocks 3..5: foot s's force, 3 components per foot in foot order
+    const int y = x - 3 * nf, fs = y / 3, k = y % 3;
+    const float fv = sd[t.feet_force_adr[fs] + k];
+    v = copysignf(log1pf(fabsf(fv)), fv) * (fv != 0.f ? 1.f : 0.f);
+  }
+  co[i] = v;
 }
 
 }  // namespace mjxt
@@ -581,11 +660,37 @@ int mjx_task_destroy(mjxTask* t) {
     return 0;                                                                              \
   } while (0)
 
-int mjx_task_action(mjxTask* t, const float* action, void* stream) { TASK_LAUNCH(mjxt::k_action, t->dev, action); }
+int mjx_task_action(mjxTask* t, const float* action, void* stream) {
+  if (!t) return task_fail("null task");
+  const long n = (long)t->nworld * t->host.njoint;
+  hipLaunchKernelGGL(mjxt::k_action, dim3((unsigned)((n + 255) / 256 > 0 ? (n + 255) / 256 : 1)),
+                     dim3(256), 0, (hipStream_t)stream, t->dev, action);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : task_fail(std::string("k_action: ") + hipGetErrorString(e));
+}
 int mjx_task_substep(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_substep, t->dev); }
-int mjx_task_post(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_post, t->dev, t->acc); }
+int mjx_task_post(mjxTask* t, void* stream) {
+  if (!t) return task_fail("null task");
+  hipLaunchKernelGGL(mjxt::k_post, dim3((t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs),
+                     dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream, t->dev, t->acc);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : task_fail(std::string("k_post: ") + hipGetErrorString(e));
+}
 int mjx_task_reset(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_reset, t->dev); }
-int mjx_task_observe(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_observe, t->dev, t->acc); }
+int mjx_task_observe(mjxTask* t, void* stream) {
+  if (!t) return task_fail("null task");
+  const int nj = t->host.njoint;
+  const int nel = 9 + 3 * nj + 3 + (t->host.critic_extras ? 6 * t->host.nfeet : 0);
+  if (nel > t->host.ncritic || 9 + 3 * nj + 3 > t->host.npolicy)
+    return task_fail("observation sizes do not match the velocity task layout");
+  hipLaunchKernelGGL(mjxt::k_observe, dim3((t->nworld + mjxt::kBlock - 1) / mjxt::kBlock),
+                     dim3(mjxt::kBlock), 0, (hipStream_t)stream, t->dev, t->acc);
+  const long n = (long)t->nworld * nel;
+  hipLaunchKernelGGL(mjxt::k_obs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, t->dev);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : task_fail(std::string("k_observe: ") + hipGetErrorString(e));
+}
 
 const char* mjx_task_last_error(void) { return g_task_err.c_str(); }
 
