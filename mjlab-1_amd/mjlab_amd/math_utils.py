@@ -9,7 +9,38 @@ from __future__ import annotations
 import torch
 
 
+_quat_mul_fn = None
+
+
+def _quat_mul_hip(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  """One `mjx_quat_mul` launch (csrc/quat_ops.hip) instead of ~30 strided torch kernels;
+  bit-identical to the torch expression below.  Raises if the HIP library is missing."""
+  global _quat_mul_fn
+  if _quat_mul_fn is None:
+    import ctypes
+    from ._lib import lib
+    f = lib().mjx_quat_mul
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    _quat_mul_fn = f
+  a, b = torch.broadcast_tensors(q1, q2)
+  if a.shape[-1] != 4:
+    raise ValueError(f"quat_mul: last dim must be 4, got {tuple(a.shape)}")
+  # the kernel reads float4 rows: contiguous and 16-byte aligned (a view may start mid-row)
+  a = a.contiguous() if a.data_ptr() % 16 == 0 else a.clone(memory_format=torch.contiguous_format)
+  b = b.contiguous() if b.data_ptr() % 16 == 0 else b.clone(memory_format=torch.contiguous_format)
+  out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+  rc = _quat_mul_fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), out.numel() // 4,
+                    torch.cuda.current_stream(a.device).cuda_stream)
+  if rc != 0:
+    raise RuntimeError(f"mjx_quat_mul failed ({rc})")
+  return out
+
+
 def quat_mul(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  if (q1.is_cuda and q1.dtype == torch.float32 and q2.dtype == torch.float32
+      and q1.device == q2.device):
+    return _quat_mul_hip(q1, q2)
   w1, x1, y1, z1 = q1.unbind(-1)
   w2, x2, y2, z2 = q2.unbind(-1)
   return torch.stack([
