@@ -159,6 +159,7 @@ def main():
   if rank == 0:
     bytes_launch = b_env(m, dec) / dec * args.num_envs
     achieved = bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic = measured_traffic(args.task, args.num_envs, m.nv)
     out = {
       "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
       "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -172,9 +173,15 @@ def main():
                                (", fused HIP managers" if getattr(env, "_fused", None) is not None else ""))},
       "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": achieved / HBM_PEAK_GBS,
-                   "traffic": measured_traffic(args.task, args.num_envs, m.nv),
+                   "traffic": traffic,
                    "kernel": "mjx::step_phase<NR,0|1|2> (one Simulation.step)", "launch_ms": launch_ms,
-                   "bytes_per_launch": bytes_launch},
+                   "bytes_per_launch": bytes_launch,
+                   # the HBM roofline is the north star's pricing; what actually bounds the
+                   # kernel is per-world dependency latency and VALU issue,
+                   # as the measured traffic rate next to the peak shows
+                   "limiter": "latency/VALU issue (not HBM)",
+                   "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9
+                                    if traffic is not None and launch_ms > 0 else None)},
       "cpu_baseline": None,
     }
     if not args.no_cpu_baseline and world == 1:

@@ -136,8 +136,9 @@ int mjx_task_observe(mjxTask* task, void* stream);
 size_t mjx_task_desc_size(void);  /* sizeof(mjxTaskDesc): ABI check for FFI bindings */
 const char* mjx_task_last_error(void);
 
-/* out[i] = q1[i] * q2[i] (wxyz Hamilton product) for n contiguous quaternions, bit-identical
- * to the reference's torch quat_mul (src/mjlab/utils/lab_api/math.py:275).  Pointers are
+/* out[i] = q1[i] * q2[i] (wxyz Hamilton product) for n contiguous quaternions, in the
+ * reference's 8-multiply operation order without FP contraction: bit-identical to its
+ * torch quat_mul (src/mjlab/utils/lab_api/math.py:526-563) in eager mode.  Pointers are
  * device memory, 16-byte aligned.  Returns 0, -1 bad arguments, -2 misaligned, -3 launch. */
 int mjx_quat_mul(const float* q1, const float* q2, float* out, long n, void* stream);
 

@@ -385,6 +385,11 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_INT
   s->dd.stats = (int32_t*)(base + offs[k++].second);
   s->dd.wstats = (int32_t*)(base + offs[k++].second);
+  // per-world engine counters [nworld, 8] (phase C, last substep): [0] contacts found,
+  // [1] rows, [2] contact-overflow / [3] row-overflow / [4] unsupported-pair events
+  // (cumulative), [5] Newton iterations -- a zero-copy view for device-side logging
+  s->fields["engine_counters"] = FieldInfo{s->dd.wstats, false, 8, 1, true, false};
+  s->names.push_back("engine_counters");
   s->dd.prof = (unsigned long long*)(base + offs[k++].second);
   s->stats = s->dd.stats;
   // model fields visible as "model.<name>"

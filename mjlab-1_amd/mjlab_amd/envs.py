@@ -55,6 +55,24 @@ class ManagerBasedRlEnvCfg:
   is_finite_horizon: bool = False
 
 
+def _cfg_fingerprint(v, depth: int = 0):
+  """Hashable snapshot of the plain values in a cfg (dataclass / dict / sequence of
+  scalars); callables, tensors and other objects are skipped (curricula change numbers,
+  not functions)."""
+  if isinstance(v, (bool, int, float, str)) or v is None:
+    return v
+  if depth > 4:
+    return None
+  if isinstance(v, (tuple, list)):
+    return tuple(_cfg_fingerprint(x, depth + 1) for x in v)
+  if isinstance(v, dict):
+    return tuple((k, _cfg_fingerprint(x, depth + 1)) for k, x in v.items())
+  fields = getattr(v, "__dataclass_fields__", None)
+  if fields is not None:
+    return tuple((k, _cfg_fingerprint(getattr(v, k, None), depth + 1)) for k in fields)
+  return None
+
+
 def seed_rng(seed: int) -> None:
   import random
   random.seed(seed)
@@ -164,6 +182,7 @@ class ManagerBasedRlEnv:
       self.obs_buf, rew, term, trunc = self._fused.step(action)
       self.reward_buf, self.reset_terminated, self.reset_time_outs = rew, term, trunc
       self.reset_buf = self._fused.reset_buf
+      self._log_sim_counters(self.extras.setdefault("log", {}))
       return self.obs_buf, rew, term, trunc
     self.action_manager.process_action(action)
     for _ in range(self.cfg.decimation):
@@ -194,13 +213,21 @@ class ManagerBasedRlEnv:
     for mgr in (self.action_manager, self.reward_manager, self.command_manager,
                 self.event_manager, self.termination_manager):
       log.update(mgr.reset_masked(mask))
+    self._log_sim_counters(log)
     self.observation_manager.reset(None)
     self.episode_length_buf.masked_fill_(mask, 0)
 
   def _graph_key(self):
-    if not self.cfg.commands:
-      return ()
-    return tuple(repr(getattr(t.cfg, "ranges", None)) for t in self.command_manager._terms.values())
+    """Everything a curriculum may mutate that the captured step bakes in as a host
+    constant: every field of each command cfg (ranges, and e.g. the jump task's
+    target_height / height_tolerance, `tasks/jump/mdp/curriculums.py:37-70`), and each
+    reward term's weight and scalar params (`curriculums.py:73-97` sets a weight; a
+    zero weight is skipped at capture time).  A change re-records the graph."""
+    cmds = tuple(_cfg_fingerprint(t.cfg) for t in self.command_manager._terms.values()) \
+        if self.cfg.commands else ()
+    rm = self.reward_manager
+    rews = tuple((c.weight, _cfg_fingerprint(c.params)) for c in rm._term_cfgs)
+    return cmds, rews
 
   def enable_graph(self, capture: bool = True, fused: bool = True) -> None:
     """Switch to the sync-free step; with capture=True record it into a HIP graph
@@ -295,7 +322,20 @@ class ManagerBasedRlEnv:
                 self.curriculum_manager, self.command_manager, self.event_manager,
                 self.termination_manager):
       self.extras["log"].update(mgr.reset(env_ids))
+    self._log_sim_counters(self.extras["log"])
     self.episode_length_buf[env_ids] = 0
+
+  def _log_sim_counters(self, log: dict) -> None:
+    """Engine overflow counters (contacts dropped because a world's contacts or rows
+    exceeded its LDS capacity, and unsupported geom pairs), cumulative over all worlds,
+    as device scalars: no host sync."""
+    ev = getattr(self, "_sim_events", None)
+    if ev is None:
+      ev = self._sim_events = torch.zeros(3, dtype=torch.int64, device=self.device)
+    torch.sum(self.sim.engine_counters[:, 2:5], dim=0, out=ev)
+    log["Sim/contact_overflow"] = ev[0]
+    log["Sim/row_overflow"] = ev[1]
+    log["Sim/unsupported_pairs"] = ev[2]
 
   def packed_episode_stats(self) -> torch.Tensor:
     """Episode statistics of the last reset, packed into one fp32 vector (for the

@@ -473,8 +473,11 @@ class FusedVelocityStep:
 
   # ------------------------------------------------------------------ device handle
   def upload(self):
-    """(Re)create the device copy of the descriptor (after a curriculum changed ranges)."""
+    """(Re)create the device copy of the descriptor (after a curriculum changed command
+    ranges or reward weights)."""
     self._set_command_ranges(self._desc, self._cmd_term.cfg)
+    for k, c in enumerate(self.env.reward_manager._term_cfgs):
+      self._desc.reward_weight[k] = float(c.weight)
     if self._task is not None:
       self._L.mjx_task_destroy(self._task)
     h = ctypes.c_void_p()

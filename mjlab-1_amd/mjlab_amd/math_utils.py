@@ -14,7 +14,7 @@ _quat_mul_fn = None
 
 def _quat_mul_hip(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
   """One `mjx_quat_mul` launch (csrc/quat_ops.hip) instead of ~30 strided torch kernels;
-  bit-identical to the torch expression below.  Raises if the HIP library is missing."""
+  bit-identical to the reference expression below.  Raises if the HIP library is missing."""
   global _quat_mul_fn
   if _quat_mul_fn is None:
     import ctypes
@@ -24,8 +24,6 @@ def _quat_mul_hip(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
     f.restype = ctypes.c_int
     _quat_mul_fn = f
   a, b = torch.broadcast_tensors(q1, q2)
-  if a.shape[-1] != 4:
-    raise ValueError(f"quat_mul: last dim must be 4, got {tuple(a.shape)}")
   # the kernel reads float4 rows: contiguous and 16-byte aligned (a view may start mid-row)
   a = a.contiguous() if a.data_ptr() % 16 == 0 else a.clone(memory_format=torch.contiguous_format)
   b = b.contiguous() if b.data_ptr() % 16 == 0 else b.clone(memory_format=torch.contiguous_format)
@@ -38,16 +36,31 @@ def _quat_mul_hip(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
 
 
 def quat_mul(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
+  """`utils/lab_api/math.py:526-563`: the 8-multiply (ww, yy, zz, xx, qq) product, same
+  operation order.  Unlike the reference, inputs broadcast against each other (the
+  reference raises ValueError on any shape mismatch); non-broadcastable shapes and a last
+  dim other than 4 raise ValueError."""
+  try:
+    shape = torch.broadcast_shapes(q1.shape, q2.shape)
+  except RuntimeError as e:
+    raise ValueError(f"Expected input quaternion shape mismatch: {q1.shape} != {q2.shape}.") from e
+  if len(shape) == 0 or shape[-1] != 4:
+    raise ValueError(f"quat_mul: last dim must be 4, got {tuple(shape)}")
   if (q1.is_cuda and q1.dtype == torch.float32 and q2.dtype == torch.float32
       and q1.device == q2.device):
     return _quat_mul_hip(q1, q2)
   w1, x1, y1, z1 = q1.unbind(-1)
   w2, x2, y2, z2 = q2.unbind(-1)
-  return torch.stack([
-    w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
-    w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
-    w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
-    w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], dim=-1)
+  ww = (z1 + x1) * (x2 + y2)
+  yy = (w1 - y1) * (w2 + z2)
+  zz = (w1 + y1) * (w2 - z2)
+  xx = ww + yy + zz
+  qq = 0.5 * (xx + (z1 - x1) * (x2 - y2))
+  w = qq - ww + (z1 - y1) * (y2 - z2)
+  x = qq - xx + (x1 + w1) * (x2 + w2)
+  y = qq - yy + (w1 - x1) * (y2 + z2)
+  z = qq - zz + (z1 + y1) * (w2 - x2)
+  return torch.stack([w, x, y, z], dim=-1)
 
 
 def quat_apply(quat: torch.Tensor, vec: torch.Tensor) -> torch.Tensor:

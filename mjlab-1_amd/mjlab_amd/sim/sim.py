@@ -103,6 +103,24 @@ def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   return ncon, rows
 
 
+_capacity_warned: set = set()
+
+
+def _warn_capacity(cfg: SimulationCfg, ncon: int, rows: int) -> None:
+  """Warn once per distinct clamp: a world whose contacts or rows overflow the LDS
+  capacity drops whole contacts (counted in `engine_counters`, `stats()` and the env's
+  extras["log"]["Sim/..."] entries)."""
+  asked = (cfg.nconmax, cfg.njmax)
+  if (cfg.njmax is not None and cfg.njmax > rows) and asked not in _capacity_warned:
+    _capacity_warned.add(asked)
+    import warnings
+    warnings.warn(
+        f"mjlab_amd.Simulation: njmax={cfg.njmax} clamped to {rows} constraint rows per world "
+        f"(nconmax {cfg.nconmax} -> {ncon} contacts per world held in LDS); contacts beyond "
+        "that are dropped whole and counted as row/contact overflow events",
+        RuntimeWarning, stacklevel=3)
+
+
 class Simulation:
   """GPU-batched MuJoCo physics on MI355X (see module docstring)."""
 
@@ -126,6 +144,7 @@ class Simulation:
                              ctypes.byref(self._model_ptr)))
     del keep
     self.nconmax, self.njmax = world_capacity(cfg, model)
+    _warn_capacity(cfg, self.nconmax, self.njmax)
     self._sim = ctypes.c_void_p()
     check(L.mjx_sim_create(self._model_ptr, self.num_envs, self.nconmax, self.njmax,
                            ctypes.byref(self._sim)))
@@ -255,6 +274,18 @@ class Simulation:
     self._reset_mask.fill_(0)
     self._reset_mask[env_ids] = 1
     check(lib().mjx_reset(self._sim, ctypes.c_void_p(self._reset_mask.data_ptr()), stream))
+
+  @property
+  def engine_counters(self) -> torch.Tensor:
+    """[nworld, 8] int32 device view: [0] contacts, [1] constraint rows, [2] contact
+    overflow, [3] row overflow, [4] unsupported-pair events (cumulative), [5] Newton
+    iterations.  No host sync (stats() is the synchronising summary)."""
+    return self.field("engine_counters")
+
+  def overflow_events(self) -> torch.Tensor:
+    """Device [3] tensor: total contact-overflow, row-overflow and unsupported-pair
+    events over all worlds since creation (no host sync)."""
+    return self.engine_counters[:, 2:5].sum(dim=0)
 
   def stats(self) -> dict:
     """Engine counters: max contacts/rows seen, overflow and unsupported-pair events."""

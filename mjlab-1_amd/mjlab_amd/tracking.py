@@ -117,10 +117,20 @@ def synthesize_motion(scene_name: str = "g1_tracking", device: str = "cuda:0", T
 
 
 def write_motion_npz(path: str, motion: dict) -> None:
-  os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-  tmp = path + ".tmp.npz"
-  np.savez(tmp, **motion)
-  os.replace(tmp, path)
+  """Atomic publish: each process writes its own temp file in the target directory, then
+  renames it over `path` (ranks racing on a fresh checkout each publish a whole file)."""
+  import tempfile
+  d = os.path.dirname(path) or "."
+  os.makedirs(d, exist_ok=True)
+  fd, tmp = tempfile.mkstemp(dir=d, prefix=".motion-", suffix=".npz")
+  try:
+    with os.fdopen(fd, "wb") as f:
+      np.savez(f, **motion)
+    os.replace(tmp, path)
+  except BaseException:
+    if os.path.exists(tmp):
+      os.remove(tmp)
+    raise
 
 
 def ensure_synthetic_motion(path: str = SYNTHETIC_G1_MOTION, device: str = "cuda:0") -> str:

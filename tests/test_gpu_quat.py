@@ -1,6 +1,6 @@
 """`mjx_quat_mul` (csrc/quat_ops.hip) against the torch expression of the reference's
-quat_mul (src/mjlab/utils/lab_api/math.py:275): bit-identical, with broadcasting,
-misaligned views and the empty batch."""
+quat_mul (src/mjlab/utils/lab_api/math.py:526-563, the 8-multiply form, restated below in
+eager torch): bit-identical, with broadcasting, misaligned views and the empty batch."""
 
 import pytest
 import torch
@@ -9,6 +9,19 @@ pytestmark = pytest.mark.gpu
 
 
 def _torch_quat_mul(q1, q2):
+  q1, q2 = torch.broadcast_tensors(q1, q2)
+  w1, x1, y1, z1 = q1.unbind(-1)
+  w2, x2, y2, z2 = q2.unbind(-1)
+  ww = (z1 + x1) * (x2 + y2)
+  yy = (w1 - y1) * (w2 + z2)
+  zz = (w1 + y1) * (w2 - z2)
+  xx = ww + yy + zz
+  qq = 0.5 * (xx + (z1 - x1) * (x2 - y2))
+  return torch.stack([qq - ww + (z1 - y1) * (y2 - z2), qq - xx + (x1 + w1) * (x2 + w2),
+                      qq - yy + (w1 - x1) * (y2 + z2), qq - zz + (z1 + y1) * (w2 - x2)], dim=-1)
+
+
+def _hamilton(q1, q2):
   w1, x1, y1, z1 = q1.unbind(-1)
   w2, x2, y2, z2 = q2.unbind(-1)
   return torch.stack([
@@ -28,6 +41,8 @@ def test_quat_mul_bit_identical(gpu_device):
   c = a[:, :1, :]
   assert torch.equal(quat_mul(c, b), _torch_quat_mul(c, b))
   assert torch.equal(quat_mul(b, c.expand(-1, 37, -1)), _torch_quat_mul(b, c))
+  # and it is the Hamilton product (to rounding)
+  torch.testing.assert_close(quat_mul(a, b), _hamilton(a, b), rtol=1e-4, atol=1e-4)
 
 
 def test_quat_mul_misaligned_and_empty(gpu_device):
