@@ -147,6 +147,11 @@ int mjx_field_is_expanded(const mjxSim* sim, const char* name);
 int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);
 /* Diagnostics: per-stage cycle sums uint64[48] (non-zero only in the -DMJX_STAMPS build). */
 int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
+/* Which step kernels the sim launches: k > 0 = kernels compiled for entry k of
+ * csrc/specs.inc (the sim's dims, nconmax and njmax equal that entry), 0 = the generic
+ * kernels; -1 for a null sim.  No reference counterpart (mujoco_warp specialises by
+ * tracing Python at graph-capture time, sim/sim.py:164-191). */
+int mjx_sim_spec(const mjxSim* sim);
 
 #ifdef __cplusplus
 }

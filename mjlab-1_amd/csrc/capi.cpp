@@ -82,6 +82,7 @@ struct mjxSim_ {
   mjx::Lds lds_ph[3 + mjx::kRowClasses];  // per-phase LDS carves ([3 + k]: Newton row class k)
   int nrowclass = 0;
   int row_cap[mjx::kRowClasses] = {};
+  int spec = 0;  // model specialisation in use (mjx::find_spec), 0 = generic kernels
   mjx::SideStream side{};  // streams of the Newton row classes (when classes are used)
   ~mjxSim_() {
     if (side.fork) (void)hipEventDestroy(side.fork);
@@ -113,6 +114,7 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.gC = s->gC;
   p.gF = s->gF;
   p.gstride = s->gstride;
+  p.spec = s->spec;
   return p;
 }
 
@@ -324,7 +326,8 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
   }
-  s->nrowclass = mjx::choose_row_classes(s->d, s->row_cap);
+  s->spec = mjx::find_spec(s->d);
+  s->nrowclass = mjx::choose_row_classes(s->d, s->spec, s->row_cap);
   for (int k = 0; k < mjx::kRowClasses; k++) {
     mjx::Dims ds = s->d;
     ds.njmax = k < s->nrowclass ? s->row_cap[k] : s->d.njmax;
@@ -563,6 +566,8 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }
+
+int mjx_sim_spec(const mjxSim* s) { return s ? s->spec : -1; }
 
 int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {
   if (!s || !out) return fail("null argument");

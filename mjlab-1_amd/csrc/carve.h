@@ -1,0 +1,114 @@
+// carve.h — per-phase LDS carves of the step kernels (offsets in 4-byte words).
+//
+// constexpr so that the model-specialised kernels (specs.inc) get every LDS offset as a
+// compile-time immediate; the generic kernels and the host use the same function at run
+// time.  Included by engine.h after the Dims / Lds definitions.
+#pragma once
+
+#include <initializer_list>
+#include <utility>
+
+namespace mjx {
+
+// Phase carves.  Masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4
+// (post/integrate).  A phase carve holds only the regions that phase touches (the rest sit
+// past the allocation and are never accessed).  Phase inputs are carved FIRST, in a fixed
+// order, so the per-world global scratch holds them as one contiguous "pack" with the same
+// internal offsets: B pack = [ints M qacc_smooth qfrc_smooth efc_aref efc_D efc_J] (J last,
+// so only the live rows are copied), C pack = [A outputs | B outputs].  Each phase then
+// fills its inputs with a single bulk copy.
+constexpr Lds make_lds(const Dims& d, int ph) {
+  Lds L{};
+  const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
+  constexpr int A = 1, B = 2, Cp = 4;
+  struct Slot { int Lds::*f; int n; int mask; };
+  const Slot all[] = {
+    {&Lds::ints, 8, A | B | Cp},
+    {&Lds::qpos, d.nq, A | Cp}, {&Lds::qvel, nv, A | Cp}, {&Lds::ctrl, d.nu, A},
+    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, A}, {&Lds::xfrc, 6 * nb, 0},  // xfrc read from HBM (rare)
+    {&Lds::xpos, 3 * nb, A}, {&Lds::xquat, 4 * nb, A}, {&Lds::xmat, 9 * nb, A},
+    {&Lds::xipos, 3 * nb, A}, {&Lds::ximat, 9 * nb, A}, {&Lds::xanchor, 3 * d.njnt, A},
+    {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, A}, {&Lds::subtree_com, 3 * nb, A | Cp},
+    {&Lds::cinert, 10 * nb, A}, {&Lds::crb, 10 * nb, A}, {&Lds::cvel, 6 * nb, A | Cp},
+    {&Lds::cacc, 6 * nb, A | Cp}, {&Lds::stlin, 3 * nb, A}, {&Lds::stang, 3 * nb, A},
+    {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
+    {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
+    {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
+    {&Lds::M, nv * nv, A | B}, {&Lds::H, nv * nv, A | B},
+    {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
+    {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
+    {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
+    {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
+    {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
+    {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
+    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, A | Cp},
+    {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_kb, 2 * C, A}, {&Lds::con_imp, C, A},
+    {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
+    {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
+    {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
+    {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
+    {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, 0},
+    {&Lds::red, 5 * kWave, B},
+  };
+  int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
+                                     &Lds::efc_aref, &Lds::efc_D, &Lds::efc_J};
+  int Lds::* const packC[] = {
+      &Lds::cdof, &Lds::cdofdot, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
+      &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
+      &Lds::con_frame, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
+      // written by phase B:
+      &Lds::ints, &Lds::x, &Lds::qfrc_con, &Lds::efc_force};
+  constexpr int kAbsent = 1 << 24;
+  for (const Slot& sp : all) L.*(sp.f) = kAbsent;
+  int o = 0;
+  auto take = [&](int Lds::*f) {
+    if (L.*f != kAbsent) return;
+    for (const Slot& sp : all)
+      if (sp.f == f) { L.*f = o; o += (sp.n + 3) & ~3; return; }  // 16-B aligned carve
+  };
+  if (ph == 1) for (auto f : packB) take(f);
+  if (ph == 2) for (auto f : packC) take(f);
+  L.pack_len = o;
+  L.packC_b = ph == 2 ? L.ints : 0;  // start of the phase-B-written part of the C pack
+  if (ph == 1) {
+    // Phase B holds M in register tiles for the whole solve (tiles_symv), so M's pack slot
+    // is reused as the Cholesky staging area H and as jt_mul's partial sums; the line-search
+    // direction J s reuses efc_aref (only read by the warmstart).
+    L.H = L.M;
+    L.red = L.M;
+    L.efc_Js = L.efc_aref;
+  }
+  if (ph == 0) {
+    // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
+    // collision, contacts, rows.  Two aliases follow from it:
+    //  - M and H (the smooth solve's in-place factor) live in the contact/row block, which
+    //    is first written by collision, after the smooth solve;
+    //  - geom frames (computed at the start of collision) live in [cinert crb cacc
+    //    xanchor xaxis], all dead once RNE has run.
+    auto group = [&](std::initializer_list<int Lds::*> fs) {
+      const int start = o;
+      for (auto f : fs) take(f);
+      return std::make_pair(start, o - start);
+    };
+    auto g1 = group({&Lds::con_g1, &Lds::con_g2, &Lds::con_key, &Lds::con_dist, &Lds::con_pos,
+                     &Lds::con_frame, &Lds::con_mu, &Lds::con_kb, &Lds::con_imp,
+                     &Lds::con_imargin, &Lds::con_dim, &Lds::con_efc, &Lds::efc_aref, &Lds::efc_D,
+                     &Lds::efc_cid});
+    // M (assembled after CRB, copied to the B/C packs at once, factored in place by the
+    // smooth solve) is dead before collision: M and H share the contact/row block too.
+    if (g1.second >= nv * nv) L.M = L.H = g1.first;
+    auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc, &Lds::xanchor, &Lds::xaxis});
+    const int gp = (3 * d.ngeom_lds + 3) & ~3;
+    if (g2.second >= gp + 9 * d.ngeom_lds) {
+      L.gxpos = g2.first;
+      L.gxmat = g2.first + gp;
+    }
+  }
+  const int bit = 1 << ph;
+  for (const Slot& sp : all)
+    if (sp.mask & bit) take(sp.f);
+  L.total = o;
+  return L;
+}
+
+}  // namespace mjx

@@ -88,7 +88,15 @@ struct Lds {
   int total;
 };
 
-Lds make_lds(const Dims& d, int phase);  // phase 0/1/2 = A/B/C
+}  // namespace mjx
+#include "carve.h"  // constexpr Lds make_lds(const Dims& d, int phase): phase 0/1/2 = A/B/C
+namespace mjx {
+
+// Model specialisation: 0 = generic kernels (dims and carves read from Params at run
+// time), k > 0 = kernels compiled for the k-th entry of specs.inc (dims and carves are
+// compile-time constants).  find_spec returns the entry equal to d in every field, else 0.
+constexpr int kMaxSpecs = 8;
+int find_spec(const Dims& d);
 
 // Everything a launch needs, resident in device memory (read through the scalar cache
 // instead of occupying ~500 SGPRs of kernarg space).
@@ -108,6 +116,7 @@ struct Params {
   int gF;        // offset of F: the implicit-integration factor (nvp x nvp rows), read by
                  // phase C straight from global memory (not staged in LDS)
   int gstride;
+  int spec;      // model specialisation (find_spec) whose kernels launch_step uses
 };
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
@@ -123,7 +132,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side);
 // Newton row classes (capacities ascending into caps[]); returns how many are used.
-int choose_row_classes(const Dims& d, int (&caps)[kRowClasses]);
+int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
                         int nworld, hipStream_t stream);
 

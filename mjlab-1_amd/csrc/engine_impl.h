@@ -1,0 +1,2506 @@
+#pragma once
+// engine_impl.h — the step kernels of the batched mj_step for MI355X (gfx950): one
+// wavefront (64 lanes) per world.  Included by engine.hip (generic kernels) and by
+// spec.hip (one translation unit per model specialisation of specs.inc).
+//
+// Each workgroup is ONE wave that owns ONE world.  The world's state and every
+// intermediate (body frames, com-based inertias, mass matrix, contacts, dense
+// constraint Jacobian, Newton Hessian) lives in that workgroup's LDS for the whole
+// step, so HBM sees only the coalesced load of the state at the start and the
+// coalesced store of state + API-visible kinematics at the end (the "algorithmic
+// bytes" of DESIGN.md section 4).  Stages map to lanes as:
+//   tree recursions  -> one lane per body of the current tree level (level-synchronous)
+//   dof stages       -> one lane per dof (M rows, Jacobian columns, J^T f)
+//   broad+narrowphase-> one lane per candidate geom pair, LDS-atomic append, then a
+//                       64-lane bitonic sort on (pair, sub-contact) so contact order is
+//                       deterministic and equals the CPU oracle's pair order
+//   constraint rows  -> one lane per row
+//   Cholesky / H     -> one lane per lower-triangle element (right-looking, in LDS)
+// Semantics follow the reference's mujoco_warp.step (src/mjlab/sim/sim.py:267-273)
+// stage by stage, restated in oracle/oracle.c (the parity checker).
+#include <float.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <initializer_list>
+#include <utility>
+#include <math.h>
+
+#include "engine.h"
+
+namespace mjx {
+
+#define MINVAL 1e-15f
+#define MINMU 1e-5f
+#define MINIMP 0.0001f
+#define MAXIMP 0.9999f
+
+enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
+enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
+enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum { SENS_GYRO = 0, SENS_VELOCIMETER = 1, SENS_ACCELEROMETER = 2, SENS_SUBTREEANGMOM = 3,
+       SENS_CONTACT = 4, SENS_FRAMEPOS = 5, SENS_FRAMEQUAT = 6, SENS_JOINTPOS = 7,
+       SENS_JOINTVEL = 8 };
+enum { OBJ_SITE = 6 };
+enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
+
+// --------------------------------------------------------------------------- device math
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(const float* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ void st3(float* p, V3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float norm(V3 a) { return sqrtf(dot(a, a)); }
+// row-major 3x3
+__device__ __forceinline__ V3 mulv(const float* M, V3 v) {
+  return {M[0] * v.x + M[1] * v.y + M[2] * v.z, M[3] * v.x + M[4] * v.y + M[5] * v.z,
+          M[6] * v.x + M[7] * v.y + M[8] * v.z};
+}
+__device__ __forceinline__ V3 mulTv(const float* M, V3 v) {
+  return {M[0] * v.x + M[3] * v.y + M[6] * v.z, M[1] * v.x + M[4] * v.y + M[7] * v.z,
+          M[2] * v.x + M[5] * v.y + M[8] * v.z};
+}
+__device__ __forceinline__ void mat3mul(float* R, const float* A, const float* B) {
+  float t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) R[i] = t[i];
+}
+struct Q4 { float w, x, y, z; };
+__device__ __forceinline__ Q4 q4(const float* p) { return {p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ void st4(float* p, Q4 q) { p[0] = q.w; p[1] = q.x; p[2] = q.y; p[3] = q.z; }
+__device__ __forceinline__ Q4 qmul(Q4 a, Q4 b) {
+  return {a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+          a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x, a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w};
+}
+__device__ __forceinline__ Q4 qnorm(Q4 q) {
+  float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  if (n < MINVAL) return {1, 0, 0, 0};
+  float s = 1.0f / n;
+  return {q.w * s, q.x * s, q.y * s, q.z * s};
+}
+__device__ __forceinline__ void qmat(float* M, Q4 q) {
+  q = qnorm(q);
+  float w = q.w, x = q.x, y = q.y, z = q.z;
+  M[0] = 1 - 2 * (y * y + z * z); M[1] = 2 * (x * y - w * z); M[2] = 2 * (x * z + w * y);
+  M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
+  M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ Q4 qaxisangle(V3 a, float ang) {
+  float s = sinf(0.5f * ang);
+  return {cosf(0.5f * ang), a.x * s, a.y * s, a.z * s};
+}
+// spatial algebra, vectors [ang; lin]
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* s) {
+  V3 w = v3(v), u = v3(v + 3), a = v3(s), b = v3(s + 3);
+  st3(r, cross(w, a));
+  st3(r + 3, cross(w, b) + cross(u, a));
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  V3 w = v3(v), u = v3(v + 3), a = v3(f), b = v3(f + 3);
+  st3(r, cross(w, a) + cross(u, b));
+  st3(r + 3, cross(w, b));
+}
+__device__ __forceinline__ void inert_mul(float* r, const float* I, const float* v) {
+  V3 w = v3(v), u = v3(v + 3), h = v3(I + 6);
+  float m = I[9];
+  V3 t = {I[0] * w.x + I[3] * w.y + I[4] * w.z, I[3] * w.x + I[1] * w.y + I[5] * w.z,
+          I[4] * w.x + I[5] * w.y + I[2] * w.z};
+  st3(r, t + cross(h, u));
+  st3(r + 3, u * m - cross(h, w));
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// --------------------------------------------------------------------------- wave utils
+// Full-wave float sum, result wave-uniform.  DPP within each 16-lane row (quad swaps,
+// half-row and row mirrors), then the four row totals via v_readlane: no LDS crossbar
+// round trips (a __shfl_xor chain costs six ds_swizzle latencies).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+}
+// min / max over the wave (same DPP pattern as wave_sum; all lanes must be active)
+__device__ __forceinline__ float wave_min(float v) {
+  v = fminf(v, dpp<0xB1>(v));
+  v = fminf(v, dpp<0x4E>(v));
+  v = fminf(v, dpp<0x141>(v));
+  v = fminf(v, dpp<0x140>(v));
+  const auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return fminf(fminf(rl(0), rl(16)), fminf(rl(32), rl(48)));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  const auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return fmaxf(fmaxf(rl(0), rl(16)), fmaxf(rl(32), rl(48)));
+}
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  *total = __shfl(x, kWave - 1);
+  return x - v;
+}
+// A workgroup is exactly one wavefront and LDS operations of a wavefront execute in
+// issue order, so cross-lane LDS hand-offs need only a compiler barrier (no s_barrier,
+// no lgkmcnt drain).  MJX_SYNCTHREADS=1 restores __syncthreads() for A/B checks.
+#ifndef MJX_SYNCTHREADS
+__device__ __forceinline__ void sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+#else
+__device__ __forceinline__ void sync() { __syncthreads(); }
+#endif
+
+#define MF(f) (m.f + (size_t)w * m.f##_ws)
+
+// Diagnostic build only (-DMJX_STAMPS): per-stage s_memtime deltas, accumulated in
+// registers and added to D.prof once per wave at kernel end (STAMP_FLUSH) -- per-stamp global
+// atomics sit in vmcnt and would charge their contention to the next memory wait.
+#ifdef MJX_STAMPS
+#define STAMP(k)                                                                 \
+  do {                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+    stamp_acc[k] += t_ - stamp_prev;                                             \
+    stamp_prev = t_;                                                             \
+  } while (0)
+// SUBSTAMP(k): nested split of the Newton stage into slots 16+ (does not advance STAMP).
+#define SUBSTAMP(k)                                                              \
+  do {                                                                           \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                          \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+    stamp_acc[16 + (k)] += t_ - sub_prev;                                        \
+    sub_prev = t_;                                                               \
+  } while (0)
+#define STAMP_FLUSH()                                                            \
+  do {                                                                           \
+    if (lane == 0)                                                               \
+      for (int k_ = 0; k_ < 48; k_++)                                            \
+        if (stamp_acc[k_]) atomicAdd((unsigned long long*)&D.prof[k_], stamp_acc[k_]); \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#define SUBSTAMP(k) do {} while (0)
+#define STAMP_FLUSH() do {} while (0)
+#endif
+
+// --------------------------------------------------------------------------- tiled SPD algebra
+// The nv x nv SPD systems (mass matrix, Newton Hessian, implicit-integration matrix) are
+// padded to NVP = 4*ceil(nv/4) and split into 4x4 tiles of the lower triangle; lane l owns
+// tiles l and l+64 (at most 2, so NVP <= 60).  Tiles live in registers through assembly
+// and factorization; the Cholesky factor is published to LDS (row stride NVP) for the
+// triangular solves.  Padding rows/cols are identity, so padded unknowns solve to 0.
+struct Tiles {
+  int nb, ntile;
+  int bi[2], bj[2];
+  bool own[2];
+};
+__device__ __forceinline__ Tiles make_tiles(int nvp, int lane) {
+  Tiles t;
+  t.nb = nvp >> 2;
+  t.ntile = t.nb * (t.nb + 1) / 2;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    int idx = lane + kWave * s;
+    t.own[s] = idx < t.ntile;
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= idx) bi++;
+    t.bi[s] = bi;
+    t.bj[s] = idx - bi * (bi + 1) / 2;
+  }
+  return t;
+}
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4v(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ void tiles_load(float (&A)[2][16], const Tiles& T, const float* Mm, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float4 v = ld4(Mm + (4 * T.bi[s] + r) * nvp + 4 * T.bj[s]);
+      A[s][4 * r + 0] = v.x; A[s][4 * r + 1] = v.y; A[s][4 * r + 2] = v.z; A[s][4 * r + 3] = v.w;
+    }
+  }
+}
+// A += sum_k D[act[k]] * J[act[k], iblock]^T J[act[k], jblock]
+__device__ __forceinline__ void tiles_add_jtdj(float (&A)[2][16], const Tiles& T, const float* J,
+                                               const float* Dv, const int* act, int nact, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+    const int oi = 4 * T.bi[s], oj = 4 * T.bj[s];
+    int k = 0;
+    for (; k + 1 < nact; k += 2) {
+      int r0 = act[k], r1 = act[k + 1];
+      float4 a0 = ld4(J + r0 * nvp + oi), b0 = ld4(J + r0 * nvp + oj);
+      float4 a1 = ld4(J + r1 * nvp + oi), b1 = ld4(J + r1 * nvp + oj);
+      float d0 = Dv[r0], d1 = Dv[r1];
+      float ai0[4] = {a0.x, a0.y, a0.z, a0.w}, bj0[4] = {b0.x * d0, b0.y * d0, b0.z * d0, b0.w * d0};
+      float ai1[4] = {a1.x, a1.y, a1.z, a1.w}, bj1[4] = {b1.x * d1, b1.y * d1, b1.z * d1, b1.w * d1};
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) A[s][4 * r + c] += ai0[r] * bj0[c] + ai1[r] * bj1[c];
+    }
+    if (k < nact) {
+      int r0 = act[k];
+      float4 a0 = ld4(J + r0 * nvp + oi), b0 = ld4(J + r0 * nvp + oj);
+      float d0 = Dv[r0];
+      float ai0[4] = {a0.x, a0.y, a0.z, a0.w}, bj0[4] = {b0.x * d0, b0.y * d0, b0.z * d0, b0.w * d0};
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) A[s][4 * r + c] += ai0[r] * bj0[c];
+    }
+  }
+}
+// out[i] = Mm[i,:] . v for i < nrow (row stride nvp), v broadcast-read as float4.
+__device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const float* v, int nrow,
+                                            int nvp, int lane) {
+  const int nb = nvp >> 2;
+  for (int i = lane; i < nrow; i += kWave) {
+    const float* row = Mm + i * nvp;
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    for (; k + 1 < nb; k += 2) {
+      float4 a = ld4(row + 4 * k), b = ld4(v + 4 * k);
+      float4 c = ld4(row + 4 * k + 4), e = ld4(v + 4 * k + 4);
+      s0 += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+      s1 += c.x * e.x + c.y * e.y + c.z * e.z + c.w * e.w;
+    }
+    if (k < nb) {
+      float4 a = ld4(row + 4 * k), b = ld4(v + 4 * k);
+      s0 += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    }
+    out[i] = s0 + s1;
+  }
+}
+// out[c] = sum_k J[act[k], c] * wv[act[k]] (c < nvp).  Lanes split (column block, row
+// group); partial sums reduced through `part` (>= 64*4 floats).  Ends with a sync.
+__device__ __forceinline__ void jt_mul(float* out, const float* J, const float* wv, const int* act, int nact,
+                       int nvp, int lane) {
+  // lane = g * nb + cb: column block cb (4 columns) summed over the rows k = g (mod ng),
+  // then the ng group partials are folded by a fixed shuffle tree (no LDS scratch, so the
+  // Newton factor in the H slot survives across iterations)
+  const int nb = nvp >> 2;
+  const int ng = kWave / nb;
+  const int cb = lane % nb, g = lane / nb;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < ng) {
+    for (int k = g; k < nact; k += ng) {
+      int r = act[k];
+      float4 j = ld4(J + r * nvp + 4 * cb);
+      float wr = wv[r];
+      acc.x += j.x * wr; acc.y += j.y * wr; acc.z += j.z * wr; acc.w += j.w * wr;
+    }
+  }
+  for (int off = 1; off < ng; off <<= 1) {
+    const int src = min(lane + off * nb, kWave - 1);
+    const bool take = g + off < ng;
+    const float x = __shfl(acc.x, src), y = __shfl(acc.y, src);
+    const float z = __shfl(acc.z, src), w = __shfl(acc.w, src);
+    if (take) { acc.x += x; acc.y += y; acc.z += z; acc.w += w; }
+  }
+  if (g == 0) st4v(out + 4 * cb, acc);
+  sync();
+}
+// Compact the rows with jar < 0 into act[]; returns the count (wave-uniform).  sig holds
+// the active set of the previous call as 64-row ballots; *same is set when it is unchanged
+// (then H = M + J_act^T D J_act is unchanged too).  Sets over 4*64 rows never compare same.
+__device__ __forceinline__ int build_active(int* act, const float* jar, int nefc, int lane,
+                                            unsigned long long (&sig)[4], bool* same) {
+  int base = 0;
+  bool eq = nefc <= 4 * kWave;
+  for (int r0 = 0, k = 0; r0 < nefc; r0 += kWave, k++) {
+    int r = r0 + lane;
+    bool f = r < nefc && jar[r] < 0.f;
+    unsigned long long bal = __ballot(f);
+    if (f) act[base + __popcll(bal & ((1ull << lane) - 1ull))] = r;
+    base += __popcll(bal);
+    if (k < 4) {
+      eq = eq && bal == sig[k];
+      sig[k] = bal;
+    }
+  }
+  *same = eq;
+  return base;
+}
+
+// --------------------------------------------------------------------------- register-row SPD
+// Lane i holds row i of an nvp x nvp SPD matrix in NR registers (NR = compile-time row
+// length >= nvp; rows/cols >= nvp are identity).  Cholesky and both triangular solves run
+// as v_readlane broadcast chains: no LDS round trips and no single-lane sections.
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+template <int NR>
+__device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int nvp, int lane) {
+  const int row = lane < nvp ? lane : 0;
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < nvp) v = ld4(Mm + row * nvp + c);
+    A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
+  }
+  if (lane >= nvp) {
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] = c == lane ? 1.f : 0.f;
+  }
+}
+// In-place right-looking Cholesky of the lower triangle: afterwards A[c] (c <= lane) is
+// L[lane][c] and rdiag = 1/L[lane][lane].  Entries above the diagonal are scratch; they
+// never feed the lower part (every broadcast reads a lower entry).
+template <int NR>
+__device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, int nvp, int lane) {
+  rdiag = 1.f;
+  // Padding rows/cols (>= nvp) are identity/zero, so the full NR sweep is exact there:
+  // no per-step guards (guards get hoisted into spilled SGPR masks).
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
+    A[j] *= r;
+    rdiag = lane == j ? r : rdiag;
+    // pairs of broadcasts -> one SGPR pair feeding a packed FMA (v_pk_fma_f32)
+#pragma unroll
+    for (int k = j + 1; k < NR; k += 2) {
+      if (k + 1 < NR) {
+        const float b0 = rl(A[j], k), b1 = rl(A[j], k + 1);
+        A[k] = fmaf(-A[j], b0, A[k]);
+        A[k + 1] = fmaf(-A[j], b1, A[k + 1]);
+      } else {
+        A[k] = fmaf(-A[j], rl(A[j], k), A[k]);
+      }
+    }
+  }
+}
+// Publish L (row stride nvp): strictly-lower part, 1/L[i][i] on the diagonal, zeros above.
+// The solves never let a diagonal entry reach another lane (a lane's own y is dead once it
+// has been broadcast), so rows_solve can run from these rows (rows_load_factor) as well.
+template <int NR>
+__device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float rd, float* Lm, int nvp,
+                                                  int lane) {
+  if (lane >= nvp) return;
+#pragma unroll
+  for (int c = 0; c < NR; c += 4)
+    if (c < nvp)
+      st4v(Lm + lane * nvp + c,
+           make_float4(c < lane ? A[c] : c == lane ? rd : 0.f, c + 1 < lane ? A[c + 1] : c + 1 == lane ? rd : 0.f,
+                       c + 2 < lane ? A[c + 2] : c + 2 == lane ? rd : 0.f,
+                       c + 3 < lane ? A[c + 3] : c + 3 == lane ? rd : 0.f));
+}
+// Rows of a factor stored by rows_store_strict, and this lane's 1/L[i][i].
+template <int NR>
+__device__ __forceinline__ void rows_load_factor(float (&A)[NR], float& rd, const float* Lm, int nvp,
+                                                 int lane) {
+  rows_load<NR>(A, Lm, nvp, lane);
+  rd = lane < nvp ? Lm[lane * nvp + lane] : 1.f;
+}
+// x (lane i holds x[i]) <- (L L^T)^-1 x.  Forward from the register rows, backward from
+// columns of the strictly-lower L in Lm (written by rows_store_strict, then synced).
+template <int NR>
+__device__ __forceinline__ float rows_solve(const float (&A)[NR], float rdiag, const float* Lm,
+                                            float x, int nvp, int lane) {
+  float y = x, out = 0.f;
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const float s = rl(y * rdiag, j);
+    out = lane == j ? s : out;
+    y = fmaf(-(lane > j ? A[j] : 0.f), s, y);
+  }
+  float Lc[NR];
+  const int col = lane < nvp ? lane : 0;
+#pragma unroll
+  for (int j = 0; j < NR; j++) Lc[j] = (j < nvp && lane < nvp) ? Lm[j * nvp + col] : 0.f;
+  y = out;
+  out = 0.f;
+#pragma unroll
+  for (int j = NR - 1; j >= 0; j--) {
+    const float s = rl(y * rdiag, j);
+    out = lane == j ? s : out;
+    y = fmaf(-Lc[j], s, y);
+  }
+  return out;
+}
+// Tiles (lower 4x4 blocks) -> LDS matrix (row stride nvp), for rows_load.
+__device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles& T, float* Mm, int nvp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      st4v(Mm + (4 * T.bi[s] + r) * nvp + 4 * T.bj[s],
+           make_float4(A[s][4 * r], A[s][4 * r + 1], A[s][4 * r + 2], A[s][4 * r + 3]));
+  }
+}
+// out = A v for the symmetric matrix held as lower 4x4 register tiles (diagonal blocks
+// full); each tile contributes its block and, off the diagonal, its transpose, through LDS
+// float atomics.  Ends synced.
+__device__ __forceinline__ void tiles_symv(const float (&A)[2][16], const Tiles& T, const float* v,
+                                           float* out, int nvp, int lane) {
+  for (int i = lane; i < nvp; i += kWave) out[i] = 0.f;
+  sync();
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+    const int bi = T.bi[s], bj = T.bj[s];
+    const float4 vj = ld4(v + 4 * bj);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      atomicAdd(out + 4 * bi + r, A[s][4 * r] * vj.x + A[s][4 * r + 1] * vj.y +
+                                      A[s][4 * r + 2] * vj.z + A[s][4 * r + 3] * vj.w);
+    if (bi != bj) {
+      const float4 vi = ld4(v + 4 * bi);
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        atomicAdd(out + 4 * bj + c, A[s][c] * vi.x + A[s][4 + c] * vi.y + A[s][8 + c] * vi.z +
+                                        A[s][12 + c] * vi.w);
+    }
+  }
+  sync();
+}
+// Factor the nvp x nvp SPD matrix in Mm (row stride nvp) and solve for vector v (LDS,
+// length nvp) in place.  Lm (nvp*nvp) receives the strictly-lower factor.  Lm may alias Mm.
+template <int NR>
+__device__ __forceinline__ void spd_factor_solve(const float* Mm, const float* diag_add, float* Lm,
+                                                 float* v, int nvp, int lane) {
+  float A[NR];
+  rows_load<NR>(A, Mm, nvp, lane);
+  if (diag_add && lane < nvp) {
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] += c == lane ? diag_add[lane] : 0.f;
+  }
+  float rd;
+  rows_chol<NR>(A, rd, nvp, lane);
+  rows_store_strict<NR>(A, rd, Lm, nvp, lane);
+  sync();
+  float x = lane < nvp ? v[lane] : 0.f;
+  x = rows_solve<NR>(A, rd, Lm, x, nvp, lane);
+  if (lane < nvp) v[lane] = x;
+  sync();
+}
+
+// --------------------------------------------------------------------------- collision
+struct ConOut {
+  float* S;
+  int* ints;
+  const Lds* L;
+  int cap;
+};
+__device__ __forceinline__ void append(const ConOut& co, int key, int g1, int g2, float dist,
+                                       V3 pos, V3 n) {
+  int slot = atomicAdd(&co.ints[0], 1);
+  if (slot >= co.cap) {
+    atomicOr(&co.ints[3], 1);
+    return;
+  }
+  const Lds& L = *co.L;
+  int* Si = reinterpret_cast<int*>(co.S);
+  Si[L.con_key + slot] = key;
+  Si[L.con_g1 + slot] = g1;
+  Si[L.con_g2 + slot] = g2;
+  co.S[L.con_dist + slot] = dist;
+  st3(co.S + L.con_pos + 3 * slot, pos);
+  st3(co.S + L.con_frame + 9 * slot, n);
+}
+__device__ __forceinline__ int plane_sphere(const ConOut& co, int key, int g1, int g2, V3 pp,
+                                            V3 n, V3 c, float r, float margin) {
+  float dist = dot(c - pp, n) - r;
+  if (dist > margin) return 0;
+  append(co, key, g1, g2, dist, c - n * (r + 0.5f * dist), n);
+  return 1;
+}
+__device__ __forceinline__ int sphere_sphere(const ConOut& co, int key, int g1, int g2, V3 p1,
+                                             float r1, V3 p2, float r2, float margin) {
+  V3 dif = p2 - p1;
+  float cd = norm(dif);
+  float dist = cd - r1 - r2;
+  if (dist > margin) return 0;
+  V3 n = cd < MINVAL ? V3{1, 0, 0} : dif * (1.0f / cd);
+  append(co, key, g1, g2, dist, p1 + n * (r1 + 0.5f * dist), n);
+  return 1;
+}
+__device__ __forceinline__ float clamp01(float t) { return t < 0 ? 0 : (t > 1 ? 1 : t); }
+__device__ __forceinline__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
+  V3 u = a1 - a0, v = b1 - b0, wv = a0 - b0;
+  float a = dot(u, u), b = dot(u, v), c = dot(v, v), dd = dot(u, wv), e = dot(v, wv);
+  float den = a * c - b * b, s, t;
+  if (a < MINVAL && c < MINVAL) { s = t = 0; }
+  else if (a < MINVAL) { s = 0; t = clamp01(e / c); }
+  else if (c < MINVAL) { t = 0; s = clamp01(-dd / a); }
+  else {
+    s = den > MINVAL * a * c ? (b * e - c * dd) / den : 0;
+    s = clamp01(s);
+    t = (b * s + e) / c;
+    if (t < 0) { t = 0; s = clamp01(-dd / a); }
+    else if (t > 1) { t = 1; s = clamp01((b - dd) / a); }
+  }
+  *pa = a0 + u * s;
+  *pb = b0 + v * t;
+}
+
+
+// Heightfield frame (static body) and the sphere-vs-hfield narrowphase.  The surface is the
+// piecewise-linear interpolation of the elevation grid, two triangles per cell (p00 p10
+// p11 / p00 p11 p01); the contact is the deepest closest-point over the triangles of the
+// cells under the sphere footprint (oracle/oracle.c col_hfield_sphere, same arithmetic in
+// fp32).  Row r spans y, column c spans x, as MuJoCo lays out hfield data.
+struct HFrame { V3 p; float R[9]; };
+__device__ __forceinline__ HFrame hfield_frame(const DModel& m, const float* S, const Lds& L,
+                                               const float* gpos, const float* gquat, int g) {
+  HFrame f;
+  const int b = m.geom_bodyid[g];
+  const float* Rb = S + L.xmat + 9 * b;
+  f.p = v3(S + L.xpos + 3 * b) + mulv(Rb, v3(gpos + 3 * g));
+  float Rg[9];
+  qmat(Rg, q4(gquat + 4 * g));
+  mat3mul(f.R, Rb, Rg);
+  return f;
+}
+__device__ __forceinline__ int hfield_sphere(const ConOut& co, int key, int g1, int g2,
+                                             const HFrame& F, const float* hdata,
+                                             const float* hsize, int nr, int nc, V3 center,
+                                             float r, float margin, int* trunc) {
+  const V3 loc = mulTv(F.R, center - F.p);
+  const float sx = hsize[0], sy = hsize[1], sz = hsize[2];
+  const float dx = 2 * sx / (nc - 1), dy = 2 * sy / (nr - 1);
+  int c0 = (int)floorf((loc.x - r + sx) / dx), c1 = (int)floorf((loc.x + r + sx) / dx);
+  int r0 = (int)floorf((loc.y - r + sy) / dy), r1 = (int)floorf((loc.y + r + sy) / dy);
+  if (c1 < 0 || r1 < 0 || c0 > nc - 2 || r0 > nr - 2) return 0;
+  c0 = max(c0, 0); r0 = max(r0, 0);
+  c1 = min(c1, nc - 2); r1 = min(r1, nr - 2);
+  if ((c1 - c0 + 1) * (r1 - r0 + 1) > 64) { *trunc = 1; return 0; }  // footprint cap
+  float best = 1e30f;
+  V3 bestn = {0, 0, 1};
+  bool found = false;
+  for (int rr = r0; rr <= r1; rr++)
+    for (int cc = c0; cc <= c1; cc++) {
+      const float x0 = -sx + cc * dx, y0 = -sy + rr * dy;
+      const float* row0 = hdata + rr * nc + cc;
+      const V3 p00 = {x0, y0, row0[0] * sz}, p10 = {x0 + dx, y0, row0[1] * sz};
+      const V3 p01 = {x0, y0 + dy, row0[nc] * sz}, p11 = {x0 + dx, y0 + dy, row0[nc + 1] * sz};
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const V3 a = p00, b = k ? p11 : p10, c = k ? p01 : p11;
+        const V3 e1 = b - a, e2 = c - a;
+        V3 n = cross(e1, e2);
+        n = n * (1.0f / fmaxf(norm(n), MINVAL));
+        const float sd = dot(loc - a, n);
+        const V3 pp = loc - n * sd;
+        const V3 v2 = pp - a;
+        const float d00 = dot(e2, e2), d01 = dot(e2, e1), d11 = dot(e1, e1);
+        const float d20 = dot(v2, e2), d21 = dot(v2, e1);
+        const float den = d00 * d11 - d01 * d01;
+        const float u = (d11 * d20 - d01 * d21) / den, vv = (d00 * d21 - d01 * d20) / den;
+        V3 q;
+        if (u >= 0 && vv >= 0 && u + vv <= 1) {
+          q = pp;
+        } else {
+          float bd = 1e30f;
+          q = a;
+#pragma unroll
+          for (int e = 0; e < 3; e++) {
+            const V3 s0 = e == 0 ? a : (e == 1 ? b : c), s1 = e == 0 ? b : (e == 1 ? c : a);
+            const V3 ab = s1 - s0;
+            const float tt = clamp01(dot(loc - s0, ab) / fmaxf(dot(ab, ab), MINVAL));
+            const V3 cp = s0 + ab * tt;
+            const V3 df = loc - cp;
+            const float dd = dot(df, df);
+            if (dd < bd) { bd = dd; q = cp; }
+          }
+        }
+        const V3 diff = loc - q;
+        float dist = norm(diff);
+        V3 nn;
+        if (dist < MINVAL || sd < 0) { nn = n; dist = sd; }
+        else { nn = diff * (1.0f / dist); }
+        dist -= r;
+        if (dist < best) { best = dist; bestn = nn; found = true; }
+      }
+    }
+  if (!found || best > margin) return 0;
+  const V3 nw = mulv(F.R, bestn);
+  const V3 pw = mulv(F.R, loc - bestn * (r + 0.5f * best)) + F.p;
+  append(co, key, g1, g2, best, pw, nw);
+  return 1;
+}
+
+// --------------------------------------------------------------------------- impedance
+__device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
+  float dmin = fminf(MAXIMP, fmaxf(MINIMP, si[0])), dmax = fminf(MAXIMP, fmaxf(MINIMP, si[1]));
+  float width = fmaxf(0.f, si[2]), mid = fminf(1.f, fmaxf(MINIMP, si[3])), power = fmaxf(1.f, si[4]);
+  if (dmin == dmax || width <= MINVAL) return 0.5f * (dmin + dmax);
+  float x = fabsf(pos - margin) / width;
+  if (x >= 1 || x <= 0) return x >= 1 ? dmax : dmin;
+  float y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1);
+  else y = 1 - powf(1 - x, power) / powf(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+// reference stiffness / damping of a constraint row (mj_makeImpedance, solref > 0: time
+// constant and damping ratio; solref <= 0: direct stiffness and damping)
+__device__ __forceinline__ void solref_kb(const float* sref, const float* simp, float h, float& K,
+                                          float& B) {
+  const float dmax = fminf(MAXIMP, fmaxf(MINIMP, simp[1]));
+  if (sref[0] > 0) {
+    const float tc = fmaxf(sref[0], 2 * h), dr = sref[1];
+    K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+    B = 2.0f / (dmax * tc);
+  } else {
+    K = -sref[0] / (dmax * dmax);
+    B = -sref[1] / dmax;
+  }
+}
+// efc_cid row code: type (2 bits) | payload << 2; payload = contact index, or for joint
+// limits joint | dof << 8
+__device__ __forceinline__ int efc_code(int type, int payload) { return type | payload << 2; }
+
+// --------------------------------------------------------------------------- specialisation
+// ModelSpec<SP>: SP > 0 is the SP-th entry of specs.inc (scripts/gen_specs.py); its dims
+// and the three phase carves are returned BY VALUE from constexpr functions, so every
+// d.* bound and L.* LDS offset in the kernel folds to an immediate.  SP = 0 binds the
+// run-time Params copies (generic kernels for any model).
+template <int SP> struct ModelSpec {
+  static constexpr bool on = false;
+  static constexpr Dims dims() { return Dims{}; }
+};
+constexpr int nr_for_nv(int nv) {
+  // register-row length: exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36),
+  // multiples of 8 otherwise (engine.hip step_fn)
+  const int nvp = (nv + 3) & ~3;
+  return nvp <= 8 ? 8 : nvp <= 16 ? 16 : nvp <= 20 ? 20 : nvp <= 24 ? 24 : nvp <= 32 ? 32
+       : nvp <= 36 ? 36 : nvp <= 40 ? 40 : nvp <= 48 ? 48 : nvp <= 56 ? 56 : 64;
+}
+#define MJX_SPEC(id, scene, ...)                                              \
+  template <> struct ModelSpec<id> {                                          \
+    static constexpr bool on = true;                                          \
+    static constexpr Dims dims() { return Dims{__VA_ARGS__}; }                \
+  };
+#include "specs.inc"
+#undef MJX_SPEC
+template <int SP> constexpr int spec_nr() { return nr_for_nv(ModelSpec<SP>::dims().nv); }
+template <int SP, int K> struct SpecLds {
+  static constexpr Lds get() {
+    constexpr Lds v = make_lds(ModelSpec<SP>::dims(), K);
+    return v;
+  }
+};
+// `const auto& x = dims_of<SP>(P)`: a reference to Params for SP = 0, a constant
+// temporary (folded) for SP > 0.
+template <int SP>
+__device__ __forceinline__ decltype(auto) dims_of(const Params* P) {
+  if constexpr (SP > 0) return ModelSpec<SP>::dims();
+  else return static_cast<const Dims&>(P->d);
+}
+template <int SP, int K>
+__device__ __forceinline__ decltype(auto) lds_of(const Params* P) {
+  if constexpr (SP > 0) return SpecLds<SP, K>::get();
+  else return static_cast<const Lds&>(P->LP[K]);
+}
+
+// --------------------------------------------------------------------------- kernels
+// One substep = three launches, each holding only its own working set in LDS (more
+// resident worlds per CU); hand-off through the per-world global scratch P->gscr, laid out
+// with the full carve P->LG:
+//   PH 0 (A): kinematics, com, CRB/M, velocity/RNE/actuation, smooth solve, subtree
+//             momenta, pos/vel sensors, collision, contact parameters, constraint rows
+//             (J rows written straight to the scratch);
+//   PH 1 (B): Newton solver;
+//   PH 2 (C): post-constraint acceleration, acc-stage sensors, contact forces, integration.
+__device__ __forceinline__ void cp4(float* dst, const float* src, int n, int lane) {
+  for (int i = 4 * lane; i < n; i += 4 * kWave) st4v(dst + i, ld4(src + i));
+}
+// Bulk global->LDS copy of a phase's input pack by LDS-DMA (global_load_lds_dwordx4: each
+// wave-instruction lands 1 KiB at the wave-uniform LDS base + 16*lane, no VGPR staging), so
+// the whole pack is in flight at once; the caller waits with lds_dma_wait() before reading.
+// n is a multiple of 4 floats and dst/src are 16-byte aligned.
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* glob_void_t;
+__device__ __forceinline__ void cp_pack(float* __restrict__ dst, const float* __restrict__ src,
+                                        int n, int lane) {
+  for (int i0 = 0; i0 < n; i0 += 4 * kWave)
+    if (i0 + 4 * lane < n)
+      __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + 4 * lane), (lds_void_t)(dst + i0),
+                                       16, 0, 0);
+}
+// Global -> LDS copy of n floats (any alignment) by 4-byte LDS-DMA, lane per float.
+__device__ __forceinline__ void dma_row(float* dst, const float* src, int n, int lane) {
+  for (int i0 = 0; i0 < n; i0 += kWave)
+    if (i0 + lane < n)
+      __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + lane), (lds_void_t)(dst + i0), 4, 0, 0);
+}
+__device__ __forceinline__ void lds_dma_wait() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DModel& m, int b, V3 p) {
+  if (b <= 0) return {0.f, 0.f, 0.f};
+  const float* cv = S + L.cvel + 6 * b;
+  return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+}
+
+// Per-lane model records, loaded once at phase entry: the tree passes then index registers
+// instead of walking level_body -> body_* -> jnt_* chains of dependent global loads per
+// level.  Lane i holds level-order body i (BodyRec), dof i (DofRec) and actuator i (ActRec);
+// nbody, nv, nu <= 64 (mjx_model_create).  Only a body's first joint and five children are
+// cached; further ones (rare) are read from the model arrays.
+struct BodyRec {
+  int b, p, lv, j0, jn, jt, qa, da, d0, dn, mocap, root, c0, cn, chp;
+  V3 pos, jpos, jaxis, ipos, inert;
+  Q4 quat, iquat;
+  float qp0, mass;
+};
+struct BodyPtrs {
+  const float *pos, *quat, *ipos, *iquat, *mass, *inertia, *jpos, *jaxis, *qpos0;
+};
+__device__ __forceinline__ BodyRec load_body(const DModel& m, const Dims& d, const BodyPtrs& P,
+                                             int i) {
+  BodyRec r;
+  const int b = m.level_body[i];
+  r.b = b;
+  r.lv = 0;
+  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
+  r.p = m.body_parentid[b];
+  r.j0 = m.body_jntadr[b]; r.jn = m.body_jntnum[b];
+  r.d0 = m.body_dofadr[b]; r.dn = m.body_dofnum[b];
+  r.mocap = m.body_mocapid[b];
+  r.root = m.body_rootid[b];
+  r.c0 = m.body_childadr[b]; r.cn = m.body_childadr[b + 1] - r.c0;
+  r.chp = 0;
+  for (int t = 0; t < 5 && t < r.cn; t++) r.chp |= m.body_child[r.c0 + t] << (6 * t);
+  r.pos = v3(P.pos + 3 * b); r.quat = q4(P.quat + 4 * b);
+  r.ipos = v3(P.ipos + 3 * b); r.iquat = q4(P.iquat + 4 * b);
+  r.mass = P.mass[b]; r.inert = v3(P.inertia + 3 * b);
+  const int k = r.jn > 0 ? r.j0 : 0;
+  r.jt = m.jnt_type[k]; r.qa = m.jnt_qposadr[k]; r.da = m.jnt_dofadr[k];
+  r.jpos = v3(P.jpos + 3 * k); r.jaxis = v3(P.jaxis + 3 * k);
+  r.qp0 = P.qpos0[r.qa];
+  return r;
+}
+__device__ __forceinline__ int body_child(const DModel& m, const BodyRec& r, int t) {
+  return t < 5 ? (r.chp >> (6 * t)) & 63 : m.body_child[r.c0 + t];
+}
+// joint k of body r: the cached first joint or a model read
+struct JntRec { int jt, qa, da; V3 jpos, jaxis; float qp0; };
+__device__ __forceinline__ JntRec jnt_of(const DModel& m, const BodyPtrs& P, const BodyRec& r,
+                                         int k) {
+  if (k == r.j0) return {r.jt, r.qa, r.da, r.jpos, r.jaxis, r.qp0};
+  const int qa = m.jnt_qposadr[k];
+  return {m.jnt_type[k], qa, m.jnt_dofadr[k], v3(P.jpos + 3 * k), v3(P.jaxis + 3 * k), P.qpos0[qa]};
+}
+struct BodyLite { int b, p, lv, d0, dn; };
+__device__ __forceinline__ BodyLite load_body_lite(const DModel& m, const Dims& d, int i) {
+  BodyLite r;
+  r.b = m.level_body[i];
+  r.lv = 0;
+  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
+  r.p = m.body_parentid[r.b];
+  r.d0 = m.body_dofadr[r.b]; r.dn = m.body_dofnum[r.b];
+  return r;
+}
+struct DofRec {
+  int body, jt, qa;
+  uint64_t anc;
+  float arm, damp, stiff, qs;
+};
+struct ActRec {
+  int dof, qa, ctrllim, forcelim;
+  float gear, gain, b0, b1, b2, fr0, fr1, cr0, cr1;
+};
+__device__ __forceinline__ ActRec load_act(const DModel& m, const float* gear, const float* gain,
+                                           const float* bias, const float* frange,
+                                           const float* crange, int u) {
+  ActRec r;
+  const int j = m.actuator_trnid[u];
+  r.dof = m.jnt_dofadr[j]; r.qa = m.jnt_qposadr[j];
+  r.ctrllim = m.actuator_ctrllimited[u]; r.forcelim = m.actuator_forcelimited[u];
+  r.gear = gear[u]; r.gain = gain[3 * u];
+  r.b0 = bias[3 * u]; r.b1 = bias[3 * u + 1]; r.b2 = bias[3 * u + 2];
+  r.fr0 = frange[2 * u]; r.fr1 = frange[2 * u + 1];
+  r.cr0 = crange[2 * u]; r.cr1 = crange[2 * u + 1];
+  return r;
+}
+// contact bodies packed in one int (nbody <= 64): b1 | b2 << 8 | root(b1) << 16 | root(b2) << 24
+__device__ __forceinline__ int cb_b1(int v) { return v & 255; }
+__device__ __forceinline__ int cb_b2(int v) { return (v >> 8) & 255; }
+__device__ __forceinline__ int cb_r1(int v) { return (v >> 16) & 255; }
+__device__ __forceinline__ int cb_r2(int v) { return (v >> 24) & 255; }
+__device__ __forceinline__ V3 point_vel_r(const float* S, const Lds& L, int b, int root, V3 p) {
+  if (b <= 0) return {0.f, 0.f, 0.f};
+  const float* cv = S + L.cvel + 6 * b;
+  return v3(cv + 3) + cross(v3(cv), p - v3(S + L.subtree_com + 3 * root));
+}
+
+// mjSENS_CONTACT with one slot (sensor/contact_sensor.py:16-97, 472-533), one wave per
+// world, lane = contact: match by the geom masks, then found = popcount(ballot), netforce =
+// wave sums of the signed world-frame forces, and for mindist / maxforce / none the
+// single selected contact is the wave argmin of its key (ties -> lowest contact index).
+__device__ __forceinline__ void contact_sensors_wave(const float* S, const int* Si, const Lds& L,
+                                                     const DModel& m, const Dims& d, float* sd,
+                                                     int ncon, int lane) {
+  const int c = lane;
+  const bool valid = c < ncon;
+  int g1 = 0, g2 = 0;
+  V3 fg = {0, 0, 0}, fc = {0, 0, 0};
+  float dist = 0.f;
+  if (valid) {
+    g1 = Si[L.con_g1 + c];
+    g2 = Si[L.con_g2 + c];
+    dist = S[L.con_dist + c];
+    const int r0 = Si[L.con_efc + c];
+    if (Si[L.con_dim + c] == 1) {
+      fc.x = S[L.efc_force + r0];
+    } else {
+      float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+      float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+      fc = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+    }
+    fg = mulTv(S + L.con_frame + 9 * c, fc);
+  }
+  for (int s = 0; s < d.nsensor; s++) {
+    if (m.sensor_type[s] != SENS_CONTACT) continue;
+    const int32_t* ip = m.sensor_intprm + 3 * s;
+    if (ip[2] > 1) continue;  // multi-slot: serial path
+    const int bits = ip[0], reduce = ip[1];
+    float* out = sd + m.sensor_adr[s];
+    const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+    const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+    bool a1 = false, a2 = false;
+    if (valid) {
+      a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+      a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+    }
+    const bool match = a1 || a2;
+    const unsigned long long bal = __ballot(match);
+    const float found = (float)__popcll(bal);
+    const int dim = m.sensor_dim[s];
+    if (reduce == REDUCE_NETFORCE) {
+      const float sg = match ? (a1 ? 1.f : -1.f) : 0.f;
+      const float nx = wave_sum(sg * fg.x), ny = wave_sum(sg * fg.y), nz = wave_sum(sg * fg.z);
+      if (lane == 0) {
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        if (bits & 1) out[0] = found;
+        else if (bits & 2) { out[0] = nx; out[1] = ny; out[2] = nz; }
+      }
+      continue;
+    }
+    // one slot: the matching contact with the smallest key
+    float key = reduce == REDUCE_MINDIST ? dist
+              : reduce == REDUCE_MAXFORCE ? -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z)
+              : (float)c;
+    if (!match) key = FLT_MAX;
+    float kmin = key;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kmin = fminf(kmin, __shfl_xor(kmin, o));
+    const unsigned long long win = __ballot(match && key == kmin);
+    const int sel = win ? __ffsll((long long)win) - 1 : -1;
+    if (lane == 0) for (int i = 0; i < dim; i++) out[i] = 0.f;
+    if (sel >= 0 && lane == sel) {
+      const float sg = a1 ? 1.f : -1.f;
+      if (bits & 1) out[0] = found;
+      else if (bits & 8) out[0] = dist;
+      else if (bits & 16) { for (int t = 0; t < 3; t++) out[t] = S[L.con_pos + 3 * c + t]; }
+      else if (bits & 32) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + t]; }
+      else if (bits & 64) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+      else if (bits & 2) { out[0] = fc.x; out[1] = fc.y; out[2] = fc.z; }
+    }
+  }
+}
+
+template <int NR, int PH, int SP>
+__global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int nworld,
+                                                    int last, int integrate,
+                                                    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  const auto& d = dims_of<SP>(P);
+  const Opt& o = P->o;
+  const DModel& m = P->m;
+  const DData& D = P->D;
+  // phase B: `integrate` carries the Newton row class (0 = full capacity, k > 0 = LP[2 + k])
+  const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate] : lds_of<SP, PH>(P);
+  const auto& LB = lds_of<SP, 1>(P);
+  const auto& LC = lds_of<SP, 2>(P);
+  const int w = blockIdx.x;
+  if (w >= nworld) return;
+  if (mask && !mask[w]) return;  // masked forward: only the selected worlds
+  float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
+  float* gc = gw + P->gC;
+  float* gf = gw + P->gF;  // implicit-integration factor (phase A writes, phase C reads)
+  (void)LB; (void)LC; (void)gc;
+  const int lane = threadIdx.x;
+  int* Si = reinterpret_cast<int*>(S);
+  int* ints = Si + L.ints;
+  const int nv = d.nv, nb = d.nbody, nq = d.nq, nu = d.nu;
+  const int nvp = (nv + 3) & ~3;
+  const int nvq = (nvp + 3) & ~3;  // copy length of an nvp vector region
+  const float h = o.timestep;
+  (void)nq; (void)nu; (void)h;
+#ifdef MJX_STAMPS
+  unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
+  unsigned long long sub_prev = stamp_prev;
+  unsigned long long stamp_acc[48];
+#pragma unroll
+  for (int k_ = 0; k_ < 48; k_++) stamp_acc[k_] = 0;
+#endif
+  const float* body_pos = MF(body_pos);
+  const float* body_quat = MF(body_quat);
+  const float* body_ipos = MF(body_ipos);
+  const float* body_iquat = MF(body_iquat);
+  const float* body_mass = MF(body_mass);
+  const float* body_inertia = MF(body_inertia);
+  const float* jnt_pos = MF(jnt_pos);
+  const float* jnt_axis = MF(jnt_axis);
+  const float* qpos0 = MF(qpos0);
+  (void)body_pos; (void)body_quat; (void)body_ipos; (void)body_iquat; (void)body_mass;
+  (void)body_inertia; (void)jnt_pos; (void)jnt_axis; (void)qpos0;
+
+  if constexpr (PH == 0) {
+    // ----------------------------------------------------------- phase A
+    // Preamble: every independent global read is in flight before the first wait -- state
+    // rows go straight into LDS (LDS-DMA), model records into registers, then one wait
+    // (copied loop by loop, each load-then-LDS-store would wait out a global latency).
+    for (int i = lane; i < nvp; i += kWave) {
+      if (i >= nv) { S[L.qvel + i] = 0.f; S[L.qfrc_applied + i] = 0.f; }  // DMA fills i < nv
+      S[L.qfrc_bias + i] = 0.f; S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f;
+      S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f;
+    }
+    dma_row(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
+    dma_row(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
+    dma_row(S + L.qfrc_applied, D.qfrc_applied + (size_t)w * nv, nv, lane);
+    dma_row(S + L.ctrl, D.ctrl + (size_t)w * nu, nu, lane);
+    SUBSTAMP(15);
+    float* Jg = gw + LB.efc_J;
+    const BodyPtrs BP{body_pos, body_quat, body_ipos, body_iquat, body_mass, body_inertia,
+                      jnt_pos, jnt_axis, qpos0};
+    const BodyRec B = load_body(m, d, BP, min(lane, nb - 1));
+#ifdef MJX_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SUBSTAMP(16);
+    const bool bl = lane < nb;  // this lane holds a body record
+    DofRec Dr;
+    {
+      const int i = min(lane, max(nv - 1, 0));
+      const int j = m.dof_jntid[i];
+      const float* arm = MF(dof_armature);
+      const float* damping = MF(dof_damping);
+      const float* jstiff = MF(jnt_stiffness);
+      const float* qspring = MF(qpos_spring);
+      Dr.body = m.dof_bodyid[i]; Dr.anc = m.dof_ancmask[i];
+      Dr.jt = m.jnt_type[j]; Dr.qa = m.jnt_qposadr[j];
+      Dr.arm = arm[i]; Dr.damp = damping[i]; Dr.stiff = jstiff[j]; Dr.qs = qspring[Dr.qa];
+    }
+#ifdef MJX_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SUBSTAMP(17);
+    const ActRec Ar = load_act(m, MF(actuator_gear), MF(actuator_gainprm), MF(actuator_biasprm),
+                               MF(actuator_forcerange), MF(actuator_ctrlrange),
+                               min(lane, max(nu - 1, 0)));
+    int any_xfrc = 0;
+    for (int i = lane; i < 6 * nb; i += kWave) any_xfrc |= D.xfrc_applied[(size_t)w * 6 * nb + i] != 0.f;
+    any_xfrc = __any(any_xfrc);
+    lds_dma_wait();
+    sync();
+    SUBSTAMP(13);
+    // =========================================================== kinematics (levels)
+    if (lane == 0) {
+      S[L.xpos + 0] = S[L.xpos + 1] = S[L.xpos + 2] = 0;
+      S[L.xquat + 0] = 1; S[L.xquat + 1] = S[L.xquat + 2] = S[L.xquat + 3] = 0;
+    }
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
+        float Rp[9];
+        qmat(Rp, q4(S + L.xquat + 4 * p));
+        V3 pos = v3(S + L.xpos + 3 * p) + mulv(Rp, B.pos);
+        Q4 q = qmul(q4(S + L.xquat + 4 * p), B.quat);
+        if (B.mocap >= 0) {
+          pos = v3(D.mocap_pos + ((size_t)w * d.nmocap + B.mocap) * 3);
+          q = q4(D.mocap_quat + ((size_t)w * d.nmocap + B.mocap) * 4);
+        }
+        for (int k = B.j0; k < B.j0 + B.jn; k++) {
+          const JntRec J = jnt_of(m, BP, B, k);
+          const int a = J.qa;
+          float R[9];
+          if (J.jt == JNT_FREE) {
+            pos = v3(S + L.qpos + a);
+            q = qnorm(q4(S + L.qpos + a + 3));
+            st3(S + L.xanchor + 3 * k, pos);
+            qmat(R, q);
+            st3(S + L.xaxis + 3 * k, mulv(R, J.jaxis));
+            continue;
+          }
+          qmat(R, q);
+          V3 anchor = mulv(R, J.jpos) + pos;
+          V3 axis = mulv(R, J.jaxis);
+          st3(S + L.xanchor + 3 * k, anchor);
+          st3(S + L.xaxis + 3 * k, axis);
+          if (J.jt == JNT_HINGE) {
+            q = qmul(q, qaxisangle(J.jaxis, S[L.qpos + a] - J.qp0));
+            qmat(R, q);
+            pos = anchor - mulv(R, J.jpos);
+          } else if (J.jt == JNT_SLIDE) {
+            pos = pos + axis * (S[L.qpos + a] - J.qp0);
+          }
+        }
+        q = qnorm(q);
+        st3(S + L.xpos + 3 * b, pos);
+        st4(S + L.xquat + 4 * b, q);
+      }
+      sync();
+    }
+    SUBSTAMP(14);
+    if (bl) {
+      const int b = B.b;
+      float* R = S + L.xmat + 9 * b;
+      qmat(R, q4(S + L.xquat + 4 * b));
+      st3(S + L.xipos + 3 * b, v3(S + L.xpos + 3 * b) + mulv(R, B.ipos));
+      float Ri[9];
+      qmat(Ri, B.iquat);
+      mat3mul(S + L.ximat + 9 * b, R, Ri);
+    }
+    sync();
+    {
+      const float* spos = MF(site_pos);
+      const float* squat = MF(site_quat);
+      for (int s = lane; s < d.nsite; s += kWave) {
+        int b = m.site_bodyid[s];
+        const float* R = S + L.xmat + 9 * b;
+        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + mulv(R, v3(spos + 3 * s)));
+        float Rs[9];
+        qmat(Rs, q4(squat + 4 * s));
+        mat3mul(S + L.sxmat + 9 * s, R, Rs);
+      }
+    }
+    STAMP(0);
+    // =========================================================== com / cinert / cdof
+    if (bl) {
+      S[L.stmass + B.b] = B.mass;
+      st3(S + L.subtree_com + 3 * B.b, v3(S + L.xipos + 3 * B.b) * B.mass);
+    }
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      if (bl && B.lv == lv) {
+        const int b = B.b;
+        float ms = S[L.stmass + b];
+        V3 c = v3(S + L.subtree_com + 3 * b);
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
+          ms += S[L.stmass + ch];
+          c = c + v3(S + L.subtree_com + 3 * ch);
+        }
+        S[L.stmass + b] = ms;
+        st3(S + L.subtree_com + 3 * b, c);
+      }
+      sync();
+    }
+    if (bl) {
+      const int b = B.b;
+      float ms = S[L.stmass + b];
+      V3 c = ms > MINVAL ? v3(S + L.subtree_com + 3 * b) * (1.0f / ms) : v3(S + L.xipos + 3 * b);
+      st3(S + L.subtree_com + 3 * b, c);
+    }
+    sync();
+    if (bl) {
+      const int b = B.b;
+      float* c = S + L.cinert + 10 * b;
+      if (b == 0) {
+        for (int i = 0; i < 10; i++) c[i] = 0;
+      } else {
+      V3 off = v3(S + L.subtree_com + 3 * B.root);
+      const float* R = S + L.ximat + 9 * b;
+      const float I[3] = {B.inert.x, B.inert.y, B.inert.z};
+      float full[9];
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+          full[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] +
+                            R[3 * i + 2] * I[2] * R[3 * j + 2];
+      V3 dv = v3(S + L.xipos + 3 * b) - off;
+      float ms = B.mass, dd = dot(dv, dv);
+      c[0] = full[0] + ms * (dd - dv.x * dv.x);
+      c[1] = full[4] + ms * (dd - dv.y * dv.y);
+      c[2] = full[8] + ms * (dd - dv.z * dv.z);
+      c[3] = full[1] - ms * dv.x * dv.y;
+      c[4] = full[2] - ms * dv.x * dv.z;
+      c[5] = full[5] - ms * dv.y * dv.z;
+      c[6] = ms * dv.x; c[7] = ms * dv.y; c[8] = ms * dv.z; c[9] = ms;
+      }
+    }
+    // cdof: lane per body over its joints
+    for (int k = B.j0; bl && k < B.j0 + B.jn; k++) {
+      const int b = B.b;
+      const JntRec J = jnt_of(m, BP, B, k);
+      const int dof = J.da;
+      V3 rel = v3(S + L.subtree_com + 3 * B.root) - v3(S + L.xanchor + 3 * k);
+      const int t = J.jt;
+      if (t == JNT_FREE) {
+        for (int i = 0; i < 3; i++) {
+          float* c = S + L.cdof + 6 * (dof + i);
+          for (int j = 0; j < 6; j++) c[j] = 0;
+          c[3 + i] = 1;
+        }
+        const float* R = S + L.xmat + 9 * b;
+        for (int i = 0; i < 3; i++) {
+          float* c = S + L.cdof + 6 * (dof + 3 + i);
+          V3 ax = {R[i], R[3 + i], R[6 + i]};
+          st3(c, ax);
+          st3(c + 3, cross(ax, rel));
+        }
+      } else if (t == JNT_HINGE) {
+        float* c = S + L.cdof + 6 * dof;
+        V3 ax = v3(S + L.xaxis + 3 * k);
+        st3(c, ax);
+        st3(c + 3, cross(ax, rel));
+      } else if (t == JNT_SLIDE) {
+        float* c = S + L.cdof + 6 * dof;
+        c[0] = c[1] = c[2] = 0;
+        st3(c + 3, v3(S + L.xaxis + 3 * k));
+      }
+    }
+    sync();
+    STAMP(1);
+    // =========================================================== CRB + mass matrix
+    for (int i = lane; i < 10 * nb; i += kWave) S[L.crb + i] = S[L.cinert + i];
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
+      if (bl && B.lv == lv) {
+        const int b = B.b;
+        float acc[10];
+        for (int j = 0; j < 10; j++) acc[j] = S[L.crb + 10 * b + j];
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
+          for (int j = 0; j < 10; j++) acc[j] += S[L.crb + 10 * ch + j];
+        }
+        for (int j = 0; j < 10; j++) S[L.crb + 10 * b + j] = acc[j];
+      }
+      sync();
+    }
+    for (int i = lane; i < nvp * nvp; i += kWave) S[L.M + i] = 0;
+    sync();
+    for (int i = nv + lane; i < nvp; i += kWave) S[L.M + i * nvp + i] = 1.f;  // identity padding
+    if (lane < nv) {
+      const int i = lane;
+      float f[6];
+      inert_mul(f, S + L.crb + 10 * Dr.body, S + L.cdof + 6 * i);
+      for (uint64_t a = Dr.anc; a; a &= a - 1) {  // dof i and its ancestors
+        const int j = __builtin_ctzll(a);
+        float v = dot6(S + L.cdof + 6 * j, f);
+        S[L.M + i * nvp + j] = v;
+        S[L.M + j * nvp + i] = v;
+      }
+      S[L.M + i * nvp + i] += Dr.arm;
+    }
+    sync();
+    // M to the B pack now: its LDS slot is reused (in place factor, then contacts).  Phase C
+    // gets the implicit-integration factor of M + h D instead (below, scratch region F).
+    cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
+    STAMP(2);
+    // =========================================================== velocity stage
+    if (lane < 6) S[L.cvel + lane] = 0;
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
+        float v[6];
+        for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
+        for (int k = B.j0; k < B.j0 + B.jn; k++) {
+          const int dof = k == B.j0 ? B.da : m.jnt_dofadr[k];
+          if ((k == B.j0 ? B.jt : m.jnt_type[k]) == JNT_FREE) {
+            for (int a = 0; a < 3; a++) {
+              for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+            }
+            for (int a = 3; a < 6; a++) cross_motion(S + L.cdofdot + 6 * (dof + a), v, S + L.cdof + 6 * (dof + a));
+            for (int a = 3; a < 6; a++)
+              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
+          } else {
+            cross_motion(S + L.cdofdot + 6 * dof, v, S + L.cdof + 6 * dof);
+            for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * dof + j] * S[L.qvel + dof];
+          }
+        }
+        for (int j = 0; j < 6; j++) S[L.cvel + 6 * b + j] = v[j];
+      }
+      sync();
+    }
+    // RNE (flg_acc = 0): cacc with gravity, body forces into crb scratch (reused as cfrc)
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        const int d0 = B.d0, d1 = d0 + B.dn;
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+        float f1[6], iv[6], f2[6];
+        inert_mul(f1, S + L.cinert + 10 * b, a);
+        inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
+        cross_force(f2, S + L.cvel + 6 * b, iv);
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = f1[j] + f2[j];
+      }
+      sync();
+    }
+    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
+      if (bl && B.lv == lv) {
+        const int b = B.b;
+        float acc[6];
+        for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
+        for (int t = 0; t < B.cn; t++) {
+          const int ch = body_child(m, B, t);
+          for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
+        }
+        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
+      }
+      sync();
+    }
+    if (lane < nv) {
+      const int i = lane;
+      S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * Dr.body);
+      float pf = -Dr.damp * S[L.qvel + i];
+      if ((Dr.jt == JNT_HINGE || Dr.jt == JNT_SLIDE) && Dr.stiff != 0.f)
+        pf -= Dr.stiff * (S[L.qpos + Dr.qa] - Dr.qs);
+      S[L.qfrc_passive + i] = pf;
+      S[L.qfrc_act + i] = 0.f;
+    }
+    sync();
+    // actuation: position / motor actuators on joints
+    if (lane < nu) {
+      const int u = lane;
+      const float g = Ar.gear;
+      float len = g * S[L.qpos + Ar.qa], vel = g * S[L.qvel + Ar.dof];
+      float c = S[L.ctrl + u];
+      if (Ar.ctrllim) c = fminf(fmaxf(c, Ar.cr0), Ar.cr1);
+      float f = Ar.gain * c + Ar.b0 + Ar.b1 * len + Ar.b2 * vel;
+      if (Ar.forcelim) f = fminf(fmaxf(f, Ar.fr0), Ar.fr1);
+      S[L.act_force + u] = f;
+      S[L.act_len + u] = len;
+      S[L.act_vel + u] = vel;
+      atomicAdd(S + L.qfrc_act + Ar.dof, g * f);
+    }
+    sync();
+    for (int i = lane; i < nv; i += kWave) {
+      float f = S[L.qfrc_passive + i] - S[L.qfrc_bias + i] + S[L.qfrc_applied + i] + S[L.qfrc_act + i];
+      if (any_xfrc) {
+        uint64_t bm = m.dof_bodymask[i];
+        const float* cd = S + L.cdof + 6 * i;
+        V3 cang = v3(cd), clin = v3(cd + 3);
+        for (int b = 1; b < nb; b++) {
+          if (!((bm >> b) & 1ull)) continue;
+          const float* xf = D.xfrc_applied + ((size_t)w * nb + b) * 6;
+          V3 jp = clin + cross(cang, v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * m.body_rootid[b]));
+          f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
+        }
+      }
+      S[L.qfrc_smooth + i] = f;
+      S[L.qacc_smooth + i] = f;
+    }
+    // subtree momenta (for subtreeangmom sensors)
+    if (bl) {
+      const int b = B.b;
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      st3(S + L.stlin + 3 * b, vc * B.mass);
+      const float* Ri = S + L.ximat + 9 * b;
+      V3 wl = mulTv(Ri, v3(cv));
+      V3 hl = {B.inert.x * wl.x, B.inert.y * wl.y, B.inert.z * wl.z};
+      st3(S + L.stang + 3 * b, mulv(Ri, hl));
+    }
+    sync();
+    STAMP(6);
+    if (integrate) {
+      // implicitfast / Euler: factor M + h diag(dof damping - gear^2 biasprm2) here, where M
+      // and the (clamped) actuator forces are at hand, into the scratch region F; phase C then
+      // runs only the two triangular solves.  The actuator term is dropped for an actuator
+      // whose force is at its forcerange limit (zero derivative), as in mj_implicit.
+      float act_d = 0.f;
+      if (o.integrator == 1 && lane < nu && Ar.b2 != 0.f) {
+        bool skip = false;
+        if (Ar.forcelim) {
+          const float fo = S[L.act_force + lane];
+          skip = fo <= Ar.fr0 || fo >= Ar.fr1;
+        }
+        if (!skip) act_d = -h * Ar.gear * Ar.gear * Ar.b2;
+      }
+      float da = lane < nv ? h * Dr.damp : 0.f;
+      for (int u = 0; u < nu; u++) {  // scatter actuator terms onto their dofs
+        const float cu = rl(act_d, u);
+        if (lane == __builtin_amdgcn_readlane(Ar.dof, u)) da += cu;
+      }
+      float A[NR];
+      rows_load<NR>(A, S + L.M, nvp, lane);
+#pragma unroll
+      for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
+      float rd;
+      rows_chol<NR>(A, rd, nvp, lane);
+      rows_store_strict<NR>(A, rd, gf, nvp, lane);
+    }
+    // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
+    spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, nvp, lane);
+    STAMP(7);
+    // linear momentum of subtrees -> velocity of subtree com
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      if (bl && B.lv == lv) {
+        const int b = B.b;
+        V3 acc = v3(S + L.stlin + 3 * b);
+        for (int t = 0; t < B.cn; t++) acc = acc + v3(S + L.stlin + 3 * body_child(m, B, t));
+        st3(S + L.stlin + 3 * b, acc);
+      }
+      sync();
+    }
+    if (bl) {
+      const int b = B.b;
+      float sm = S[L.stmass + b];
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
+      st3(S + L.stlin + 3 * b, lin);
+    }
+    sync();
+    if (bl && B.b != 0) {
+      const int b = B.b;
+      const float* cv = S + L.cvel + 6 * b;
+      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
+      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
+      V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
+      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * B.mass;
+      st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
+    }
+    sync();
+    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
+      if (bl && B.lv == lv) {
+        const int p = B.b;
+        V3 acc = v3(S + L.stang + 3 * p);
+        for (int t = 0; t < B.cn; t++) {
+          const int b = body_child(m, B, t);
+          V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
+          V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
+          acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
+        }
+        st3(S + L.stang + 3 * p, acc);
+      }
+      sync();
+    }
+    STAMP(8);
+    if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
+    // geom frames (here, not in kinematics: their LDS aliases regions dead after RNE)
+    {
+      const float* gpos = MF(geom_pos);
+      const float* gquat = MF(geom_quat);
+      for (int sl = lane; sl < d.ngeom_lds; sl += kWave) {
+        const int g = m.lds_geom[sl];
+        int b = m.geom_bodyid[g];
+        const float* R = S + L.xmat + 9 * b;
+        st3(S + L.gxpos + 3 * sl, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
+        float Rg[9];
+        qmat(Rg, q4(gquat + 4 * g));
+        mat3mul(S + L.gxmat + 9 * sl, R, Rg);
+      }
+    }
+    sync();
+    // =========================================================== collision
+    {
+      ConOut co{S, ints, &L, d.nconmax};
+      const float* gsize = MF(geom_size);
+      const float* grb = MF(geom_rbound);
+      const float* gmargin = MF(geom_margin);
+      for (int p = lane; p < d.npair; p += kWave) {
+        int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+        int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+        const int l1 = m.geom_lds[g1], l2 = m.geom_lds[g2];  // LDS frame slots
+        float margin = fmaxf(gmargin[g1], gmargin[g2]);
+        V3 p1 = v3(S + L.gxpos + 3 * l1), p2 = v3(S + L.gxpos + 3 * l2);
+        float r1 = grb[g1], r2 = grb[g2];
+        if (r1 > 0 && r2 > 0 && t1 != GEOM_HFIELD) {
+          if (norm(p2 - p1) > r1 + r2 + margin) continue;
+        }
+        const float* s1 = gsize + 3 * g1;
+        const float* s2 = gsize + 3 * g2;
+        int key = p * 8;
+        if (t1 == GEOM_PLANE) {
+          const float* Rp = S + L.gxmat + 9 * l1;
+          V3 n = {Rp[2], Rp[5], Rp[8]};
+          if (t2 == GEOM_SPHERE) {
+            plane_sphere(co, key, g1, g2, p1, n, p2, s2[0], margin);
+          } else if (t2 == GEOM_CAPSULE) {
+            const float* R2 = S + L.gxmat + 9 * l2;
+            V3 ax = {R2[2], R2[5], R2[8]};
+            int k = key;
+            k += plane_sphere(co, k, g1, g2, p1, n, p2 + ax * s2[1], s2[0], margin);
+            plane_sphere(co, k, g1, g2, p1, n, p2 - ax * s2[1], s2[0], margin);
+          } else if (t2 == GEOM_BOX) {
+            float dist = dot(p2 - p1, n);
+            const float* R2 = S + L.gxmat + 9 * l2;
+            int cnt = 0;
+            for (int i = 0; i < 8 && cnt < 4; i++) {
+              V3 v = {(i & 1) ? s2[0] : -s2[0], (i & 2) ? s2[1] : -s2[1], (i & 4) ? s2[2] : -s2[2]};
+              V3 corner = mulv(R2, v);
+              float ld = dot(n, corner);
+              if (dist + ld > margin || ld > 0) continue;
+              append(co, key + cnt, g1, g2, dist + ld, corner + p2 - n * (0.5f * (dist + ld)), n);
+              cnt++;
+            }
+          } else {
+            atomicOr(&ints[3], 4);
+          }
+        } else if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) {
+          sphere_sphere(co, key, g1, g2, p1, s1[0], p2, s2[0], margin);
+        } else if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
+          const float* R2 = S + L.gxmat + 9 * l2;
+          V3 ax = {R2[2], R2[5], R2[8]};
+          V3 pa, pb;
+          seg_seg(p1, p1, p2 + ax * s2[1], p2 - ax * s2[1], &pa, &pb);
+          sphere_sphere(co, key, g1, g2, p1, s1[0], pb, s2[0], margin);
+        } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
+          const float* R1 = S + L.gxmat + 9 * l1;
+          const float* R2 = S + L.gxmat + 9 * l2;
+          V3 a1 = {R1[2], R1[5], R1[8]}, a2 = {R2[2], R2[5], R2[8]};
+          V3 pa, pb;
+          seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
+          sphere_sphere(co, key, g1, g2, pa, s1[0], pb, s2[0], margin);
+        } else {
+          atomicOr(&ints[3], 4);
+        }
+      }
+      // heightfield pairs: the union AABB of the hfield partners (bounding spheres) culls
+      // the hfield geoms (lane per hfield), then lanes take the pairs of each overlapping
+      // hfield block.  A terrain of many sub-terrain hfields costs ~1 block per world.
+      if (d.nhfgeom > 0) {
+        float lo0 = 1e30f, lo1 = 1e30f, lo2 = 1e30f, hi0 = -1e30f, hi1 = -1e30f, hi2 = -1e30f;
+        for (int i = lane; i < d.nhfpartner; i += kWave) {
+          const int g = m.hf_partner[i];
+          const V3 c = v3(S + L.gxpos + 3 * m.geom_lds[g]);
+          const float r = grb[g] + gmargin[g];
+          lo0 = fminf(lo0, c.x - r); lo1 = fminf(lo1, c.y - r); lo2 = fminf(lo2, c.z - r);
+          hi0 = fmaxf(hi0, c.x + r); hi1 = fmaxf(hi1, c.y + r); hi2 = fmaxf(hi2, c.z + r);
+        }
+        lo0 = wave_min(lo0); lo1 = wave_min(lo1); lo2 = wave_min(lo2);
+        hi0 = wave_max(hi0); hi1 = wave_max(hi1); hi2 = wave_max(hi2);
+        const float* gpos = MF(geom_pos);
+        const float* gquat = MF(geom_quat);
+        const float* hsz_all = MF(hfield_size);
+        const float* hdat_all = MF(hfield_data);
+        int trunc = 0;
+        for (int base = 0; base < d.nhfgeom; base += kWave) {
+          bool act = false;
+          const int i = base + lane;
+          if (i < d.nhfgeom) {
+            const int g = m.hf_geom[i];
+            const HFrame F = hfield_frame(m, S, L, gpos, gquat, g);
+            const float* hs = hsz_all + 4 * m.geom_dataid[g];
+            // local box [-sx, sx] x [-sy, sy] x [-base, z_max] -> world AABB
+            const float ex = hs[0], ey = hs[1], ez = 0.5f * (hs[2] + hs[3]);
+            const V3 cw = F.p + mulv(F.R, V3{0, 0, 0.5f * (hs[2] - hs[3])});
+            const float wx = fabsf(F.R[0]) * ex + fabsf(F.R[1]) * ey + fabsf(F.R[2]) * ez;
+            const float wy = fabsf(F.R[3]) * ex + fabsf(F.R[4]) * ey + fabsf(F.R[5]) * ez;
+            const float wz = fabsf(F.R[6]) * ex + fabsf(F.R[7]) * ey + fabsf(F.R[8]) * ez;
+            act = cw.x - wx <= hi0 && cw.x + wx >= lo0 && cw.y - wy <= hi1 &&
+                  cw.y + wy >= lo1 && cw.z - wz <= hi2 && cw.z + wz >= lo2;
+          }
+          unsigned long long bal = __ballot(act);
+          while (bal) {
+            const int j = base + __ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+            const int hg = m.hf_geom[j];
+            const HFrame F = hfield_frame(m, S, L, gpos, gquat, hg);
+            const int hid = m.geom_dataid[hg];
+            const float* hs = hsz_all + 4 * hid;
+            const float* hd = hdat_all + m.hfield_adr[hid];
+            const int nr = m.hfield_nrow[hid], nc = m.hfield_ncol[hid];
+            for (int p = m.hf_pairadr[j] + lane; p < m.hf_pairadr[j + 1]; p += kWave) {
+              const int g2 = m.pair_geom2[p];
+              const int t2 = m.geom_type[g2];
+              const int l2 = m.geom_lds[g2];
+              const V3 p2 = v3(S + L.gxpos + 3 * l2);
+              const float* s2 = gsize + 3 * g2;
+              const float margin = fmaxf(gmargin[hg], gmargin[g2]);
+              const int key = p * 8;
+              if (t2 == GEOM_SPHERE) {
+                hfield_sphere(co, key, hg, g2, F, hd, hs, nr, nc, p2, s2[0], margin, &trunc);
+              } else if (t2 == GEOM_CAPSULE) {
+                const float* R2 = S + L.gxmat + 9 * l2;
+                const V3 ax = {R2[2], R2[5], R2[8]};
+                int k = key;
+                k += hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 + ax * s2[1], s2[0], margin, &trunc);
+                hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 - ax * s2[1], s2[0], margin, &trunc);
+              } else {
+                atomicOr(&ints[3], 4);
+              }
+            }
+          }
+        }
+        if (trunc) atomicOr(&ints[3], 4);
+      }
+    }
+    sync();
+    STAMP(3);
+    // deterministic order: bitonic sort of (key, slot) over 64 lanes, then permute
+    int ncon = min(ints[0], d.nconmax);
+    {
+      int key = lane < ncon ? Si[L.con_key + lane] : 0x7fffffff;
+      int idx = lane;
+#pragma unroll
+      for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          int pk = __shfl_xor(key, j);
+          int pi = __shfl_xor(idx, j);
+          bool up = (lane & k) == 0;
+          bool lower = (lane & j) == 0;
+          bool sw = lower ? (up ? key > pk : key < pk) : (up ? key < pk : key > pk);
+          if (sw) { key = pk; idx = pi; }
+        }
+      }
+      // lane holds the source slot of sorted position `lane`
+      int g1 = 0, g2 = 0;
+      float dist = 0, px = 0, py = 0, pz = 0, nx = 0, ny = 0, nz = 0;
+      if (lane < ncon) {
+        g1 = Si[L.con_g1 + idx]; g2 = Si[L.con_g2 + idx]; dist = S[L.con_dist + idx];
+        px = S[L.con_pos + 3 * idx]; py = S[L.con_pos + 3 * idx + 1]; pz = S[L.con_pos + 3 * idx + 2];
+        nx = S[L.con_frame + 9 * idx]; ny = S[L.con_frame + 9 * idx + 1]; nz = S[L.con_frame + 9 * idx + 2];
+      }
+      sync();
+      if (lane < ncon) {
+        Si[L.con_g1 + lane] = g1; Si[L.con_g2 + lane] = g2; S[L.con_dist + lane] = dist;
+        {  // con_key is dead after the sort: it now holds the packed contact bodies
+          const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+          Si[L.con_key + lane] = b1 | b2 << 8 | m.body_rootid[b1] << 16 | m.body_rootid[b2] << 24;
+        }
+        S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
+        // contact frame (mju_makeFrame) from the normal
+        V3 n = {nx, ny, nz};
+        n = n * (1.0f / fmaxf(norm(n), MINVAL));
+        V3 t = fabsf(n.y) < 0.5f ? V3{0, 1, 0} : V3{0, 0, 1};
+        t = t - n * dot(n, t);
+        t = t * (1.0f / fmaxf(norm(t), MINVAL));
+        V3 b = cross(n, t);
+        float* fr = S + L.con_frame + 9 * lane;
+        st3(fr, n); st3(fr + 3, t); st3(fr + 6, b);
+        // contact parameters (mj_contactParam semantics)
+        const float* fri = MF(geom_friction);
+        const float* sref = MF(geom_solref);
+        const float* simp = MF(geom_solimp);
+        const float* smix = MF(geom_solmix);
+        const float* gmar = MF(geom_margin);
+        const float* ggap = MF(geom_gap);
+        int p1 = m.geom_priority[g1], p2 = m.geom_priority[g2];
+        int dim;
+        float f0, f1;
+        float sr[2], si[5];
+        if (p1 != p2) {
+          int g = p1 > p2 ? g1 : g2;
+          dim = m.geom_condim[g];
+          f0 = fri[3 * g]; f1 = fri[3 * g + 1];
+          sr[0] = sref[2 * g]; sr[1] = sref[2 * g + 1];
+          for (int i = 0; i < 5; i++) si[i] = simp[5 * g + i];
+        } else {
+          dim = max(m.geom_condim[g1], m.geom_condim[g2]);
+          f0 = fmaxf(fri[3 * g1], fri[3 * g2]);
+          f1 = fmaxf(fri[3 * g1 + 1], fri[3 * g2 + 1]);
+          float s1 = smix[g1], s2 = smix[g2], mix;
+          if (s1 < MINVAL && s2 < MINVAL) mix = 0.5f;
+          else if (s1 < MINVAL) mix = 0.f;
+          else if (s2 < MINVAL) mix = 1.f;
+          else mix = s1 / (s1 + s2);
+          const float* r1 = sref + 2 * g1;
+          const float* r2 = sref + 2 * g2;
+          if (r1[0] > 0 && r2[0] > 0) {
+            sr[0] = mix * r1[0] + (1 - mix) * r2[0];
+            sr[1] = mix * r1[1] + (1 - mix) * r2[1];
+          } else {
+            sr[0] = fminf(r1[0], r2[0]);
+            sr[1] = fminf(r1[1], r2[1]);
+          }
+          for (int i = 0; i < 5; i++) si[i] = mix * simp[5 * g1 + i] + (1 - mix) * simp[5 * g2 + i];
+        }
+        (void)f1;
+        S[L.con_mu + 2 * lane] = fmaxf(MINMU, f0);
+        S[L.con_mu + 2 * lane + 1] = fmaxf(MINMU, f0);
+        Si[L.con_dim + lane] = dim;
+        const float imargin = fmaxf(gmar[g1], gmar[g2]) - fmaxf(ggap[g1], ggap[g2]);
+        S[L.con_imargin + lane] = imargin;
+        // row impedance and reference K, B are per contact: computed once here
+        S[L.con_imp + lane] = impedance(si, dist, imargin);
+        solref_kb(sr, si, h, S[L.con_kb + 2 * lane], S[L.con_kb + 2 * lane + 1]);
+      }
+      sync();
+    }
+    STAMP(4);
+    // =========================================================== constraints
+    {
+      // row counts: limits (lane per joint) then contacts (lane per contact)
+      const float* jrange = MF(jnt_range);
+      const float* jmargin = MF(jnt_margin);
+      int nlim_rows = 0;
+      int lim_mask = 0;  // bit0 lower, bit1 upper
+      if (lane < d.njnt && m.jnt_limited[lane] &&
+          (m.jnt_type[lane] == JNT_HINGE || m.jnt_type[lane] == JNT_SLIDE)) {
+        float q = S[L.qpos + m.jnt_qposadr[lane]];
+        float mg = jmargin[lane];
+        if (q - jrange[2 * lane] < mg) lim_mask |= 1;
+        if (jrange[2 * lane + 1] - q < mg) lim_mask |= 2;
+        nlim_rows = (lim_mask & 1) + ((lim_mask >> 1) & 1);
+      }
+      int lim_total, lim_off = wave_excl_scan(nlim_rows, lane, &lim_total);
+      int cdim = lane < ncon ? Si[L.con_dim + lane] : 0;
+      int crow = lane < ncon ? (cdim == 1 ? 1 : 2 * (cdim - 1)) : 0;
+      if (lane < ncon && cdim != 1 && cdim != 3) atomicOr(&ints[3], 4);
+      int con_total, con_off = wave_excl_scan(crow, lane, &con_total);
+      int nefc = lim_total + con_total;
+      if (nefc > d.njmax) {
+        if (lane == 0) atomicOr(&ints[3], 2);
+      }
+      // contacts whose rows do not fit are dropped as whole contacts
+      int keep_con = ncon;
+      {
+        bool fits = lane < ncon && lim_total + con_off + crow <= d.njmax;
+        unsigned long long bal = __ballot(lane < ncon && !fits);
+        if (bal) keep_con = __ffsll((long long)bal) - 1;
+        keep_con = min(keep_con, ncon);
+      }
+      ncon = keep_con;
+      nefc = lim_total + (ncon > 0 ? __shfl(con_off + crow, ncon - 1) : 0);
+      if (lim_total > d.njmax) { nefc = 0; ncon = 0; }
+      const float* dinvw = MF(dof_invweight0);
+      const float* binvw = MF(body_invweight0);
+      const float* jsolref = MF(jnt_solref);
+      const float* jsolimp = MF(jnt_solimp);
+      // limit rows metadata (J set below) -- lane per joint
+      if (lim_mask && nefc > 0) {
+        int r = lim_off;
+        float q = S[L.qpos + m.jnt_qposadr[lane]];
+        for (int side = -1; side <= 1; side += 2) {
+          if (!((side < 0 ? lim_mask & 1 : lim_mask & 2))) continue;
+          float dist = side * (jrange[2 * lane + (side + 1) / 2] - q);
+          Si[L.efc_cid + r] = efc_code(EFC_LIMIT, lane | m.jnt_dofadr[lane] << 8);
+          S[L.efc_aref + r] = dist;       // temporarily: pos
+          S[L.efc_D + r] = (float)(-side);  // temporarily: jacobian sign
+          r++;
+        }
+      }
+      if (lane < ncon) {
+        int r0 = lim_total + con_off;
+        Si[L.con_efc + lane] = r0;
+        for (int k = 0; k < crow; k++)
+          Si[L.efc_cid + r0 + k] = efc_code(cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, lane);
+      }
+      sync();
+      // Jacobian rows: lane per dof
+      for (int i = lane; i < nvp; i += kWave) {
+        // limits
+        for (int r = 0; r < lim_total && r < nefc; r++) {
+          const int jd = Si[L.efc_cid + r] >> 2;
+          Jg[r * nvp + i] = (jd >> 8) == i ? S[L.efc_D + r] : 0.f;
+        }
+        if (i >= nv) {  // zero padding columns of the contact rows
+          for (int r = lim_total; r < nefc; r++) Jg[r * nvp + i] = 0.f;
+          continue;
+        }
+        uint64_t bm = m.dof_bodymask[i];
+        const float* cd = S + L.cdof + 6 * i;
+        V3 cang = v3(cd), clin = v3(cd + 3);
+        for (int c = 0; c < ncon; c++) {
+          const int cb = Si[L.con_key + c];
+          const int b1 = cb_b1(cb), b2 = cb_b2(cb);
+          V3 pos = v3(S + L.con_pos + 3 * c);
+          V3 jd = {0, 0, 0};
+          if (b2 > 0 && ((bm >> b2) & 1ull))
+            jd = jd + clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r2(cb)));
+          if (b1 > 0 && ((bm >> b1) & 1ull))
+            jd = jd - (clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r1(cb))));
+          const float* fr = S + L.con_frame + 9 * c;
+          float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
+          int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) {
+            Jg[r0 * nvp + i] = jn;
+          } else {
+            float jt1 = fr[3] * jd.x + fr[4] * jd.y + fr[5] * jd.z;
+            float jt2 = fr[6] * jd.x + fr[7] * jd.y + fr[8] * jd.z;
+            float mu0 = S[L.con_mu + 2 * c], mu1 = S[L.con_mu + 2 * c + 1];
+            Jg[(r0 + 0) * nvp + i] = jn + mu0 * jt1;
+            Jg[(r0 + 1) * nvp + i] = jn - mu0 * jt1;
+            Jg[(r0 + 2) * nvp + i] = jn + mu1 * jt2;
+            Jg[(r0 + 3) * nvp + i] = jn - mu1 * jt2;
+          }
+        }
+      }
+      sync();
+      // row parameters: lane per row
+      for (int r = lane; r < nefc; r += kWave) {
+        const int code = Si[L.efc_cid + r];
+        const int type = code & 3, pl = code >> 2;  // pl: contact, or joint | dof << 8
+        float pos, margin, diag, imp, K, B;
+        if (type == EFC_LIMIT) {
+          const int j = pl & 255;
+          pos = S[L.efc_aref + r];
+          margin = jmargin[j];
+          diag = dinvw[pl >> 8];
+          imp = impedance(jsolimp + 5 * j, pos, margin);
+          solref_kb(jsolref + 2 * j, jsolimp + 5 * j, h, K, B);
+        } else {
+          const int c = pl;
+          pos = S[L.con_dist + c];
+          margin = S[L.con_imargin + c];
+          const int cb = Si[L.con_key + c];
+          float tran = binvw[2 * cb_b1(cb)] + binvw[2 * cb_b2(cb)];
+          if (type == EFC_FRICTIONLESS) {
+            diag = tran;
+          } else {
+            float mu = S[L.con_mu + 2 * c + ((r - Si[L.con_efc + c]) >> 1)];
+            diag = (tran + mu * mu * tran) / o.impratio;
+          }
+          imp = S[L.con_imp + c];
+          K = S[L.con_kb + 2 * c];
+          B = S[L.con_kb + 2 * c + 1];
+        }
+        float Rr = fmaxf(MINVAL, (1 - imp) * diag / imp);
+        // efc_vel = J qvel, evaluated from the body velocities (cvel is the same chain sum)
+        float vel;
+        if (type == EFC_LIMIT) {
+          vel = S[L.efc_D + r] * S[L.qvel + (pl >> 8)];
+        } else {
+          const int c = pl;
+          V3 pc = v3(S + L.con_pos + 3 * c);
+          const int cb = Si[L.con_key + c];
+          V3 v = point_vel_r(S, L, cb_b2(cb), cb_r2(cb), pc) - point_vel_r(S, L, cb_b1(cb), cb_r1(cb), pc);
+          const float* fr = S + L.con_frame + 9 * c;
+          vel = fr[0] * v.x + fr[1] * v.y + fr[2] * v.z;
+          if (type != EFC_FRICTIONLESS) {
+            int kr = r - Si[L.con_efc + c];
+            const float* t = fr + 3 * (1 + (kr >> 1));
+            float mu = S[L.con_mu + 2 * c + (kr >> 1)];
+            vel += ((kr & 1) ? -mu : mu) * (t[0] * v.x + t[1] * v.y + t[2] * v.z);
+          }
+        }
+        S[L.efc_D + r] = 1.0f / Rr;
+        S[L.efc_aref + r] = -B * vel - K * imp * (pos - margin);
+      }
+      if (lane == 0) { ints[1] = nefc; ints[2] = lim_total; ints[4] = ncon; }
+      sync();
+    }
+    const int nefc = ints[1];
+    ncon = ints[4];
+    STAMP(5);
+    // =========================================================== sensors
+    for (int s = lane; s < d.nsensor; s += kWave) {
+      float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
+      int obj = m.sensor_objid[s];
+      int type = m.sensor_type[s];
+      // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
+      if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
+      if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
+        int b = m.site_bodyid[obj];
+        const float* R = S + L.sxmat + 9 * obj;
+        const float* cv = S + L.cvel + 6 * b;
+        V3 rel = v3(S + L.sxpos + 3 * obj) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+        V3 r;
+        if (type == SENS_GYRO) {
+          r = mulTv(R, v3(cv));
+        } else {
+          V3 v = v3(cv + 3) + cross(v3(cv), rel);
+          if (type == SENS_VELOCIMETER) {
+            r = mulTv(R, v);
+          } else {
+            const float* ca = S + L.cacc + 6 * b;
+            V3 a = v3(ca + 3) + cross(v3(ca), rel) + cross(v3(cv), v);
+            r = mulTv(R, a);
+          }
+        }
+        out[0] = r.x; out[1] = r.y; out[2] = r.z;
+      } else if (type == SENS_SUBTREEANGMOM) {
+        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+      } else if (type == SENS_FRAMEPOS) {
+        const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
+        out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+      } else if (type == SENS_JOINTPOS) {
+        out[0] = S[L.qpos + m.jnt_qposadr[obj]];
+      } else if (type == SENS_JOINTVEL) {
+        out[0] = S[L.qvel + m.jnt_dofadr[obj]];
+      } else if (type == SENS_CONTACT) {
+        const int32_t* ip = m.sensor_intprm + 3 * s;
+        int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
+        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
+        int dim = m.sensor_dim[s];
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        int found = 0;
+        V3 net = {0, 0, 0};
+        int sel[8];
+        float key[8];
+        int nsel = 0;
+        for (int c = 0; c < ncon; c++) {
+          int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+          bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+          bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+          if (!a1 && !a2) continue;
+          found++;
+          // contact force in contact frame
+          int r0 = Si[L.con_efc + c];
+          V3 f = {0, 0, 0};
+          if (Si[L.con_dim + c] == 1) {
+            f.x = S[L.efc_force + r0];
+          } else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          net = net + fg * (a1 ? 1.f : -1.f);
+          float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
+                  : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
+          if (nsel < nslot || k < key[nsel - 1]) {
+            int pos = nsel < nslot ? nsel++ : nslot - 1;
+            while (pos > 0 && key[pos - 1] > k) { key[pos] = key[pos - 1]; sel[pos] = sel[pos - 1]; pos--; }
+            key[pos] = k;
+            sel[pos] = c * 2 + (a1 ? 0 : 1);
+          }
+        }
+        if (reduce == REDUCE_NETFORCE) {
+          if (bits & 1) out[0] = (float)found;
+          else if (bits & 2) { out[0] = net.x; out[1] = net.y; out[2] = net.z; }
+        } else {
+          for (int k = 0; k < nsel; k++) {
+            int c = sel[k] >> 1;
+            float sg = (sel[k] & 1) ? -1.f : 1.f;
+            float* oo = out + k * fdim;
+            if (bits & 1) oo[0] = (float)found;
+            else if (bits & 8) oo[0] = S[L.con_dist + c];
+            else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 2) {
+              int r0 = Si[L.con_efc + c];
+              if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
+              else {
+                float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+                float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+                oo[0] = e0 + e1 + e2 + e3;
+                oo[1] = (e0 - e1) * S[L.con_mu + 2 * c];
+                oo[2] = (e2 - e3) * S[L.con_mu + 2 * c + 1];
+              }
+            }
+          }
+        }
+      }
+    }
+    STAMP(11);
+    // outputs final after phase A
+#ifdef MJX_ABLATE_OUTPUTS
+    if (false) {
+#else
+    if (last) {
+#endif
+      size_t wb = (size_t)w * nb;
+      for (int i = lane; i < 3 * nb; i += kWave) {
+        D.xpos[wb * 3 + i] = S[L.xpos + i];
+        D.xipos[wb * 3 + i] = S[L.xipos + i];
+        D.subtree_com[wb * 3 + i] = S[L.subtree_com + i];
+        D.subtree_linvel[wb * 3 + i] = S[L.stlin + i];
+        D.subtree_angmom[wb * 3 + i] = S[L.stang + i];
+      }
+      for (int i = lane; i < 4 * nb; i += kWave) D.xquat[wb * 4 + i] = S[L.xquat + i];
+      for (int i = lane; i < 9 * nb; i += kWave) {
+        D.xmat[wb * 9 + i] = S[L.xmat + i];
+        D.ximat[wb * 9 + i] = S[L.ximat + i];
+      }
+      for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
+      // lane per geom: one model-index load per lane up front, not one per element (a
+      // dependent global load in every iteration of an element loop serialises on latency);
+      // heightfield frames are static (set at sim creation)
+      size_t wg = (size_t)w * d.ngeom;
+      for (int i = lane; i < d.ngeom_lds; i += kWave) {
+        const size_t g = wg + m.lds_geom[i];
+        const float* xp = S + L.gxpos + 3 * i;
+        const float* xm = S + L.gxmat + 9 * i;
+        float* op = D.geom_xpos + g * 3;
+        float* om = D.geom_xmat + g * 9;
+#pragma unroll
+        for (int t = 0; t < 3; t++) op[t] = xp[t];
+#pragma unroll
+        for (int t = 0; t < 9; t++) om[t] = xm[t];
+      }
+      size_t ws = (size_t)w * d.nsite;
+      for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
+      for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];
+      for (int i = lane; i < nv; i += kWave) {
+        size_t k = (size_t)w * nv + i;
+        D.qacc_smooth[k] = S[L.qacc_smooth + i];
+        D.qfrc_bias[k] = S[L.qfrc_bias + i];
+        D.qfrc_passive[k] = S[L.qfrc_passive + i];
+        D.qfrc_actuator[k] = S[L.qfrc_act + i];
+        D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
+      }
+      for (int u = lane; u < nu; u += kWave) {
+        size_t k = (size_t)w * nu + u;
+        D.actuator_force[k] = S[L.act_force + u];
+        D.actuator_length[k] = S[L.act_len + u];
+        D.actuator_velocity[k] = S[L.act_vel + u];
+      }
+      size_t wc = (size_t)w * d.nconmax;
+      for (int c = lane; c < d.nconmax; c += kWave) {
+        bool v = c < ncon;
+        D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
+        D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
+        D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
+        for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
+        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? S[L.con_frame + 9 * c + t] : 0.f;
+      }
+      if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
+    }
+    STAMP(12);
+    // hand-off: B pack (J rows already written) and the A part of the C pack
+    const int C = d.nconmax;
+    const int C4 = (C + 3) & ~3;
+    const int nr4 = (nefc + 3) & ~3;
+    cp4(gw + LB.ints, S + L.ints, 8, lane);
+    cp4(gw + LB.qacc_smooth, S + L.qacc_smooth, nvq, lane);
+    cp4(gw + LB.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
+    cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
+    cp4(gw + LB.efc_D, S + L.efc_D, nr4, lane);
+    cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
+    cp4(gc + LC.cdofdot, S + L.cdofdot, 6 * nvp, lane);
+    cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
+    cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
+    cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
+    cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    cp4(gc + LC.act_force, S + L.act_force, (nu + 3) & ~3, lane);
+    cp4(gc + LC.con_g1, S + L.con_g1, C4, lane);
+    cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
+    cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
+    cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_frame, S + L.con_frame, (9 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
+    cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
+    cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
+    cp4(gc + LC.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
+    STAMP(14);
+  } else if constexpr (PH == 1) {
+    // ----------------------------------------------------------- phase B (Newton)
+    {
+      const int nefc_in = reinterpret_cast<const int*>(gw)[LB.ints + 1];
+      // row classes (launch_step): class k > 0 takes row_cap[k-2] < nefc <= row_cap[k-1],
+      // class 0 the worlds above every class capacity (all of them without classes)
+      const int cls = integrate;
+      const int nc = P->nrowclass;
+      const int lo = cls == 0 ? (nc > 0 ? P->row_cap[nc - 1] : -1) : (cls > 1 ? P->row_cap[cls - 2] : -1);
+      if (nefc_in <= lo || (cls > 0 && nefc_in > P->row_cap[cls - 1])) return;
+      if (cls == 0) {
+        cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
+      } else {
+        // the pack is laid out with the full-capacity carve LB: [ints M qacc_smooth
+        // qfrc_smooth efc_aref] sit at the same offsets in both, efc_D and efc_J move
+        const int nr4 = (nefc_in + 3) & ~3;
+        cp_pack(S, gw, LB.efc_aref + nr4, lane);
+        cp_pack(S + L.efc_D, gw + LB.efc_D, nr4, lane);
+        cp_pack(S + L.efc_J, gw + LB.efc_J, nefc_in * nvp, lane);
+      }
+    }
+    const Tiles T = make_tiles(nvp, lane);
+    for (int i = lane; i < nvp; i += kWave) {
+      S[L.x + i] = 0.f; S[L.Mx + i] = 0.f;
+      S[L.srch + i] = 0.f; S[L.Ms + i] = 0.f; S[L.qfrc_con + i] = 0.f;
+      S[L.qacc_ws + i] = i < nv ? D.qacc_warmstart[(size_t)w * nv + i] : 0.f;
+    }
+    lds_dma_wait();
+    sync();
+    const int nefc = ints[1];
+    int ncon = ints[4];
+    (void)ncon;
+    float Mt[2][16];  // M as register tiles; its LDS slot becomes H / jt_mul scratch
+    tiles_load(Mt, T, S + L.M, nvp);
+    sync();
+    STAMP(15);
+    // =========================================================== Newton solver
+    int niter = 0;
+    if (nefc == 0) {
+      for (int i = lane; i < nvp; i += kWave) {
+        S[L.x + i] = S[L.qacc_smooth + i];
+        S[L.qfrc_con + i] = 0.f;
+      }
+      sync();
+    } else {
+      float* jar = S + L.efc_jar;
+      float* Js = S + L.efc_Js;
+      float* wv = S + L.efc_force;
+      const float* Dv = S + L.efc_D;
+      const float* J = S + L.efc_J;
+      int* act = Si + L.efc_act;
+      float* Lm = S + L.H;
+      const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
+#ifdef MJX_STAMPS
+      sub_prev = __builtin_amdgcn_s_memtime();
+#endif
+      // jar = J x - aref for every row (lane per row)
+      auto set_jar = [&](const float* xv) {
+        matvec_rows(jar, J, xv, nefc, nvp, lane);
+        for (int r = lane; r < nefc; r += kWave) jar[r] -= S[L.efc_aref + r];
+      };
+      // total cost at (x, Mx, jar): Gauss term + active half-quadratics (wave-uniform)
+      auto cost_of = [&](const float* xv, const float* Mxv) -> float {
+        float g = 0.f;
+        for (int i = lane; i < nv; i += kWave)
+          g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
+        for (int r = lane; r < nefc; r += kWave) {
+          float v = jar[r];
+          if (v < 0.f) g += 0.5f * Dv[r] * v * v;
+        }
+        return wave_sum(g);
+      };
+      // warmstart: keep qacc_warmstart if its cost beats qacc_smooth
+      for (int i = lane; i < nvp; i += kWave) S[L.x + i] = S[L.qacc_ws + i];
+      sync();
+      tiles_symv(Mt, T, S + L.x, S + L.Mx, nvp, lane);
+      set_jar(S + L.x);
+      sync();
+      const float cost_ws = cost_of(S + L.x, S + L.Mx);
+      sync();
+      set_jar(S + L.qacc_smooth);
+      sync();
+      const float cost_sm = cost_of(S + L.qacc_smooth, S + L.qfrc_smooth);
+      sync();
+      float cost;
+      if (cost_sm < cost_ws) {
+        for (int i = lane; i < nvp; i += kWave) {
+          S[L.x + i] = S[L.qacc_smooth + i];
+          S[L.Mx + i] = S[L.qfrc_smooth + i];
+        }
+        cost = cost_sm;
+      } else {
+        set_jar(S + L.x);
+        cost = cost_ws;
+      }
+      sync();
+      SUBSTAMP(0);
+      unsigned long long act_sig[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+      for (int iter = 0; iter < o.iterations; iter++) {
+        // gradient = M x - qfrc_smooth + J_act^T (D jar)
+        bool same_set;
+        const int nact = build_active(act, jar, nefc, lane, act_sig, &same_set);
+        // H depends on the active set only: unchanged set -> reuse the stored factor (exact)
+        const bool refactor = iter == 0 || !same_set;
+        for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
+        sync();
+        jt_mul(S + L.srch, J, wv, act, nact, nvp, lane);
+        float gn = 0.f, gr = 0.f;
+        for (int i = lane; i < nvp; i += kWave) {
+          const float jf = S[L.srch + i], mx = S[L.Mx + i], fs = S[L.qfrc_smooth + i];
+          const float g = jf + mx - fs;  // gradient
+          S[L.srch + i] = -g;
+          gn += g * g;
+          const float a = fabsf(jf) + fabsf(mx) + fabsf(fs);
+          gr += a * a;
+        }
+        gn = sqrtf(wave_sum(gn));
+        gr = sqrtf(wave_sum(gr));
+        SUBSTAMP(1);
+        // MuJoCo's gradient test; floor = fp32 rounding scale of the summed terms
+        if (iter > 0 && scale * gn < fmaxf(o.tolerance, 16.f * FLT_EPSILON * scale * gr)) break;
+        // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
+        if (refactor) {
+          float A[2][16];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int e2 = 0; e2 < 16; e2++) A[s2][e2] = Mt[s2][e2];
+          tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
+          tiles_store(A, T, Lm, nvp);
+        }
+        sync();
+        SUBSTAMP(2);
+        {
+          float R[NR];
+          float rd;
+          if (refactor) {
+            rows_load<NR>(R, Lm, nvp, lane);
+            rows_chol<NR>(R, rd, nvp, lane);
+            rows_store_strict<NR>(R, rd, Lm, nvp, lane);
+          } else {
+            rows_load_factor<NR>(R, rd, Lm, nvp, lane);
+          }
+          sync();
+          SUBSTAMP(3);
+          float xs = lane < nvp ? S[L.srch + lane] : 0.f;
+          xs = rows_solve<NR>(R, rd, Lm, xs, nvp, lane);
+          if (lane < nvp) S[L.srch + lane] = xs;
+          sync();
+        }
+        SUBSTAMP(4);
+        matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
+        tiles_symv(Mt, T, S + L.srch, S + L.Ms, nvp, lane);
+        float g1 = 0.f, sn = 0.f;
+        for (int i = lane; i < nv; i += kWave) {
+          float sv = S[L.srch + i];
+          g1 += sv * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
+          sn += sv * sv;
+        }
+        sync();
+        float g2 = 0.f;
+        for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
+        g1 = wave_sum(g1);
+        g2 = wave_sum(g2);
+        sn = sqrtf(wave_sum(sn));
+        const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
+        SUBSTAMP(5);
+        // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
+        // The derivative is a sum of O(nefc) terms; once |der| is within its fp32
+        // rounding floor the root of the piecewise-linear derivative has been found to
+        // working precision (gtol itself, 1e-10 relative by default, is an fp64 target).
+        auto ls_eval = [&](float alpha, float* der, float* der2, float* noise) {
+          float f1 = 0.f, f2 = 0.f, fa = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float js = Js[r];
+            float v = jar[r] + alpha * js;
+            if (v < 0) {
+              float Dr = Dv[r];
+              float t = Dr * v * js;
+              f1 += t;
+              fa += fabsf(t);
+              f2 += Dr * js * js;
+            }
+          }
+          f1 = wave_sum(f1);
+          f2 = wave_sum(f2);
+          fa = wave_sum(fa);
+          *der = g1 + alpha * g2 + f1;
+          *der2 = g2 + f2;
+          *noise = 64.f * FLT_EPSILON * (fabsf(g1) + fabsf(alpha * g2) + fa);
+        };
+        float d0, dd0, nz0;
+        ls_eval(0.f, &d0, &dd0, &nz0);
+        float alpha = 0.f;
+        if (d0 < 0) {
+          float c0 = 0.f;
+          for (int r = lane; r < nefc; r += kWave) {
+            float ja = jar[r], js = Js[r];
+            if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
+          }
+          c0 = g2 + wave_sum(c0);
+          float lo = 0.f, hi = -1.f, best = 0.f;
+          float a = -d0 / c0;
+          bool done = false;
+          for (int it = 0; it < o.ls_iterations; it++) {
+            float der, der2, nz;
+            ls_eval(a, &der, &der2, &nz);
+            if (fabsf(der) <= fmaxf(gtol, nz)) { alpha = a; done = true; break; }
+            if (der < 0) { lo = a; best = a; } else { hi = a; }
+            float next = der2 > 0 ? a - der / der2 : a * 2;
+            if (hi >= 0 && !(next > lo && next < hi)) next = 0.5f * (lo + hi);
+            if (hi < 0 && next <= lo) next = lo + (lo > 0 ? lo : 1.0f);
+            a = next;
+          }
+          if (!done) alpha = best > 0 ? best : a;
+        }
+        niter = iter + 1;
+        SUBSTAMP(6);
+        if (alpha == 0.f) break;
+        for (int i = lane; i < nvp; i += kWave) {
+          S[L.x + i] += alpha * S[L.srch + i];
+          S[L.Mx + i] += alpha * S[L.Ms + i];
+        }
+        for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
+        sync();
+        float old = cost;
+        cost = cost_of(S + L.x, S + L.Mx);
+        SUBSTAMP(7);
+        // MuJoCo's improvement test, with the fp32 resolution of the cost (a sum of
+        // non-negative terms, so its rounding error is ~eps*|cost|) as the floor: below
+        // it, further iterations only chase rounding noise.
+        if (scale * (old - cost) < fmaxf(o.tolerance, 4.f * FLT_EPSILON * scale * fabsf(cost))) break;
+      }
+      // constraint forces and qfrc_constraint = J^T f over the active rows
+      sync();
+      for (int r = lane; r < nefc; r += kWave) {
+        float ja = jar[r];
+        wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
+      }
+      unsigned long long sig_f[4] = {0, 0, 0, 0};
+      bool same_f;
+      const int nact = build_active(act, jar, nefc, lane, sig_f, &same_f);
+      sync();
+      jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, lane);
+      SUBSTAMP(8);
+    }
+    STAMP(9);
+    if (lane == 0) ints[5] = niter;
+    sync();
+    cp4(gc + LC.ints, S + L.ints, 8, lane);
+    cp4(gc + LC.x, S + L.x, nvq, lane);
+    cp4(gc + LC.qfrc_con, S + L.qfrc_con, nvq, lane);
+    cp4(gc + LC.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
+    if (last) {
+      for (int i = lane; i < nv; i += kWave) {
+        size_t k = (size_t)w * nv + i;
+        D.qacc[k] = S[L.x + i];
+        D.qfrc_constraint[k] = S[L.qfrc_con + i];
+      }
+      if (lane == 0) D.solver_niter[w] = niter;
+    }
+    STAMP(14);
+  } else {
+    // ----------------------------------------------------------- phase C
+    cp_pack(S, gc, L.pack_len, lane);  // C pack: carve offsets == pack offsets
+    for (int i = lane; i < nvp; i += kWave) {
+      const bool in = i < nv;
+      S[L.qvel + i] = in ? D.qvel[(size_t)w * nv + i] : 0.f;
+      S[L.qacc_ws + i] = in ? D.qacc_warmstart[(size_t)w * nv + i] : 0.f;
+    }
+    for (int i = lane; i < nq; i += kWave) S[L.qpos + i] = D.qpos[(size_t)w * nq + i];
+    float time = D.time[w];
+    const BodyLite B = load_body_lite(m, d, min(lane, nb - 1));
+    const bool bl = lane < nb;
+    lds_dma_wait();
+    sync();
+    const int nefc = ints[1];
+    int ncon = ints[4];
+    const int niter_last = ints[5];
+    STAMP(15);
+    // =========================================================== post-constraint acc
+    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
+    sync();
+    for (int lv = 1; lv < d.nlevel; lv++) {
+      if (bl && B.lv == lv) {
+        const int b = B.b, p = B.p;
+        float a[6];
+        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
+        const int d0 = B.d0, d1 = d0 + B.dn;
+        for (int k = d0; k < d1 && d0 >= 0; k++)
+          for (int j = 0; j < 6; j++)
+            a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
+        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+      }
+      sync();
+    }
+    STAMP(10);
+    // =========================================================== sensors
+    for (int s = lane; s < d.nsensor; s += kWave) {
+      float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
+      int obj = m.sensor_objid[s];
+      int type = m.sensor_type[s];
+      // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
+      if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
+      if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
+        int b = m.site_bodyid[obj];
+        const float* R = S + L.sxmat + 9 * obj;
+        const float* cv = S + L.cvel + 6 * b;
+        V3 rel = v3(S + L.sxpos + 3 * obj) - v3(S + L.subtree_com + 3 * m.body_rootid[b]);
+        V3 r;
+        if (type == SENS_GYRO) {
+          r = mulTv(R, v3(cv));
+        } else {
+          V3 v = v3(cv + 3) + cross(v3(cv), rel);
+          if (type == SENS_VELOCIMETER) {
+            r = mulTv(R, v);
+          } else {
+            const float* ca = S + L.cacc + 6 * b;
+            V3 a = v3(ca + 3) + cross(v3(ca), rel) + cross(v3(cv), v);
+            r = mulTv(R, a);
+          }
+        }
+        out[0] = r.x; out[1] = r.y; out[2] = r.z;
+      } else if (type == SENS_SUBTREEANGMOM) {
+        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+      } else if (type == SENS_FRAMEPOS) {
+        const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
+        out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+      } else if (type == SENS_JOINTPOS) {
+        out[0] = S[L.qpos + m.jnt_qposadr[obj]];
+      } else if (type == SENS_JOINTVEL) {
+        out[0] = S[L.qvel + m.jnt_dofadr[obj]];
+      } else if (type == SENS_CONTACT) {
+        const int32_t* ip = m.sensor_intprm + 3 * s;
+        int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
+        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
+        int dim = m.sensor_dim[s];
+        for (int i = 0; i < dim; i++) out[i] = 0.f;
+        int found = 0;
+        V3 net = {0, 0, 0};
+        int sel[8];
+        float key[8];
+        int nsel = 0;
+        for (int c = 0; c < ncon; c++) {
+          int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+          bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
+          bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
+          if (!a1 && !a2) continue;
+          found++;
+          // contact force in contact frame
+          int r0 = Si[L.con_efc + c];
+          V3 f = {0, 0, 0};
+          if (Si[L.con_dim + c] == 1) {
+            f.x = S[L.efc_force + r0];
+          } else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          net = net + fg * (a1 ? 1.f : -1.f);
+          float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
+                  : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
+          if (nsel < nslot || k < key[nsel - 1]) {
+            int pos = nsel < nslot ? nsel++ : nslot - 1;
+            while (pos > 0 && key[pos - 1] > k) { key[pos] = key[pos - 1]; sel[pos] = sel[pos - 1]; pos--; }
+            key[pos] = k;
+            sel[pos] = c * 2 + (a1 ? 0 : 1);
+          }
+        }
+        if (reduce == REDUCE_NETFORCE) {
+          if (bits & 1) out[0] = (float)found;
+          else if (bits & 2) { out[0] = net.x; out[1] = net.y; out[2] = net.z; }
+        } else {
+          for (int k = 0; k < nsel; k++) {
+            int c = sel[k] >> 1;
+            float sg = (sel[k] & 1) ? -1.f : 1.f;
+            float* oo = out + k * fdim;
+            if (bits & 1) oo[0] = (float)found;
+            else if (bits & 8) oo[0] = S[L.con_dist + c];
+            else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 2) {
+              int r0 = Si[L.con_efc + c];
+              if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
+              else {
+                float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+                float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+                oo[0] = e0 + e1 + e2 + e3;
+                oo[1] = (e0 - e1) * S[L.con_mu + 2 * c];
+                oo[2] = (e2 - e3) * S[L.con_mu + 2 * c + 1];
+              }
+            }
+          }
+        }
+      }
+    }
+    contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon, lane);
+    STAMP(11);
+    if (last) {
+      size_t wb = (size_t)w * nb;
+      for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
+      size_t wc = (size_t)w * d.nconmax;
+      for (int c = lane; c < d.nconmax; c += kWave) {
+        V3 f = {0, 0, 0};
+        if (c < ncon && nefc > 0) {
+          int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) f.x = S[L.efc_force + r0];
+          else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          }
+        }
+        D.contact_force[(wc + c) * 3] = f.x;
+        D.contact_force[(wc + c) * 3 + 1] = f.y;
+        D.contact_force[(wc + c) * 3 + 2] = f.z;
+      }
+      if (lane < 6) {  // per-world counters: [0,1,5] running max, [2..4] event counts
+        int* ws = D.wstats + 8 * (size_t)w;
+        const int v = lane == 0 ? ints[0] : lane == 1 ? nefc : lane == 5 ? niter_last
+                    : (ints[3] >> (lane - 2)) & 1;
+        const int old = ws[lane];
+        ws[lane] = (lane >= 2 && lane <= 4) ? old + v : max(old, v);
+      }
+    }
+    STAMP(12);
+#ifdef MJX_STAMPS
+    sub_prev = __builtin_amdgcn_s_memtime();
+#endif
+    if (integrate) {
+      sync();
+    // =========================================================== implicitfast / Euler
+    sync();
+    {
+      SUBSTAMP(9);
+      // (M + h D) qacc' = qfrc_smooth + qfrc_constraint with the factor phase A stored in
+      // the world's scratch (rows and columns come straight from global memory)
+      SUBSTAMP(10);
+      {
+        float A[NR], rd;
+        rows_load_factor<NR>(A, rd, gf, nvp, lane);
+        const float f = lane < nvp ? S[L.qfrc_smooth + lane] + S[L.qfrc_con + lane] : 0.f;
+        const float acc = rows_solve<NR>(A, rd, gf, f, nvp, lane);
+        if (lane < nv) S[L.qvel + lane] += h * acc;
+      }
+      sync();
+      SUBSTAMP(11);
+      for (int k = lane; k < d.njnt; k += kWave) {
+        int a = m.jnt_qposadr[k], dof = m.jnt_dofadr[k];
+        int t = m.jnt_type[k];
+        if (t == JNT_FREE) {
+          for (int i = 0; i < 3; i++) S[L.qpos + a + i] += h * S[L.qvel + dof + i];
+          V3 wv = v3(S + L.qvel + dof + 3);
+          float nw = norm(wv);
+          V3 ax = nw < MINVAL ? V3{1, 0, 0} : wv * (1.0f / nw);
+          Q4 q = qnorm(q4(S + L.qpos + a + 3));
+          q = qmul(q, qaxisangle(ax, h * nw));
+          st4(S + L.qpos + a + 3, q);
+        } else if (t == JNT_HINGE || t == JNT_SLIDE) {
+          S[L.qpos + a] += h * S[L.qvel + dof];
+        }
+      }
+      for (int i = lane; i < nv; i += kWave) S[L.qacc_ws + i] = S[L.x + i];
+      time += h;
+      sync();
+      SUBSTAMP(12);
+    }
+
+      for (int i = lane; i < nq; i += kWave) D.qpos[(size_t)w * nq + i] = S[L.qpos + i];
+      for (int i = lane; i < nv; i += kWave) {
+        D.qvel[(size_t)w * nv + i] = S[L.qvel + i];
+        D.qacc_warmstart[(size_t)w * nv + i] = S[L.qacc_ws + i];
+      }
+      if (lane == 0) D.time[w] = time;
+    }
+    STAMP(13);
+  }
+  STAMP_FLUSH();
+}
+
+using StepFn = void (*)(const Params*, int, int, int, const uint8_t*);
+
+}  // namespace mjx

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MJX355_LIB", os.path.join(_HERE, "libmjx355.so"))
 EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_model_create",
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
-           "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile",
+           "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile", "mjx_sim_spec",
            "mjx_forward_masked",
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
   L.mjx_expand_field.argtypes = [vp, ctypes.c_char_p, vp]
   L.mjx_field_is_expanded.argtypes = [vp, ctypes.c_char_p]
   L.mjx_sim_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp]
+  L.mjx_sim_spec.argtypes = [vp]
+  L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
   for name in EXPORTS:
     if name.startswith("mjx_task_"):
