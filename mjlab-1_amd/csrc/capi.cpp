@@ -93,6 +93,7 @@ struct mjxSim_ {
   }
   int gC = 0, gF = 0, gstride = 0;
   float* gscr = nullptr;
+  int* wl = nullptr;  // Newton work lists: [nworld] world ids + [2 * (kRowClasses + 1)] segments
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
   std::vector<void*> expanded_allocs;
@@ -111,6 +112,8 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.nrowclass = s->nrowclass;
   for (int k = 0; k < mjx::kRowClasses; k++) p.row_cap[k] = s->row_cap[k];
   p.gscr = s->gscr;
+  p.wl_list = s->wl;
+  p.wl_seg = s->wl ? s->wl + s->nworld : nullptr;
   p.gC = s->gC;
   p.gF = s->gF;
   p.gstride = s->gstride;
@@ -335,6 +338,8 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   }
   if (s->nrowclass > 0) {
     hipError_t e = hipEventCreateWithFlags(&s->side.fork, hipEventDisableTiming);
+    // default priority: measured, high-priority side streams let the few heavy worlds hold
+    // LDS that the bulk of small-class worlds needs (Newton span 214 -> 281 us, G1 4096)
     for (int k = 0; k < s->nrowclass && e == hipSuccess; k++) {
       e = hipStreamCreateWithFlags(&s->side.stream[k], hipStreamNonBlocking);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[k], hipEventDisableTiming);
@@ -364,9 +369,14 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   reserve("__stats", sizeof(int32_t) * 8);
   reserve("__wstats", sizeof(int32_t) * 8 * (size_t)nworld);
   reserve("__prof", sizeof(unsigned long long) * 48);
+  reserve("__wtrace", sizeof(unsigned long long) * 8 * (size_t)nworld);
   hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
   e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->gstride);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
+  e = hipMalloc((void**)&s->wl, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1)));
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc work lists: ") + hipGetErrorString(e)); }
+  e = hipMemset(s->wl, 0, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1)));
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
   e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }
@@ -394,6 +404,11 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   s->fields["engine_counters"] = FieldInfo{s->dd.wstats, false, 8, 1, true, false};
   s->names.push_back("engine_counters");
   s->dd.prof = (unsigned long long*)(base + offs[k++].second);
+  // per-world phase start/end timestamps (s_memrealtime, 100 MHz; diagnostic MJX_STAMPS
+  // build): [A0 A1 B0 B1 C0 C1 - -] as int32 pairs
+  s->dd.wtrace = (unsigned long long*)(base + offs[k++].second);
+  s->fields["world_trace"] = FieldInfo{s->dd.wtrace, false, 16, 1, true, false};
+  s->names.push_back("world_trace");
   s->stats = s->dd.stats;
   // model fields visible as "model.<name>"
   for (auto& kv : model->float_dims) {
@@ -441,6 +456,7 @@ int mjx_sim_destroy(mjxSim* s) {
   if (!s) return 0;
   if (s->arena) (void)hipFree(s->arena);
   if (s->gscr) (void)hipFree(s->gscr);
+  if (s->wl) (void)hipFree(s->wl);
   if (s->dparams) (void)hipFree(s->dparams);
   for (void* p : s->expanded_allocs) (void)hipFree(p);
   delete s;

@@ -10,6 +10,14 @@
 
 namespace mjx {
 
+// register-row length of the dense SPD kernels: exact fits for the shipped robots (Go1 nvp
+// 20, G1 nvp 36), multiples of 8 otherwise (engine.hip generic_fn)
+constexpr int nr_for_nv(int nv) {
+  const int nvp = (nv + 3) & ~3;
+  return nvp <= 8 ? 8 : nvp <= 16 ? 16 : nvp <= 20 ? 20 : nvp <= 24 ? 24 : nvp <= 32 ? 32
+       : nvp <= 36 ? 36 : nvp <= 40 ? 40 : nvp <= 48 ? 48 : nvp <= 56 ? 56 : 64;
+}
+
 // Phase carves.  Masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4
 // (post/integrate).  A phase carve holds only the regions that phase touches (the rest sit
 // past the allocation and are never accessed).  Phase inputs are carved FIRST, in a fixed
@@ -49,6 +57,9 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
     {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, 0},
     {&Lds::red, 5 * kWave, B},
+    // column-block broadcast buffer of the blocked Cholesky (rows_chol): 4 floats per lane;
+    // aliased below into a region that is dead while a factorization runs
+    {&Lds::chol, 4 * kWave, 0},
   };
   int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
                                      &Lds::efc_aref, &Lds::efc_D, &Lds::efc_J};
@@ -77,6 +88,9 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     L.H = L.M;
     L.red = L.M;
     L.efc_Js = L.efc_aref;
+    // the Cholesky stages H in M's slot: rows are loaded before the first column block is
+    // published and the factor is stored after the last (LDS ops of a wave run in order)
+    if (nv * nv >= 4 * kWave) L.chol = L.M;
   }
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
@@ -103,10 +117,14 @@ constexpr Lds make_lds(const Dims& d, int ph) {
       L.gxpos = g2.first;
       L.gxmat = g2.first + gp;
     }
+    // both phase-A factorizations (implicit-integration factor, smooth solve) run after RNE
+    // and before the geom frames are computed: the same dead group holds the Cholesky buffer
+    if (g2.second >= 4 * kWave) L.chol = g2.first;
   }
   const int bit = 1 << ph;
   for (const Slot& sp : all)
     if (sp.mask & bit) take(sp.f);
+  if (ph <= 1) take(&Lds::chol);  // no alias fitted: a slot of its own
   L.total = o;
   return L;
 }

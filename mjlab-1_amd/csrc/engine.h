@@ -67,6 +67,7 @@ struct DData {
   int32_t* stats;   // [8] reduced engine counters (filled by mjx_sim_stats)
   int32_t* wstats;  // [nworld][8] per-world counters (no cross-world atomics in the kernels)
   unsigned long long* prof;  // [48] stage cycle sums (diagnostic -DMJX_STAMPS build)
+  unsigned long long* wtrace;  // [nworld][8] per-world phase start/end s_memrealtime (MJX_STAMPS)
 };
 
 // Per-world LDS carve (offsets in 4-byte words).
@@ -82,6 +83,7 @@ struct Lds {
       con_imp, con_imargin, con_dim, con_efc;
   int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_act, hdiag;
   int red;      // 5*kWave scratch (J^T w partial sums)
+  int chol;     // 4*NR floats: column blocks of the blocked Cholesky (rows_chol)
   int ints;     // small int block: [0]=raw ncon [1]=nefc [2]=nlimit [3]=flags [4]=ncon [5]=niter
   int pack_len; // length of the phase's input pack (carved first; see make_lds)
   int packC_b;  // C carve: offset of the part of the pack written by phase B
@@ -111,6 +113,12 @@ struct Params {
   Lds LP[3 + kRowClasses];
   int nrowclass;                 // row classes in use (0 = every world in LP[1])
   int row_cap[kRowClasses];      // ascending row capacities of the classes
+  // Newton work lists (classify_kernel, every substep between phases A and B): worlds sorted
+  // by constraint-row count, descending; row class k's worlds are wl_list[wl_seg[2k] ..
+  // wl_seg[2k] + wl_seg[2k+1]) -- each class launch takes its worlds densely and largest
+  // first instead of filtering all nworld workgroups.
+  int* wl_list;
+  int* wl_seg;   // [2 * (kRowClasses + 1)]
   float* gscr;   // per-world hand-off scratch: [B pack | C pack | F], gstride floats per world
   int gC;        // offset of the C pack inside a world's scratch
   int gF;        // offset of F: the implicit-integration factor (nvp x nvp rows), read by

@@ -35,6 +35,75 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
   if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
 }
 
+// ------------------------------------------------------------------ Newton work lists
+// One workgroup: counting sort of the worlds by constraint-row count (phase A's D.nefc),
+// descending, then the segment of each row class.  Worlds outside `mask` are not listed.
+// Order within equal row counts follows LDS atomics (each world's result is independent of
+// it).
+constexpr int kClassifyThreads = 1024;
+constexpr int kMaxRowBins = 2048;
+__global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params* __restrict__ P,
+                                                                    int nworld,
+                                                                    const uint8_t* __restrict__ mask) {
+  __shared__ int bin[kMaxRowBins];
+  __shared__ int wsum[kClassifyThreads / kWave];
+  constexpr int nwave = kClassifyThreads / kWave;
+  const int nb = min(P->d.njmax + 1, kMaxRowBins);
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  for (int i = t; i < nb; i += kClassifyThreads) bin[i] = 0;
+  __syncthreads();
+  const int* nefc = P->D.nefc;
+  for (int w = t; w < nworld; w += kClassifyThreads)
+    if (!mask || mask[w]) atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1);
+  __syncthreads();
+  // exclusive scan of the bins in descending row count: bin[r] <- #listed worlds with more
+  // than r rows.  Thread t owns a contiguous chunk of the reversed bin order.
+  const int per = (nb + kClassifyThreads - 1) / kClassifyThreads;
+  const int i0 = min(t * per, nb), i1 = min(i0 + per, nb);
+  int run = 0;
+  for (int i = i0; i < i1; i++) run += bin[nb - 1 - i];
+  int x = run;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wsum[wv] = x;
+  __syncthreads();
+  if (wv == 0) {
+    int v = lane < nwave ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(v, o);
+      if (lane >= o) v += y;
+    }
+    if (lane < nwave) wsum[lane] = v;  // inclusive over waves
+  }
+  __syncthreads();
+  const int total = wsum[nwave - 1];
+  int base = x - run + (wv > 0 ? wsum[wv - 1] : 0);
+  for (int i = i0; i < i1; i++) {
+    const int r = nb - 1 - i, c = bin[r];
+    bin[r] = base;
+    base += c;
+  }
+  __syncthreads();
+  // row class k's segment: class 0 = rows > cap[nc-1] (the front of the list), class k >= 1
+  // = rows in (cap[k-2], cap[k-1]] (class 1 from 0 rows)
+  const int nc = P->nrowclass;
+  if (t <= nc) {
+    const int hi = t == 0 ? nb - 1 : min(P->row_cap[t - 1], nb - 1);
+    const int lo = t == 0 ? (nc > 0 ? P->row_cap[nc - 1] : -1) : (t > 1 ? P->row_cap[t - 2] : -1);
+    const int s0 = bin[hi];
+    const int s1 = lo < 0 ? total : bin[min(lo, nb - 1)];
+    P->wl_seg[2 * t] = s0;
+    P->wl_seg[2 * t + 1] = max(s1 - s0, 0);
+  }
+  __syncthreads();  // the segments read the bins before the scatter advances them
+  for (int w = t; w < nworld; w += kClassifyThreads)
+    if (!mask || mask[w]) P->wl_list[atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1)] = w;
+}
+
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
 template <int NR>
 static StepFn phase_fn_nr(int ph) {
@@ -130,6 +199,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(host, 0), stream, dev, nworld,
                        last, integrate, mask);
     if (nc > 0) {
+      hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, stream, dev, nworld, mask);
       // Newton by row class, concurrently: the full-capacity class (few worlds, long
       // per-world latency) first on a side stream so its blocks dispatch first, the middle
       // classes on further side streams, the smallest (most worlds) on the launch stream.

@@ -377,35 +377,57 @@ __device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int n
     for (int c = 0; c < NR; c++) A[c] = c == lane ? 1.f : 0.f;
   }
 }
-// In-place right-looking Cholesky of the lower triangle: afterwards A[c] (c <= lane) is
-// L[lane][c] and rdiag = 1/L[lane][lane].  Entries above the diagonal are scratch; they
-// never feed the lower part (every broadcast reads a lower entry).
+// In-place blocked right-looking Cholesky of the lower triangle: afterwards A[c] (c <= lane)
+// is L[lane][c] and rdiag = 1/L[lane][lane].  Entries above the diagonal are scratch; they
+// never feed the lower part.  Columns go in blocks of 4: the diagonal block is factored with
+// v_readlane broadcasts (6 per block), then each lane publishes its 4 block entries to
+// `cb` (LDS, 4*64 floats: every lane writes, no branch) and every lane reads the block rows of the trailing columns back
+// as broadcast float4s -- one LDS round trip per 4 columns instead of one v_readlane per
+// trailing element (630 for NR 36).
 template <int NR>
-__device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, int nvp, int lane) {
+__device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, float* cb, int nvp, int lane) {
+  static_assert(NR % 4 == 0, "register rows come in column blocks of 4");
   rdiag = 1.f;
   // Padding rows/cols (>= nvp) are identity/zero, so the full NR sweep is exact there:
   // no per-step guards (guards get hoisted into spilled SGPR masks).
 #pragma unroll
-  for (int j = 0; j < NR; j++) {
-    const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
-    A[j] *= r;
-    rdiag = lane == j ? r : rdiag;
-    // pairs of broadcasts -> one SGPR pair feeding a packed FMA (v_pk_fma_f32)
+  for (int j0 = 0; j0 < NR; j0 += 4) {
 #pragma unroll
-    for (int k = j + 1; k < NR; k += 2) {
-      if (k + 1 < NR) {
-        const float b0 = rl(A[j], k), b1 = rl(A[j], k + 1);
-        A[k] = fmaf(-A[j], b0, A[k]);
-        A[k + 1] = fmaf(-A[j], b1, A[k + 1]);
-      } else {
-        A[k] = fmaf(-A[j], rl(A[j], k), A[k]);
+    for (int t = 0; t < 4; t++) {
+      const int j = j0 + t;
+      const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
+      A[j] *= r;
+      rdiag = lane == j ? r : rdiag;
+#pragma unroll
+      for (int u = t + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
+    }
+    if (j0 + 4 < NR) {
+      st4v(cb + 4 * lane, make_float4(A[j0], A[j0 + 1], A[j0 + 2], A[j0 + 3]));  // all 64 lanes (no branch)
+      sync();
+      // trailing columns in groups of 4 (at most 16 broadcast VGPRs in flight: unbounded,
+      // the scheduler hoists every read of the block and the kernel loses occupancy)
+#pragma unroll
+      for (int k0 = j0 + 4; k0 < NR; k0 += 4) {
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) c[u] = ld4(cb + 4 * (k0 + u));  // row k of the block: broadcast
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          A[k0 + u] = fmaf(-A[j0 + 3], c[u].w, fmaf(-A[j0 + 2], c[u].z,
+                      fmaf(-A[j0 + 1], c[u].y, fmaf(-A[j0], c[u].x, A[k0 + u]))));
       }
+      sync();  // the next block's publish follows these reads
     }
   }
+  (void)nvp;
 }
-// Publish L (row stride nvp): strictly-lower part, 1/L[i][i] on the diagonal, zeros above.
-// The solves never let a diagonal entry reach another lane (a lane's own y is dead once it
-// has been broadcast), so rows_solve can run from these rows (rows_load_factor) as well.
+// The triangular solves run on scaled copies of L so that each of their 2*NR sequential
+// steps is one v_readlane plus one FMA (no per-step rescale or select):
+//   forward  L y = b   as u = diag(L) y:  u_j = b_j - sum_{k<j} M_jk u_k,  M_jk = L_jk / L_kk
+//   backward L^T x = y as v = diag(L) x:  v_j = y_j - sum_{k>j} N_kj v_k,  N_kj = L_kj / L_kk
+// M is column-scaled (register rows, rows_fwd_rows), N row-scaled (published to LDS by
+// rows_store_strict and read back by columns).
+// Publish N (row stride nvp): strictly-lower part, 1/L[i][i] on the diagonal, zeros above.
 template <int NR>
 __device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float rd, float* Lm, int nvp,
                                                   int lane) {
@@ -414,42 +436,44 @@ __device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float rd
   for (int c = 0; c < NR; c += 4)
     if (c < nvp)
       st4v(Lm + lane * nvp + c,
-           make_float4(c < lane ? A[c] : c == lane ? rd : 0.f, c + 1 < lane ? A[c + 1] : c + 1 == lane ? rd : 0.f,
-                       c + 2 < lane ? A[c + 2] : c + 2 == lane ? rd : 0.f,
-                       c + 3 < lane ? A[c + 3] : c + 3 == lane ? rd : 0.f));
+           make_float4(c < lane ? A[c] * rd : c == lane ? rd : 0.f,
+                       c + 1 < lane ? A[c + 1] * rd : c + 1 == lane ? rd : 0.f,
+                       c + 2 < lane ? A[c + 2] * rd : c + 2 == lane ? rd : 0.f,
+                       c + 3 < lane ? A[c + 3] * rd : c + 3 == lane ? rd : 0.f));
 }
-// Rows of a factor stored by rows_store_strict, and this lane's 1/L[i][i].
+// Factor rows L (rows_chol) -> forward rows M (strictly lower, column-scaled).
+template <int NR>
+__device__ __forceinline__ void rows_fwd_rows(float (&A)[NR], float rd, int lane) {
+#pragma unroll
+  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * rl(rd, k) : 0.f;
+}
+// Forward rows M of a factor published by rows_store_strict (M_jk = N_jk L_jj / L_kk), and
+// this lane's 1/L[i][i].
 template <int NR>
 __device__ __forceinline__ void rows_load_factor(float (&A)[NR], float& rd, const float* Lm, int nvp,
                                                  int lane) {
   rows_load<NR>(A, Lm, nvp, lane);
   rd = lane < nvp ? Lm[lane * nvp + lane] : 1.f;
-}
-// x (lane i holds x[i]) <- (L L^T)^-1 x.  Forward from the register rows, backward from
-// columns of the strictly-lower L in Lm (written by rows_store_strict, then synced).
-template <int NR>
-__device__ __forceinline__ float rows_solve(const float (&A)[NR], float rdiag, const float* Lm,
-                                            float x, int nvp, int lane) {
-  float y = x, out = 0.f;
+  const float ljj = __builtin_amdgcn_rcpf(rd);
 #pragma unroll
-  for (int j = 0; j < NR; j++) {
-    const float s = rl(y * rdiag, j);
-    out = lane == j ? s : out;
-    y = fmaf(-(lane > j ? A[j] : 0.f), s, y);
-  }
-  float Lc[NR];
+  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * (rl(rd, k) * ljj) : 0.f;
+}
+// x (lane i holds x[i]) <- (L L^T)^-1 x, from the forward rows M (registers) and the columns
+// of N in Lm (rows_store_strict, then synced).  Lanes >= nvp hold x = 0 and stay 0.
+template <int NR>
+__device__ __forceinline__ float rows_solve(const float (&M)[NR], float rdiag, const float* Lm,
+                                            float x, int nvp, int lane) {
+  float u = x;
+#pragma unroll
+  for (int j = 0; j < NR; j++) u = fmaf(-M[j], rl(u, j), u);  // M[j] = 0 on lanes <= j
+  float Nc[NR];
   const int col = lane < nvp ? lane : 0;
 #pragma unroll
-  for (int j = 0; j < NR; j++) Lc[j] = (j < nvp && lane < nvp) ? Lm[j * nvp + col] : 0.f;
-  y = out;
-  out = 0.f;
+  for (int j = 0; j < NR; j++) Nc[j] = (j < nvp && j > lane) ? Lm[j * nvp + col] : 0.f;
+  float v = u * rdiag;  // y = u / L_jj: the backward sweep starts at v = y
 #pragma unroll
-  for (int j = NR - 1; j >= 0; j--) {
-    const float s = rl(y * rdiag, j);
-    out = lane == j ? s : out;
-    y = fmaf(-Lc[j], s, y);
-  }
-  return out;
+  for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
+  return v * rdiag;
 }
 // Tiles (lower 4x4 blocks) -> LDS matrix (row stride nvp), for rows_load.
 __device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles& T, float* Mm, int nvp) {
@@ -492,7 +516,7 @@ __device__ __forceinline__ void tiles_symv(const float (&A)[2][16], const Tiles&
 // length nvp) in place.  Lm (nvp*nvp) receives the strictly-lower factor.  Lm may alias Mm.
 template <int NR>
 __device__ __forceinline__ void spd_factor_solve(const float* Mm, const float* diag_add, float* Lm,
-                                                 float* v, int nvp, int lane) {
+                                                 float* v, float* cb, int nvp, int lane) {
   float A[NR];
   rows_load<NR>(A, Mm, nvp, lane);
   if (diag_add && lane < nvp) {
@@ -500,8 +524,9 @@ __device__ __forceinline__ void spd_factor_solve(const float* Mm, const float* d
     for (int c = 0; c < NR; c++) A[c] += c == lane ? diag_add[lane] : 0.f;
   }
   float rd;
-  rows_chol<NR>(A, rd, nvp, lane);
+  rows_chol<NR>(A, rd, cb, nvp, lane);
   rows_store_strict<NR>(A, rd, Lm, nvp, lane);
+  rows_fwd_rows<NR>(A, rd, lane);
   sync();
   float x = lane < nvp ? v[lane] : 0.f;
   x = rows_solve<NR>(A, rd, Lm, x, nvp, lane);
@@ -695,13 +720,6 @@ template <int SP> struct ModelSpec {
   static constexpr bool on = false;
   static constexpr Dims dims() { return Dims{}; }
 };
-constexpr int nr_for_nv(int nv) {
-  // register-row length: exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36),
-  // multiples of 8 otherwise (engine.hip step_fn)
-  const int nvp = (nv + 3) & ~3;
-  return nvp <= 8 ? 8 : nvp <= 16 ? 16 : nvp <= 20 ? 20 : nvp <= 24 ? 24 : nvp <= 32 ? 32
-       : nvp <= 36 ? 36 : nvp <= 40 ? 40 : nvp <= 48 ? 48 : nvp <= 56 ? 56 : 64;
-}
 #define MJX_SPEC(id, scene, ...)                                              \
   template <> struct ModelSpec<id> {                                          \
     static constexpr bool on = true;                                          \
@@ -951,7 +969,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate] : lds_of<SP, PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
-  const int w = blockIdx.x;
+  int w = blockIdx.x;
+  if constexpr (PH == 1) {
+    // Newton by row class: workgroup i takes the i-th world of its class's list
+    // (classify_kernel: rows descending, masked worlds only)
+    if (P->nrowclass > 0) {
+      const int* seg = P->wl_seg + 2 * integrate;
+      if (w >= seg[1]) return;
+      w = P->wl_list[seg[0] + w];
+    }
+  }
   if (w >= nworld) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
@@ -967,6 +994,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const float h = o.timestep;
   (void)nq; (void)nu; (void)h;
 #ifdef MJX_STAMPS
+  const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long stamp_prev = __builtin_amdgcn_s_memtime();
   unsigned long long sub_prev = stamp_prev;
   unsigned long long stamp_acc[48];
@@ -1369,11 +1397,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
 #pragma unroll
       for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
       float rd;
-      rows_chol<NR>(A, rd, nvp, lane);
+      rows_chol<NR>(A, rd, S + L.chol, nvp, lane);
       rows_store_strict<NR>(A, rd, gf, nvp, lane);
     }
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
-    spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, nvp, lane);
+    spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
     STAMP(7);
     // linear momentum of subtrees -> velocity of subtree com
     for (int lv = d.nlevel - 2; lv >= 0; lv--) {
@@ -1818,6 +1846,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     const int nefc = ints[1];
     ncon = ints[4];
+    if (lane == 0) D.nefc[w] = nefc;  // every substep: classify_kernel sorts the Newton work by it
     STAMP(5);
     // =========================================================== sensors
     for (int s = lane; s < d.nsensor; s += kWave) {
@@ -2019,12 +2048,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // ----------------------------------------------------------- phase B (Newton)
     {
       const int nefc_in = reinterpret_cast<const int*>(gw)[LB.ints + 1];
-      // row classes (launch_step): class k > 0 takes row_cap[k-2] < nefc <= row_cap[k-1],
-      // class 0 the worlds above every class capacity (all of them without classes)
+      // row classes (launch_step, classify_kernel): class k > 0 holds the worlds with
+      // row_cap[k-2] < nefc <= row_cap[k-1], class 0 the rest (all worlds without classes)
       const int cls = integrate;
-      const int nc = P->nrowclass;
-      const int lo = cls == 0 ? (nc > 0 ? P->row_cap[nc - 1] : -1) : (cls > 1 ? P->row_cap[cls - 2] : -1);
-      if (nefc_in <= lo || (cls > 0 && nefc_in > P->row_cap[cls - 1])) return;
       if (cls == 0) {
         cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
       } else {
@@ -2153,8 +2179,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           float rd;
           if (refactor) {
             rows_load<NR>(R, Lm, nvp, lane);
-            rows_chol<NR>(R, rd, nvp, lane);
+            rows_chol<NR>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
             rows_store_strict<NR>(R, rd, Lm, nvp, lane);
+            rows_fwd_rows<NR>(R, rd, lane);
           } else {
             rows_load_factor<NR>(R, rd, Lm, nvp, lane);
           }
@@ -2499,6 +2526,12 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     STAMP(13);
   }
   STAMP_FLUSH();
+#ifdef MJX_STAMPS
+  if (lane == 0) {
+    D.wtrace[(size_t)w * 8 + 2 * PH] = wt0;
+    D.wtrace[(size_t)w * 8 + 2 * PH + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 using StepFn = void (*)(const Params*, int, int, int, const uint8_t*);

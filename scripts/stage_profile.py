@@ -8,7 +8,7 @@ NAMES = ["kinematics", "com/cinert/cdof", "crb+M", "collision", "contact sort+pa
          "constraints", "velocity+rne+act", "smooth solve", "subtree mom", "newton",
          "post acc", "sensors", "outputs", "integrate", "phase hand-off out", "phase hand-off in"]
 for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
-  N = 4096
+  N = int(os.environ.get("NENV", "4096"))
   env = make_env(task, N, "cuda:0", seed=42)
   env.reset()
   g = torch.Generator(device="cuda:0"); g.manual_seed(0)
