@@ -211,6 +211,23 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     }
     if (upload(anc.data(), sizeof(uint64_t) * anc.size(), &p)) { delete m; return -1; }
     m->dm.dof_ancmask = (const uint64_t*)p;
+    // subtree masks (parents precede children in body order) and the dofs moving each body
+    const int nb = d.nbody;
+    std::vector<uint64_t> sub(nb > 0 ? nb : 1, 0), bdof(nb > 0 ? nb : 1, 0);
+    for (int b = nb - 1; b >= 0; b--) {
+      sub[b] |= 1ull << b;
+      const int par = desc->body_parentid[b];
+      if (b > 0 && par >= 0 && par < b) sub[par] |= sub[b];
+    }
+    for (int b = 0; b < nb; b++) {
+      const int par = desc->body_parentid[b];
+      if (b > 0 && par >= 0 && par < b) bdof[b] = bdof[par];
+      for (int k = 0; k < desc->body_dofnum[b]; k++) bdof[b] |= 1ull << (desc->body_dofadr[b] + k);
+    }
+    if (upload(sub.data(), sizeof(uint64_t) * sub.size(), &p)) { delete m; return -1; }
+    m->dm.body_submask = (const uint64_t*)p;
+    if (upload(bdof.data(), sizeof(uint64_t) * bdof.size(), &p)) { delete m; return -1; }
+    m->dm.body_dofmask = (const uint64_t*)p;
   }
   {
     // Heightfield broadphase tables.  The pair list is [regular pairs | hfield pairs], the

@@ -44,6 +44,8 @@ struct DModel {
 #undef X_FLT
   const uint64_t* dof_bodymask;
   const uint64_t* dof_ancmask;  // bit j set: dof j is dof i itself or an ancestor (host-derived)
+  const uint64_t* body_submask;  // bit c set: body c is in body b's subtree (b included)
+  const uint64_t* body_dofmask;  // bit j set: dof j moves body b (dofs of b and its ancestors)
   // host-derived heightfield broadphase tables (capi.cpp): LDS frame slot per geom (-1 for
   // hfields, whose static frames are computed on the fly), its inverse, hfield geoms with
   // pairs, their pair blocks [hf_pairadr[i], hf_pairadr[i+1]) in the pair tail, and the

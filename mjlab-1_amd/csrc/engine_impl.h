@@ -94,6 +94,12 @@ __device__ __forceinline__ void qmat(float* M, Q4 q) {
   M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
   M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
 }
+// q v q* for a unit quaternion (18 FMAs, no normalisation)
+__device__ __forceinline__ V3 qrot(Q4 q, V3 v) {
+  const V3 u = {q.x, q.y, q.z};
+  const V3 t = cross(u, v) * 2.f;
+  return v + t * q.w + cross(u, t);
+}
 __device__ __forceinline__ Q4 qaxisangle(V3 a, float ang) {
   float s = sinf(0.5f * ang);
   return {cosf(0.5f * ang), a.x * s, a.y * s, a.z * s};
@@ -338,8 +344,9 @@ __device__ __forceinline__ void jt_mul(float* out, const float* J, const float* 
 // the active set of the previous call as 64-row ballots; *same is set when it is unchanged
 // (then H = M + J_act^T D J_act is unchanged too).  Sets over 4*64 rows never compare same.
 __device__ __forceinline__ int build_active(int* act, const float* jar, int nefc, int lane,
-                                            unsigned long long (&sig)[4], bool* same) {
-  int base = 0;
+                                            unsigned long long (&sig)[4], bool* same,
+                                            int* nchg = nullptr) {
+  int base = 0, chg = 0;
   bool eq = nefc <= 4 * kWave;
   for (int r0 = 0, k = 0; r0 < nefc; r0 += kWave, k++) {
     int r = r0 + lane;
@@ -349,10 +356,12 @@ __device__ __forceinline__ int build_active(int* act, const float* jar, int nefc
     base += __popcll(bal);
     if (k < 4) {
       eq = eq && bal == sig[k];
+      chg += __popcll(bal ^ sig[k]);
       sig[k] = bal;
     }
   }
   *same = eq;
+  if (nchg) *nchg = chg;
   return base;
 }
 
@@ -795,6 +804,7 @@ __device__ __forceinline__ V3 point_vel(const float* S, const Lds& L, const DMod
 // cached; further ones (rare) are read from the model arrays.
 struct BodyRec {
   int b, p, lv, j0, jn, jt, qa, da, d0, dn, mocap, root, c0, cn, chp;
+  uint64_t sub, dofs;  // subtree bodies (self included), dofs moving the body
   V3 pos, jpos, jaxis, ipos, inert;
   Q4 quat, iquat;
   float qp0, mass;
@@ -814,6 +824,8 @@ __device__ __forceinline__ BodyRec load_body(const DModel& m, const Dims& d, con
   r.d0 = m.body_dofadr[b]; r.dn = m.body_dofnum[b];
   r.mocap = m.body_mocapid[b];
   r.root = m.body_rootid[b];
+  r.sub = m.body_submask[b];
+  r.dofs = m.body_dofmask[b];
   r.c0 = m.body_childadr[b]; r.cn = m.body_childadr[b + 1] - r.c0;
   r.chp = 0;
   for (int t = 0; t < 5 && t < r.cn; t++) r.chp |= m.body_child[r.c0 + t] << (6 * t);
@@ -837,10 +849,11 @@ __device__ __forceinline__ JntRec jnt_of(const DModel& m, const BodyPtrs& P, con
   const int qa = m.jnt_qposadr[k];
   return {m.jnt_type[k], qa, m.jnt_dofadr[k], v3(P.jpos + 3 * k), v3(P.jaxis + 3 * k), P.qpos0[qa]};
 }
-struct BodyLite { int b, p, lv, d0, dn; };
+struct BodyLite { int b, p, lv, d0, dn; uint64_t dofs; };
 __device__ __forceinline__ BodyLite load_body_lite(const DModel& m, const Dims& d, int i) {
   BodyLite r;
   r.b = m.level_body[i];
+  r.dofs = m.body_dofmask[r.b];
   r.lv = 0;
   for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
   r.p = m.body_parentid[r.b];
@@ -848,7 +861,7 @@ __device__ __forceinline__ BodyLite load_body_lite(const DModel& m, const Dims& 
   return r;
 }
 struct DofRec {
-  int body, jt, qa;
+  int body, jt, qa, pbody, jd0, bd0;  // parent body, first dof of the joint / of the body
   uint64_t anc;
   float arm, damp, stiff, qs;
 };
@@ -1047,6 +1060,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       const float* qspring = MF(qpos_spring);
       Dr.body = m.dof_bodyid[i]; Dr.anc = m.dof_ancmask[i];
       Dr.jt = m.jnt_type[j]; Dr.qa = m.jnt_qposadr[j];
+      Dr.pbody = m.body_parentid[Dr.body]; Dr.jd0 = m.jnt_dofadr[j]; Dr.bd0 = m.body_dofadr[Dr.body];
       Dr.arm = arm[i]; Dr.damp = damping[i]; Dr.stiff = jstiff[j]; Dr.qs = qspring[Dr.qa];
     }
 #ifdef MJX_STAMPS
@@ -1062,54 +1076,88 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     lds_dma_wait();
     sync();
     SUBSTAMP(13);
-    // =========================================================== kinematics (levels)
-    if (lane == 0) {
-      S[L.xpos + 0] = S[L.xpos + 1] = S[L.xpos + 2] = 0;
-      S[L.xquat + 0] = 1; S[L.xquat + 1] = S[L.xquat + 2] = S[L.xquat + 3] = 0;
+    // =========================================================== kinematics
+    // (1) lane per body: the body frame in its parent's frame (body offset, then its
+    //     joints) and the joint anchors / axes in that frame; free-joint, mocap and world
+    //     bodies are absolute (world) frames;
+    // (2) pointer jumping over the tree: T(b) <- T(anc) o T(b), anc <- anc(anc), until every
+    //     chain reaches an absolute frame -- ceil(log2(depth)) rounds of one LDS round trip
+    //     instead of one per tree level;
+    // (3) after the body frames: anchors / axes to the world by the parent frame.
+    int* par = Si + L.stmass;  // scratch ancestor pointers (stmass is written after kinematics)
+    bool absb = false;
+    V3 kpos = {0.f, 0.f, 0.f};
+    Q4 kq = {1.f, 0.f, 0.f, 0.f};
+    if (bl) {
+      const int b = B.b;
+      kpos = B.pos;
+      kq = B.quat;
+      if (b == 0) {
+        kpos = {0.f, 0.f, 0.f};
+        kq = {1.f, 0.f, 0.f, 0.f};
+        absb = true;
+      }
+      if (B.mocap >= 0) {
+        kpos = v3(D.mocap_pos + ((size_t)w * d.nmocap + B.mocap) * 3);
+        kq = q4(D.mocap_quat + ((size_t)w * d.nmocap + B.mocap) * 4);
+        absb = true;
+      }
+      for (int k = B.j0; k < B.j0 + B.jn; k++) {
+        const JntRec J = jnt_of(m, BP, B, k);
+        const int a = J.qa;
+        float R[9];
+        if (J.jt == JNT_FREE) {  // MuJoCo: the only joint of a top-level body
+          kpos = v3(S + L.qpos + a);
+          kq = qnorm(q4(S + L.qpos + a + 3));
+          st3(S + L.xanchor + 3 * k, kpos);
+          qmat(R, kq);
+          st3(S + L.xaxis + 3 * k, mulv(R, J.jaxis));
+          absb = true;
+          continue;
+        }
+        qmat(R, kq);
+        const V3 anchor = mulv(R, J.jpos) + kpos;
+        const V3 axis = mulv(R, J.jaxis);
+        st3(S + L.xanchor + 3 * k, anchor);  // parent frame, to the world in (3)
+        st3(S + L.xaxis + 3 * k, axis);
+        if (J.jt == JNT_HINGE) {
+          kq = qmul(kq, qaxisangle(J.jaxis, S[L.qpos + a] - J.qp0));
+          qmat(R, kq);
+          kpos = anchor - mulv(R, J.jpos);
+        } else if (J.jt == JNT_SLIDE) {
+          kpos = kpos + axis * (S[L.qpos + a] - J.qp0);
+        }
+      }
+      st3(S + L.xpos + 3 * b, kpos);
+      st4(S + L.xquat + 4 * b, kq);
+      par[b] = absb ? 0 : B.p;
     }
     sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      if (bl && B.lv == lv) {
-        const int b = B.b, p = B.p;
-        float Rp[9];
-        qmat(Rp, q4(S + L.xquat + 4 * p));
-        V3 pos = v3(S + L.xpos + 3 * p) + mulv(Rp, B.pos);
-        Q4 q = qmul(q4(S + L.xquat + 4 * p), B.quat);
-        if (B.mocap >= 0) {
-          pos = v3(D.mocap_pos + ((size_t)w * d.nmocap + B.mocap) * 3);
-          q = q4(D.mocap_quat + ((size_t)w * d.nmocap + B.mocap) * 4);
+    {
+      int pa = bl ? par[B.b] : 0;
+      while (__any(pa != 0)) {
+        V3 ppos = {0.f, 0.f, 0.f};
+        Q4 pq = {1.f, 0.f, 0.f, 0.f};
+        int ppa = 0;
+        if (pa != 0) {
+          ppos = v3(S + L.xpos + 3 * pa);
+          pq = q4(S + L.xquat + 4 * pa);
+          ppa = par[pa];
         }
-        for (int k = B.j0; k < B.j0 + B.jn; k++) {
-          const JntRec J = jnt_of(m, BP, B, k);
-          const int a = J.qa;
-          float R[9];
-          if (J.jt == JNT_FREE) {
-            pos = v3(S + L.qpos + a);
-            q = qnorm(q4(S + L.qpos + a + 3));
-            st3(S + L.xanchor + 3 * k, pos);
-            qmat(R, q);
-            st3(S + L.xaxis + 3 * k, mulv(R, J.jaxis));
-            continue;
-          }
-          qmat(R, q);
-          V3 anchor = mulv(R, J.jpos) + pos;
-          V3 axis = mulv(R, J.jaxis);
-          st3(S + L.xanchor + 3 * k, anchor);
-          st3(S + L.xaxis + 3 * k, axis);
-          if (J.jt == JNT_HINGE) {
-            q = qmul(q, qaxisangle(J.jaxis, S[L.qpos + a] - J.qp0));
-            qmat(R, q);
-            pos = anchor - mulv(R, J.jpos);
-          } else if (J.jt == JNT_SLIDE) {
-            pos = pos + axis * (S[L.qpos + a] - J.qp0);
-          }
+        sync();  // every lane's reads precede every lane's writes (one wave: LDS in order)
+        if (pa != 0) {
+          kpos = ppos + qrot(pq, kpos);
+          kq = qmul(pq, kq);
+          st3(S + L.xpos + 3 * B.b, kpos);
+          st4(S + L.xquat + 4 * B.b, kq);
+          par[B.b] = ppa;
+          pa = ppa;
         }
-        q = qnorm(q);
-        st3(S + L.xpos + 3 * b, pos);
-        st4(S + L.xquat + 4 * b, q);
+        sync();
       }
-      sync();
     }
+    if (bl) st4(S + L.xquat + 4 * B.b, qnorm(kq));
+    sync();
     SUBSTAMP(14);
     if (bl) {
       const int b = B.b;
@@ -1121,6 +1169,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       mat3mul(S + L.ximat + 9 * b, R, Ri);
     }
     sync();
+    if (bl && !absb) {  // (3): joint anchors / axes from the parent frame to the world
+      const float* Rp = S + L.xmat + 9 * B.p;
+      const V3 pp = v3(S + L.xpos + 3 * B.p);
+      for (int k = B.j0; k < B.j0 + B.jn; k++) {
+        st3(S + L.xanchor + 3 * k, pp + mulv(Rp, v3(S + L.xanchor + 3 * k)));
+        st3(S + L.xaxis + 3 * k, mulv(Rp, v3(S + L.xaxis + 3 * k)));
+      }
+    }
     {
       const float* spos = MF(site_pos);
       const float* squat = MF(site_quat);
@@ -1135,33 +1191,32 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     STAMP(0);
     // =========================================================== com / cinert / cdof
-    if (bl) {
-      S[L.stmass + B.b] = B.mass;
-      st3(S + L.subtree_com + 3 * B.b, v3(S + L.xipos + 3 * B.b) * B.mass);
-    }
-    sync();
-    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      if (bl && B.lv == lv) {
+    // Subtree sums as broadcast loops: lane b adds body c's term when c is in its subtree
+    // (B.sub); every lane reads the same LDS address per c, no level-by-level syncs.
+    {
+      float* mx = S + L.crb;  // scratch [nb][4] = (m * xipos, m); crb is written below
+      if (bl) {
+        const V3 xi = v3(S + L.xipos + 3 * B.b);
+        st4v(mx + 4 * B.b, make_float4(B.mass * xi.x, B.mass * xi.y, B.mass * xi.z, B.mass));
+      }
+      sync();
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+      for (int c = 0; c < nb; c++) {
+        const float4 v = ld4(mx + 4 * c);
+        const float f = (B.sub >> c) & 1ull ? 1.f : 0.f;
+        acc.x = fmaf(f, v.x, acc.x); acc.y = fmaf(f, v.y, acc.y);
+        acc.z = fmaf(f, v.z, acc.z); acc.w = fmaf(f, v.w, acc.w);
+      }
+      sync();
+      if (bl) {
         const int b = B.b;
-        float ms = S[L.stmass + b];
-        V3 c = v3(S + L.subtree_com + 3 * b);
-        for (int t = 0; t < B.cn; t++) {
-          const int ch = body_child(m, B, t);
-          ms += S[L.stmass + ch];
-          c = c + v3(S + L.subtree_com + 3 * ch);
-        }
-        S[L.stmass + b] = ms;
+        S[L.stmass + b] = acc.w;
+        const V3 c = acc.w > MINVAL ? V3{acc.x, acc.y, acc.z} * (1.0f / acc.w) : v3(S + L.xipos + 3 * b);
         st3(S + L.subtree_com + 3 * b, c);
       }
       sync();
     }
-    if (bl) {
-      const int b = B.b;
-      float ms = S[L.stmass + b];
-      V3 c = ms > MINVAL ? v3(S + L.subtree_com + 3 * b) * (1.0f / ms) : v3(S + L.xipos + 3 * b);
-      st3(S + L.subtree_com + 3 * b, c);
-    }
-    sync();
     if (bl) {
       const int b = B.b;
       float* c = S + L.cinert + 10 * b;
@@ -1223,21 +1278,32 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     sync();
     STAMP(1);
     // =========================================================== CRB + mass matrix
-    for (int i = lane; i < 10 * nb; i += kWave) S[L.crb + i] = S[L.cinert + i];
-    sync();
-    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
-      if (bl && B.lv == lv) {
-        const int b = B.b;
-        float acc[10];
-        for (int j = 0; j < 10; j++) acc[j] = S[L.crb + 10 * b + j];
-        for (int t = 0; t < B.cn; t++) {
-          const int ch = body_child(m, B, t);
-          for (int j = 0; j < 10; j++) acc[j] += S[L.crb + 10 * ch + j];
+    {
+      // composite rigid-body inertia = cinert summed over the subtree (broadcast loop)
+      float acc[10];
+#pragma unroll
+      for (int j = 0; j < 10; j++) acc[j] = 0.f;
+#pragma unroll 4
+      for (int c = 0; c < nb; c++) {
+        const float f = (B.sub >> c) & 1ull ? 1.f : 0.f;
+        const float* ci = S + L.cinert + 10 * c;
+#pragma unroll
+        for (int j = 0; j < 10; j += 2) {
+          const float2 v = *reinterpret_cast<const float2*>(ci + j);
+          acc[j] = fmaf(f, v.x, acc[j]);
+          acc[j + 1] = fmaf(f, v.y, acc[j + 1]);
         }
-        for (int j = 0; j < 10; j++) S[L.crb + 10 * b + j] = acc[j];
       }
-      sync();
+      if (bl && B.b > 0) {  // the world keeps its (zero) cinert
+#pragma unroll
+        for (int j = 0; j < 10; j += 2)
+          *reinterpret_cast<float2*>(S + L.crb + 10 * B.b + j) = make_float2(acc[j], acc[j + 1]);
+      } else if (bl) {
+#pragma unroll
+        for (int j = 0; j < 10; j++) S[L.crb + j] = S[L.cinert + j];
+      }
     }
+    sync();
     for (int i = lane; i < nvp * nvp; i += kWave) S[L.M + i] = 0;
     sync();
     for (int i = nv + lane; i < nvp; i += kWave) S[L.M + i * nvp + i] = 1.f;  // identity padding
@@ -1259,68 +1325,98 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
     STAMP(2);
     // =========================================================== velocity stage
-    if (lane < 6) S[L.cvel + lane] = 0;
-    sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      if (bl && B.lv == lv) {
-        const int b = B.b, p = B.p;
-        float v[6];
-        for (int j = 0; j < 6; j++) v[j] = S[L.cvel + 6 * p + j];
-        for (int k = B.j0; k < B.j0 + B.jn; k++) {
-          const int dof = k == B.j0 ? B.da : m.jnt_dofadr[k];
-          if ((k == B.j0 ? B.jt : m.jnt_type[k]) == JNT_FREE) {
-            for (int a = 0; a < 3; a++) {
-              for (int j = 0; j < 6; j++) S[L.cdofdot + 6 * (dof + a) + j] = 0;
-              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
-            }
-            for (int a = 3; a < 6; a++) cross_motion(S + L.cdofdot + 6 * (dof + a), v, S + L.cdof + 6 * (dof + a));
-            for (int a = 3; a < 6; a++)
-              for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * (dof + a) + j] * S[L.qvel + dof + a];
-          } else {
-            cross_motion(S + L.cdofdot + 6 * dof, v, S + L.cdof + 6 * dof);
-            for (int j = 0; j < 6; j++) v[j] += S[L.cdof + 6 * dof + j] * S[L.qvel + dof];
-          }
+    // cvel(b) = sum over the dofs moving b of cdof * qvel: broadcast loop over the dofs
+    {
+      float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int j = 0; j < nv; j++) {
+        const float f = (B.dofs >> j) & 1ull ? S[L.qvel + j] : 0.f;
+        const float* cd = S + L.cdof + 6 * j;
+#pragma unroll
+        for (int t = 0; t < 6; t += 2) {
+          const float2 c2 = *reinterpret_cast<const float2*>(cd + t);
+          v[t] = fmaf(f, c2.x, v[t]);
+          v[t + 1] = fmaf(f, c2.y, v[t + 1]);
         }
-        for (int j = 0; j < 6; j++) S[L.cvel + 6 * b + j] = v[j];
       }
-      sync();
+      if (bl) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) S[L.cvel + 6 * B.b + t] = v[t];
+      }
     }
-    // RNE (flg_acc = 0): cacc with gravity, body forces into crb scratch (reused as cfrc)
-    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
     sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      if (bl && B.lv == lv) {
-        const int b = B.b, p = B.p;
-        float a[6];
-        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        const int d0 = B.d0, d1 = d0 + B.dn;
-        for (int k = d0; k < d1 && d0 >= 0; k++)
-          for (int j = 0; j < 6; j++) a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k];
-        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+    // cdofdot(j) = (velocity before dof j's joint) x cdof(j), mj_comVel: the parent body's
+    // cvel plus the earlier joints of the same body; a free joint's rotations see its
+    // translations, whose own cdofdot is zero
+    if (lane < nv) {
+      const int j = lane;
+      const bool ftrans = Dr.jt == JNT_FREE && j < Dr.jd0 + 3;
+      float v[6];
+#pragma unroll
+      for (int t = 0; t < 6; t++) v[t] = S[L.cvel + 6 * Dr.pbody + t];
+      for (int e = Dr.bd0; e < j; e++) {
+        if (e >= Dr.jd0 && !(Dr.jt == JNT_FREE && e < Dr.jd0 + 3)) continue;
+        const float q = S[L.qvel + e];
+#pragma unroll
+        for (int t = 0; t < 6; t++) v[t] += S[L.cdof + 6 * e + t] * q;
+      }
+      float* cdd = S + L.cdofdot + 6 * j;
+      if (ftrans) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) cdd[t] = 0.f;
+      } else {
+        cross_motion(cdd, v, S + L.cdof + 6 * j);
+      }
+    }
+    sync();
+    // RNE (flg_acc = 0): cacc(b) = -gravity + sum over the dofs moving b of cdofdot * qvel
+    // (broadcast loop), body forces f(b) into the crb slot (dead after M), then
+    // cfrc(b) = f summed over the subtree into the cacc slot (dead after RNE in phase A)
+    {
+      float a[6] = {0.f, 0.f, 0.f, -o.gravity[0], -o.gravity[1], -o.gravity[2]};
+#pragma unroll 4
+      for (int j = 0; j < nv; j++) {
+        const float f = (B.dofs >> j) & 1ull ? S[L.qvel + j] : 0.f;
+        const float* cd = S + L.cdofdot + 6 * j;
+#pragma unroll
+        for (int t = 0; t < 6; t += 2) {
+          const float2 c2 = *reinterpret_cast<const float2*>(cd + t);
+          a[t] = fmaf(f, c2.x, a[t]);
+          a[t + 1] = fmaf(f, c2.y, a[t + 1]);
+        }
+      }
+      if (bl) {
+        const int b = B.b;
         float f1[6], iv[6], f2[6];
         inert_mul(f1, S + L.cinert + 10 * b, a);
         inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
         cross_force(f2, S + L.cvel + 6 * b, iv);
-        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = f1[j] + f2[j];
+        for (int t = 0; t < 6; t++) S[L.crb + 10 * b + t] = f1[t] + f2[t];
       }
-      sync();
     }
-    for (int lv = d.nlevel - 2; lv >= 1; lv--) {
-      if (bl && B.lv == lv) {
-        const int b = B.b;
-        float acc[6];
-        for (int j = 0; j < 6; j++) acc[j] = S[L.crb + 10 * b + j];
-        for (int t = 0; t < B.cn; t++) {
-          const int ch = body_child(m, B, t);
-          for (int j = 0; j < 6; j++) acc[j] += S[L.crb + 10 * ch + j];
+    sync();
+    {
+      float fr[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int c = 0; c < nb; c++) {
+        const float f = (B.sub >> c) & 1ull ? 1.f : 0.f;
+        const float* fc = S + L.crb + 10 * c;
+#pragma unroll
+        for (int t = 0; t < 6; t += 2) {
+          const float2 c2 = *reinterpret_cast<const float2*>(fc + t);
+          fr[t] = fmaf(f, c2.x, fr[t]);
+          fr[t + 1] = fmaf(f, c2.y, fr[t + 1]);
         }
-        for (int j = 0; j < 6; j++) S[L.crb + 10 * b + j] = acc[j];
       }
-      sync();
+      if (bl) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) S[L.cacc + 6 * B.b + t] = fr[t];
+      }
     }
+    sync();
     if (lane < nv) {
       const int i = lane;
-      S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.crb + 10 * Dr.body);
+      S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.cacc + 6 * Dr.body);  // cfrc
       float pf = -Dr.damp * S[L.qvel + i];
       if ((Dr.jt == JNT_HINGE || Dr.jt == JNT_SLIDE) && Dr.stiff != 0.f)
         pf -= Dr.stiff * (S[L.qpos + Dr.qa] - Dr.qs);
@@ -1365,7 +1461,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       const float* cv = S + L.cvel + 6 * b;
       V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
       V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      st3(S + L.stlin + 3 * b, vc * B.mass);
+      st3(S + L.stlin + 3 * b, vc);  // body com velocity; subtree sums below
       const float* Ri = S + L.ximat + 9 * b;
       V3 wl = mulTv(Ri, v3(cv));
       V3 hl = {B.inert.x * wl.x, B.inert.y * wl.y, B.inert.z * wl.z};
@@ -1403,47 +1499,33 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
     spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
     STAMP(7);
-    // linear momentum of subtrees -> velocity of subtree com
-    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      if (bl && B.lv == lv) {
-        const int b = B.b;
-        V3 acc = v3(S + L.stlin + 3 * b);
-        for (int t = 0; t < B.cn; t++) acc = acc + v3(S + L.stlin + 3 * body_child(m, B, t));
-        st3(S + L.stlin + 3 * b, acc);
-      }
+    // subtree com velocity and angular momentum about the subtree com, as sums over the
+    // subtree (broadcast loop): V = sum m vc / M, L = sum h + sum m (x - X) x (vc - V) --
+    // the closed form of the child-to-parent recursion (parallel-axis shifts)
+    {
+      float* mb = S + L.crb;  // scratch body masses (crb and the RNE forces are dead here)
+      if (bl) mb[B.b] = B.mass;
       sync();
-    }
-    if (bl) {
-      const int b = B.b;
-      float sm = S[L.stmass + b];
-      const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
-      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      V3 lin = sm > MINVAL ? v3(S + L.stlin + 3 * b) * (1.0f / sm) : vc;
-      st3(S + L.stlin + 3 * b, lin);
-    }
-    sync();
-    if (bl && B.b != 0) {
-      const int b = B.b;
-      const float* cv = S + L.cvel + 6 * b;
-      V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
-      V3 vc = v3(cv + 3) + cross(v3(cv), rel);
-      V3 dx = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * b);
-      V3 dp = (vc - v3(S + L.stlin + 3 * b)) * B.mass;
-      st3(S + L.stang + 3 * b, v3(S + L.stang + 3 * b) + cross(dx, dp));
-    }
-    sync();
-    for (int lv = d.nlevel - 2; lv >= 0; lv--) {
-      if (bl && B.lv == lv) {
-        const int p = B.b;
-        V3 acc = v3(S + L.stang + 3 * p);
-        for (int t = 0; t < B.cn; t++) {
-          const int b = body_child(m, B, t);
-          V3 dx = v3(S + L.subtree_com + 3 * b) - v3(S + L.subtree_com + 3 * p);
-          V3 dp = (v3(S + L.stlin + 3 * b) - v3(S + L.stlin + 3 * p)) * S[L.stmass + b];
-          acc = acc + v3(S + L.stang + 3 * b) + cross(dx, dp);
-        }
-        st3(S + L.stang + 3 * p, acc);
+      const V3 X = v3(S + L.subtree_com + 3 * B.b);
+      const V3 vown = v3(S + L.stlin + 3 * B.b);
+      V3 pv = {0.f, 0.f, 0.f}, hs = {0.f, 0.f, 0.f}, cx = {0.f, 0.f, 0.f}, mr = {0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int c = 0; c < nb; c++) {
+        const bool in = (B.sub >> c) & 1ull;
+        const float f = in ? mb[c] : 0.f, fh = in ? 1.f : 0.f;
+        const V3 r = v3(S + L.xipos + 3 * c) - X;
+        const V3 vc = v3(S + L.stlin + 3 * c);
+        pv = pv + vc * f;
+        hs = hs + v3(S + L.stang + 3 * c) * fh;
+        cx = cx + cross(r, vc) * f;
+        mr = mr + r * f;
+      }
+      sync();  // every lane's reads precede the in-place writes
+      if (bl) {
+        const float sm = S[L.stmass + B.b];
+        const V3 V = sm > MINVAL ? pv * (1.0f / sm) : vown;
+        st3(S + L.stlin + 3 * B.b, V);
+        st3(S + L.stang + 3 * B.b, hs + cx - cross(mr, V));
       }
       sync();
     }
@@ -2142,9 +2224,18 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int iter = 0; iter < o.iterations; iter++) {
         // gradient = M x - qfrc_smooth + J_act^T (D jar)
         bool same_set;
-        const int nact = build_active(act, jar, nefc, lane, act_sig, &same_set);
+        int nchg = 0;
+        const int nact = build_active(act, jar, nefc, lane, act_sig, &same_set, &nchg);
         // H depends on the active set only: unchanged set -> reuse the stored factor (exact)
         const bool refactor = iter == 0 || !same_set;
+#ifdef MJX_STAMPS
+        stamp_acc[40] += 1;
+        stamp_acc[41] += refactor && iter > 0;
+        stamp_acc[42] += iter > 0 ? nchg : 0;
+        stamp_acc[43] += refactor && iter > 0 && nchg <= 4;
+        stamp_acc[44] += iter == 0 ? nact : 0;
+#endif
+        (void)nchg;
         for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
         sync();
         jt_mul(S + L.srch, J, wv, act, nact, nvp, lane);
@@ -2323,21 +2414,25 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     const int niter_last = ints[5];
     STAMP(15);
     // =========================================================== post-constraint acc
-    if (lane < 6) S[L.cacc + lane] = lane < 3 ? 0.f : -o.gravity[lane - 3];
-    sync();
-    for (int lv = 1; lv < d.nlevel; lv++) {
-      if (bl && B.lv == lv) {
-        const int b = B.b, p = B.p;
-        float a[6];
-        for (int j = 0; j < 6; j++) a[j] = S[L.cacc + 6 * p + j];
-        const int d0 = B.d0, d1 = d0 + B.dn;
-        for (int k = d0; k < d1 && d0 >= 0; k++)
-          for (int j = 0; j < 6; j++)
-            a[j] += S[L.cdofdot + 6 * k + j] * S[L.qvel + k] + S[L.cdof + 6 * k + j] * S[L.x + k];
-        for (int j = 0; j < 6; j++) S[L.cacc + 6 * b + j] = a[j];
+    // cacc(b) = -gravity + sum over the dofs moving b of cdofdot * qvel + cdof * qacc
+    // (broadcast loop over the dofs, no level syncs)
+    {
+      float a[6] = {0.f, 0.f, 0.f, -o.gravity[0], -o.gravity[1], -o.gravity[2]};
+#pragma unroll 4
+      for (int j = 0; j < nv; j++) {
+        const bool in = (B.dofs >> j) & 1ull;
+        const float fv = in ? S[L.qvel + j] : 0.f, fa = in ? S[L.x + j] : 0.f;
+        const float* cdd = S + L.cdofdot + 6 * j;
+        const float* cd = S + L.cdof + 6 * j;
+#pragma unroll
+        for (int t = 0; t < 6; t++) a[t] = fmaf(fv, cdd[t], fmaf(fa, cd[t], a[t]));
       }
-      sync();
+      if (bl) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) S[L.cacc + 6 * B.b + t] = a[t];
+      }
     }
+    sync();
     STAMP(10);
     // =========================================================== sensors
     for (int s = lane; s < d.nsensor; s += kWave) {

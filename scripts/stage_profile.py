@@ -31,4 +31,8 @@ for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
          "  A: pre: body recs", "  A: pre: dof recs"]
   for i, n in enumerate(SUB):
     print(f"  {n:22s} {d[16 + i] / nsub:10.0f}  {100 * d[16 + i] / max(tot, 1):5.1f}%")
+  it = max(d[40], 1)
+  print(f"  newton: iterations {d[40] / nsub:.2f}/world-substep, refactors after the first {d[41] / nsub:.2f}, "
+        f"changed rows per later iteration {d[42] / max(d[40] - nsub, 1):.2f}, refactors with <=4 changes {d[43] / nsub:.2f}, "
+        f"active rows at iteration 0 {d[44] / nsub:.1f}")
   print("  stats", env.sim.stats(), "mean niter", float(env.sim.field("solver_niter").float().mean()))
