@@ -136,6 +136,116 @@ int mjx_task_observe(mjxTask* task, void* stream);
 size_t mjx_task_desc_size(void);  /* sizeof(mjxTaskDesc): ABI check for FFI bindings */
 const char* mjx_task_last_error(void);
 
+/* ------------------------------------------------------------------------------------
+ * Motion tracking (Mjlab-Tracking-Flat-Unitree-G1): the same fused pattern for the
+ * tracking MDP (tasks/tracking/tracking_env_cfg.py:42-317, tasks/tracking/mdp/{commands,rewards,terminations,observations}.py):
+ *
+ *   mjx_track_action   <- process_action + apply_actions with the encoder bias
+ *                         (joint_actions.py:84-104, entity/entity.py:653-670)
+ *   mjx_track_post     <- episode_length += 1, TerminationManager.compute (time_out,
+ *                         bad_anchor_pos_z_only, bad_anchor_ori, bad_motion_body_pos_z_only),
+ *                         RewardManager.compute (6 exp-kernel tracking terms, action_rate_l2,
+ *                         joint_pos_limits, self_collision_cost), reset bookkeeping
+ *                         (tracking/mdp/terminations.py:18-86, rewards.py:26-120)
+ *   mjx_track_reset    <- _reset_idx for the masked envs after mj_resetData: action /
+ *                         reward / command / event manager resets; the command reset is
+ *                         MotionCommand._resample_command: adaptive failure-binned start
+ *                         sampling + reference-state initialisation (commands.py:258-375)
+ *   mjx_track_observe  <- CommandManager.compute (MotionCommand._update_metrics,
+ *                         _update_command: time step, resampling at the motion end, yaw-
+ *                         aligned relative body targets, adaptive-sampling update),
+ *                         EventManager.apply("interval") (push), ObservationManager.compute
+ *                         (policy 160 / critic 286; tracking/mdp/observations.py:18-69)
+ *
+ * Motion arrays follow the reference's MotionLoader (commands.py:32-68), indexed by the
+ * command's body list.  Randoms: the counter-based hash of mjx_task_*; the multinomial
+ * over failure bins is an inverse-CDF draw from the same probabilities.
+ * ------------------------------------------------------------------------------------ */
+#define MJX_TRACK_MAX_BODIES 32
+#define MJX_TRACK_MAX_BINS 1024
+#define MJX_TRACK_NMETRIC 13
+/* reward kinds (tasks/tracking/mdp/rewards.py, envs/mdp/rewards.py) */
+enum { MJX_TR_ANCHOR_POS = 0, MJX_TR_ANCHOR_ORI = 1, MJX_TR_BODY_POS = 2, MJX_TR_BODY_ORI = 3,
+       MJX_TR_BODY_LIN_VEL = 4, MJX_TR_BODY_ANG_VEL = 5, MJX_TR_ACTION_RATE = 6,
+       MJX_TR_JOINT_LIMIT = 7, MJX_TR_SELF_COLLISION = 8 };
+/* termination kinds (tasks/tracking/mdp/terminations.py, envs/mdp/terminations.py) */
+enum { MJX_TT_TIME_OUT = 0, MJX_TT_ANCHOR_POS_Z = 1, MJX_TT_ANCHOR_ORI = 2, MJX_TT_BODY_POS_Z = 3,
+       MJX_TT_ANCHOR_POS = 4, MJX_TT_BODY_POS = 5 };
+/* observation layout: policy = [command anchor_pos? anchor_ori lin_vel? ang_vel jpos(biased)
+ * jvel actions], critic = [command anchor_pos anchor_ori body_pos body_ori lin_vel ang_vel
+ * jpos jvel actions] (tracking_env_cfg.py:60-110) */
+
+typedef struct mjxTrackDesc_ {
+  int nworld, nq, nv, nu, nsensordata, nbody;
+  float *qpos, *qvel, *ctrl;
+  const float *xpos, *xquat, *cvel, *subtree_com, *sensordata;
+  int root_body, free_q_adr, free_v_adr, njoint;
+  int joint_q_adr[MJX_TASK_MAX_JOINTS], joint_v_adr[MJX_TASK_MAX_JOINTS];
+  int ctrl_of_action[MJX_TASK_MAX_JOINTS], target_of_action[MJX_TASK_MAX_JOINTS];
+  float action_scale[MJX_TASK_MAX_JOINTS], action_offset[MJX_TASK_MAX_JOINTS];
+  float default_joint_pos[MJX_TASK_MAX_JOINTS];
+  float soft_lo[MJX_TASK_MAX_JOINTS], soft_hi[MJX_TASK_MAX_JOINTS];
+  const float* encoder_bias;               /* [nworld, njoint] */
+  const float* env_origins;                /* [nworld, 3] */
+  /* ---- motion (MotionLoader, body-indexed by the command's body list) */
+  int nframe, nmb;                         /* motion frames T, command bodies */
+  const float *m_joint_pos, *m_joint_vel;  /* [T, njoint] */
+  const float *m_body_pos, *m_body_quat, *m_body_lin, *m_body_ang; /* [T, nmb, 3|4] */
+  int robot_body[MJX_TRACK_MAX_BODIES];    /* model body of command body k */
+  int anchor_motion, anchor_body;          /* command index / model body of the anchor */
+  /* ---- timing */
+  float step_dt, episode_length_s;
+  int max_episode_length;
+  /* ---- terms (body terms use bit k of *_bodies for command body k) */
+  int nreward, reward_kind[MJX_TASK_MAX_TERMS];
+  float reward_weight[MJX_TASK_MAX_TERMS], reward_std[MJX_TASK_MAX_TERMS];
+  uint32_t reward_bodies[MJX_TASK_MAX_TERMS];
+  int ntermination, termination_kind[MJX_TASK_MAX_TERMS], termination_is_timeout[MJX_TASK_MAX_TERMS];
+  float termination_threshold[MJX_TASK_MAX_TERMS];
+  uint32_t termination_bodies[MJX_TASK_MAX_TERMS];
+  int selfcol_found_adr, imu_lin_vel_adr, imu_ang_vel_adr;
+  /* ---- command (MotionCommandCfg) */
+  float pose_range[6][2], vel_range[6][2], joint_position_range[2];
+  int sampling_mode;                       /* 0 start, 1 uniform, 2 adaptive */
+  int bin_count, kernel_size;
+  float kernel[8], uniform_ratio, adaptive_alpha;
+  /* ---- events */
+  int has_push;
+  float push_interval[2], push_vel_range[6][2];
+  /* ---- observations */
+  int npolicy, ncritic, corrupt_policy, policy_anchor_pos, policy_lin_vel;
+  float noise_anchor_pos, noise_anchor_ori, noise_lin_vel, noise_ang_vel, noise_joint_pos,
+      noise_joint_vel;
+  uint64_t seed;
+  /* ---- manager state (torch tensors) */
+  float *action, *prev_action, *prev_prev_action, *joint_pos_target; /* [nworld, njoint] */
+  int64_t* episode_length;
+  int64_t* time_steps;                     /* [nworld] motion frame per env */
+  float *body_pos_rel, *body_quat_rel;     /* [nworld, nmb, 3|4] relative body targets */
+  float *bin_failed_count, *current_bin_failed; /* [bin_count] */
+  float* sampling;                         /* [bin_count + 4] scratch: cdf, entropy, top1 */
+  float* metrics;                          /* [MJX_TRACK_NMETRIC, nworld] metric tensors */
+  float* time_left;
+  int64_t* command_counter;
+  float* push_time_left;
+  float* episode_sums;                     /* [nreward, nworld] */
+  float *step_reward, *reward_buf;
+  uint8_t *reset_buf, *terminated, *time_outs, *term_dones, *resample_mask;
+  float *obs_policy, *obs_critic;
+  float *log_reward, *log_termination, *log_metric; /* [nreward] [ntermination] [NMETRIC] */
+  uint64_t* step_counter;
+} mjxTrackDesc;
+
+typedef struct mjxTrack_ mjxTrack;
+int mjx_track_create(const mjxTrackDesc* desc, mjxTrack** out);
+int mjx_track_destroy(mjxTrack* task);
+int mjx_track_action(mjxTrack* task, const float* action, void* stream);
+int mjx_track_post(mjxTrack* task, void* stream);     /* writes reset_buf */
+int mjx_track_reset(mjxTrack* task, void* stream);
+int mjx_track_observe(mjxTrack* task, void* stream);
+size_t mjx_track_desc_size(void);
+const char* mjx_track_last_error(void);
+
 /* out[i] = q1[i] * q2[i] (wxyz Hamilton product) for n contiguous quaternions, in the
  * reference's 8-multiply operation order without FP contraction: bit-identical to its
  * torch quat_mul (src/mjlab/utils/lab_api/math.py:526-563) in eager mode.  Pointers are

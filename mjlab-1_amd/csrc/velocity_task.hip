@@ -443,6 +443,9 @@ __global__ void k_reset(const mjxTaskDesc* __restrict__ T) {
   }
   t.last_time[e] = t.time[e];
   for (int j = 0; j < nj; j++) t.joint_pos_target[(size_t)e * nj + j] = 0.f;
+  // Scene.write_data_to_sim after the reset (manager_based_rl_env.py:296-298): ctrl <- the
+  // cleared targets, which the masked forward then sees
+  for (int k = 0; k < nj; k++) t.ctrl[(size_t)e * t.nu + t.ctrl_of_action[k]] = 0.f;
   // reset_root_state_uniform (events.py:81-120)
   float ps[6], vs[6];
   for (int i = 0; i < 6; i++) {

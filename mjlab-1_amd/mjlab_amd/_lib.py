@@ -23,7 +23,10 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
-           "mjx_task_last_error", "mjx_quat_mul")
+           "mjx_task_last_error", "mjx_quat_mul",
+           # fused tracking-task managers (bound in fused_tracking.py)
+           "mjx_track_create", "mjx_track_destroy", "mjx_track_action", "mjx_track_post",
+           "mjx_track_reset", "mjx_track_observe", "mjx_track_desc_size", "mjx_track_last_error")
 
 _lib = None
 
@@ -63,8 +66,8 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
   for name in EXPORTS:
-    if name.startswith("mjx_task_"):
-      continue  # bound by mjlab_amd.fused
+    if name.startswith(("mjx_task_", "mjx_track_")):
+      continue  # bound by mjlab_amd.fused / mjlab_amd.fused_tracking
     if name not in ("mjx_last_error", "mjx_field_name", "mjx_model_desc_size"):
       getattr(L, name).restype = ci
   from ._capi import ABI_VERSION

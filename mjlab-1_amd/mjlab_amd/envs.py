@@ -237,7 +237,13 @@ class ManagerBasedRlEnv:
     self._fused = None
     if fused and os.environ.get("MJX355_FUSED", "1") != "0":
       from .fused import FusedVelocityStep
+      from .fused_tracking import FusedTrackingStep
       self._fused = FusedVelocityStep.build(self)
+      if self._fused is None:
+        why = getattr(self, "_fused_unsupported", "")
+        self._fused = FusedTrackingStep.build(self)
+        if self._fused is None:
+          self._fused_unsupported = f"velocity: {why}; tracking: {self._fused_unsupported}"
       if self._fused is not None:
         self.extras["log"] = self._fused.log()
     self._graph = None

@@ -348,7 +348,8 @@ class FusedVelocityStep:
     d.step_reward, d.reward_buf = _ptr(rm._step_reward), _ptr(rm._reward_buf)
     # timing
     d.step_dt, d.episode_length_s = float(env.step_dt), float(env.max_episode_length_s)
-    d.max_episode_length = int(env.max_episode_length)
+    # play configs use a 1e9 s episode: clamp into the descriptor's int32 (never reached)
+    d.max_episode_length = min(int(env.max_episode_length), 2 ** 31 - 1)
     _need(env.episode_length_buf.dtype == torch.int64, "episode length dtype")
     d.episode_length = _ptr(env.episode_length_buf, _I64)
     # command
