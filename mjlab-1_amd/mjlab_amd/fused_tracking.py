@@ -115,6 +115,7 @@ class FusedTrackingStep:
   def __init__(self, env):
     self.env = env
     L = lib()
+    _need(hasattr(L, "mjx_track_desc_size"), "library without the tracking kernels")
     L.mjx_track_desc_size.restype = ctypes.c_size_t
     _need(L.mjx_track_desc_size() == ctypes.sizeof(TrackDesc), "mjxTrackDesc layout mismatch")
     L.mjx_track_create.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
