@@ -198,7 +198,12 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     const int last = sub == nsubstep - 1;
     hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(host, 0), stream, dev, nworld,
                        last, integrate, mask);
-    if (nc > 0) {
+    if (nc > 0 && mask) {
+      // masked forward (a few reset worlds): one Newton launch at full capacity over the
+      // masked worlds -- no classify launch, no fork/join latency on this short critical path
+      hipLaunchKernelGGL(fB, dim3(nworld), dim3(kWave), lds_bytes(host, 1), stream, dev, nworld,
+                         last, -1, mask);
+    } else if (nc > 0) {
       hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, stream, dev, nworld, mask);
       // Newton by row class, concurrently: the full-capacity class (few worlds, long
       // per-world latency) first on a side stream so its blocks dispatch first, the middle

@@ -986,7 +986,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   if constexpr (PH == 1) {
     // Newton by row class: workgroup i takes the i-th world of its class's list
     // (classify_kernel: rows descending, masked worlds only)
-    if (P->nrowclass > 0) {
+    if (P->nrowclass > 0 && integrate >= 0) {  // integrate < 0: every world, full carve
       const int* seg = P->wl_seg + 2 * integrate;
       if (w >= seg[1]) return;
       w = P->wl_list[seg[0] + w];
@@ -2133,7 +2133,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       // row classes (launch_step, classify_kernel): class k > 0 holds the worlds with
       // row_cap[k-2] < nefc <= row_cap[k-1], class 0 the rest (all worlds without classes)
       const int cls = integrate;
-      if (cls == 0) {
+      if (cls <= 0) {
         cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
       } else {
         // the pack is laid out with the full-capacity carve LB: [ints M qacc_smooth
