@@ -21,6 +21,11 @@
  *                         velocity_command.py:51-107, event_manager.py:124-146,
  *                         observation_manager.py:154-208)
  *
+ * The same kernels run the jump task (command_kind MJX_CMD_JUMP: JumpCommand,
+ * tasks/jump/mdp/commands.py:17-62; its reward / termination kinds and observation layout,
+ * tasks/jump/jump_env_cfg.py:36-354, including the stateful jump_height_reward and
+ * landing_balance terms, which the reference never resets).
+ *
  * All buffers are device pointers owned by the caller (the torch tensors of the managers
  * and the mjx355 data arena); nothing is copied.  One thread per env; every call is
  * enqueued on `stream` and never synchronises.  Randoms come from a counter-based hash of
@@ -47,12 +52,22 @@ enum { MJX_RW_TRACK_LIN = 0, MJX_RW_TRACK_ANG = 1, MJX_RW_FLAT_ORIENT = 2, MJX_R
        MJX_RW_BODY_ANG_VEL = 4, MJX_RW_ANGMOM = 5, MJX_RW_JOINT_POS_LIMITS = 6,
        MJX_RW_ACTION_RATE = 7, MJX_RW_FEET_AIR_TIME = 8, MJX_RW_FEET_CLEARANCE = 9,
        MJX_RW_FEET_SWING = 10, MJX_RW_FEET_SLIP = 11, MJX_RW_SOFT_LANDING = 12,
-       MJX_RW_SELF_COLLISION = 13 };
+       MJX_RW_SELF_COLLISION = 13,
+       /* jump task (tasks/jump/mdp/rewards.py:20-316, envs/mdp/rewards.py) */
+       MJX_RW_JUMP_HEIGHT = 14, MJX_RW_EXPLOSIVE_TAKEOFF = 15, MJX_RW_SYNC_EXTENSION = 16,
+       MJX_RW_VERTICAL_IMPULSE = 17, MJX_RW_AIR_TIME_BONUS = 18, MJX_RW_LANDING_BALANCE = 19,
+       MJX_RW_SYMMETRIC_LANDING = 20, MJX_RW_ACTION_ACC = 21, MJX_RW_JOINT_TORQUES = 22,
+       MJX_RW_IS_ALIVE = 23 };
 /* termination kinds (envs/mdp/terminations.py, tasks/velocity/mdp/terminations.py) */
-enum { MJX_TM_TIME_OUT = 0, MJX_TM_BAD_ORIENT = 1, MJX_TM_ILLEGAL_CONTACT = 2 };
+enum { MJX_TM_TIME_OUT = 0, MJX_TM_BAD_ORIENT = 1, MJX_TM_ILLEGAL_CONTACT = 2,
+       MJX_TM_ROOT_HEIGHT = 3 /* root_height_below_minimum */,
+       MJX_TM_EXCESSIVE_FORCE = 4 /* jump excessive_landing_force */ };
 /* global per-step metric slots written by reward terms ("Metrics/<name>_mean") */
 enum { MJX_MT_ANGMOM = 0, MJX_MT_AIR_TIME = 1, MJX_MT_PEAK_HEIGHT = 2, MJX_MT_SLIP = 3,
-       MJX_MT_LANDING = 4, MJX_MT_COUNT = 5 };
+       MJX_MT_LANDING = 4, MJX_MT_PEAK_JUMP = 5, MJX_MT_JUMP_HEIGHT = 6,
+       MJX_MT_LANDING_SUCCESS = 7, MJX_MT_COUNT = 8 };
+/* command / observation layouts of the fused step */
+enum { MJX_CMD_TWIST = 0 /* UniformVelocityCommand */, MJX_CMD_JUMP = 1 /* JumpCommand */ };
 
 typedef struct mjxTaskDesc_ {
   int nworld, nq, nv, nu, nsensordata, nbody, nsite;
@@ -121,6 +136,16 @@ typedef struct mjxTaskDesc_ {
   float* log_command;                      /* [2] error_vel_xy, error_vel_yaw */
   float* log_metric;                       /* [MJX_MT_COUNT] */
   uint64_t* step_counter;                  /* [1] env-step counter for the RNG */
+  /* ---- jump task (Mjlab-Jump-Flat-Unitree-G1, tasks/jump/jump_env_cfg.py:36-354) */
+  int command_kind;                        /* MJX_CMD_*: also selects the observation layout */
+  float jump_target_height;                /* JumpCommandCfg.target_height (curriculum) */
+  const float* actuator_force;             /* [nworld, nu] */
+  int act_ctrl[MJX_TASK_MAX_JOINTS];       /* entity actuator i -> ctrl index (actuator order) */
+  uint64_t explosive_joints;               /* explosive_takeoff joint selection (bit per joint) */
+  float *jump_peak, *jump_initial;         /* jump_height_reward state [nworld] */
+  uint8_t* jump_initialized;
+  float* landing_timer;                    /* landing_balance state [nworld] */
+  uint8_t* was_in_air;
 } mjxTaskDesc;
 
 typedef struct mjxTask_ mjxTask;

@@ -115,6 +115,11 @@ __device__ __forceinline__ V3 site_lin_vel(const mjxTaskDesc& t, int e, int site
 __device__ __forceinline__ float command_active(const float* c, float thr) {
   return (sqrtf(c[0] * c[0] + c[1] * c[1]) + fabsf(c[2])) > thr ? 1.f : 0.f;
 }
+// reward-term command gate: the twist command's activity, or none (command_name None, p_nocmd)
+__device__ __forceinline__ float command_gate(const mjxTaskDesc& t, const float* c, float thr,
+                                              float p_nocmd) {
+  return (t.command_kind != MJX_CMD_TWIST || p_nocmd > 0.5f) ? 1.f : command_active(c, thr);
+}
 
 // ----------------------------------------------------------------------------- kernels
 // Thread per (env, joint): a thread-per-env loop serialises every iteration on a global
@@ -170,15 +175,40 @@ __global__ void k_substep(const mjxTaskDesc* __restrict__ T) {
 // Joint sums of the per-joint reward terms, reduced over the env's wave (lane per joint):
 // pose deviation under each std table, soft-limit violation, action rate.  A thread-per-env
 // loop pays two dependent global loads (joint index, then qpos) per joint.
-struct JointSums { float pose[3], lim, rate; };
+struct JointSums { float pose[3], lim, rate, acc2, torque2, power, jv_var; };
 __device__ __forceinline__ float wave_add(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
 __device__ __forceinline__ JointSums joint_sums(const mjxTaskDesc& t, int e, int lane) {
-  JointSums r{{0.f, 0.f, 0.f}, 0.f, 0.f};
+  JointSums r{{0.f, 0.f, 0.f}, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int nj = t.njoint;
+  if (t.command_kind == MJX_CMD_JUMP) {
+    // jump terms (tasks/jump/mdp/rewards.py): action acceleration, actuator torques,
+    // explosive_takeoff's |actuator_force[i] * joint_vel[i]| (actuator i paired with joint i,
+    // as the reference's element-wise product), joint-velocity variance (two passes)
+    float jv_sum = 0.f;
+    for (int j = lane; j < nj; j += 64) {
+      const size_t i = (size_t)e * nj + j;
+      const float a2 = t.action[i] - 2.f * t.prev_action[i] + t.prev_prev_action[i];
+      r.acc2 += a2 * a2;
+      const float f = t.actuator_force[(size_t)e * t.nu + t.act_ctrl[j]];
+      r.torque2 += f * f;
+      const float jv = t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]];
+      if ((t.explosive_joints >> j) & 1ull) r.power += fabsf(f * jv);
+      jv_sum += jv;
+    }
+    const float jv_mean = wave_add(jv_sum) / (float)nj;
+    for (int j = lane; j < nj; j += 64) {
+      const float d = t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]] - jv_mean;
+      r.jv_var += d * d;
+    }
+    r.acc2 = wave_add(r.acc2);
+    r.torque2 = wave_add(r.torque2);
+    r.power = wave_add(r.power);
+    r.jv_var = wave_add(r.jv_var) / (float)nj;
+  }
   for (int j = lane; j < nj; j += 64) {
     const float q = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
     const float d = q - t.default_joint_pos[j];
@@ -216,6 +246,17 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       case MJX_TM_ILLEGAL_CONTACT:
         for (int s = 0; s < t.nillegal; s++) v |= sd[t.illegal_found_adr[s]] > 0.f;
         break;
+      case MJX_TM_ROOT_HEIGHT:  // envs/mdp/terminations.py root_height_below_minimum
+        v = t.xpos[((size_t)e * t.nbody + t.root_body) * 3 + 2] < t.termination_p0[k];
+        break;
+      case MJX_TM_EXCESSIVE_FORCE: {  // tasks/jump/mdp/terminations.py:15-45
+        float fmax = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          const float* fv = sd + t.feet_force_adr[s];
+          fmax = fmaxf(fmax, sqrtf(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]));
+        }
+        v = fmax > t.termination_p0[k];
+      } break;
     }
     if (k < t.ntermination) {
       t.term_dones[(size_t)k * t.nworld + e] = v;
@@ -287,7 +328,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         }
         atomicAdd(&acc->metric_sum[MJX_MT_AIR_TIME], in_air_t);
         atomicAdd(&acc->metric_cnt[MJX_MT_AIR_TIME], in_air_n);
-        f *= command_active(cmd, p2);
+        f *= command_gate(t, cmd, p2, 0.f);
       } break;
       case MJX_RW_FEET_CLEARANCE: {  // rewards.py:155-177 (p0 target, p1 cmd thr)
         for (int s = 0; s < t.nfeet; s++) {
@@ -295,7 +336,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
           V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
           f += fabsf(z - p0) * sqrtf(v.x * v.x + v.y * v.y);
         }
-        f *= command_active(cmd, p1);
+        f *= command_gate(t, cmd, p1, 0.f);
       } break;
       case MJX_RW_FEET_SWING: {  // rewards.py:180-229 (p0 target, p1 cmd thr)
         float land_n = 0.f, land_h = 0.f;
@@ -317,7 +358,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         }
         atomicAdd(&acc->metric_sum[MJX_MT_PEAK_HEIGHT], land_h);
         atomicAdd(&acc->metric_cnt[MJX_MT_PEAK_HEIGHT], land_n);
-        f *= command_active(cmd, p1);
+        f *= command_gate(t, cmd, p1, 0.f);
       } break;
       case MJX_RW_FEET_SLIP: {  // rewards.py:232-259 (p0 cmd thr)
         float vs = 0.f, n = 0.f;
@@ -331,7 +372,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         }
         atomicAdd(&acc->metric_sum[MJX_MT_SLIP], vs);
         atomicAdd(&acc->metric_cnt[MJX_MT_SLIP], n);
-        f *= command_active(cmd, p0);
+        f *= command_gate(t, cmd, p0, 0.f);
       } break;
       case MJX_RW_SOFT_LANDING: {  // rewards.py:262-288 (p0 cmd thr)
         float n = 0.f;
@@ -344,9 +385,71 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         }
         atomicAdd(&acc->metric_sum[MJX_MT_LANDING], f);
         atomicAdd(&acc->metric_cnt[MJX_MT_LANDING], n);
-        f *= command_active(cmd, p0);
+        f *= command_gate(t, cmd, p0, p1);  // p1: command_name None
       } break;
       case MJX_RW_SELF_COLLISION: f = sd[t.selfcol_found_adr]; break;  // rewards.py:88-95
+      // ---- jump task (tasks/jump/mdp/rewards.py; p0 / p1 as noted)
+      case MJX_RW_JUMP_HEIGHT: {  // :20-70, p0 target height, p1 std; stateful, never reset
+        const float hz = t.xpos[((size_t)e * t.nbody + t.root_body) * 3 + 2];
+        float init = t.jump_initialized[e] ? t.jump_initial[e] : hz;
+        t.jump_initial[e] = init;
+        t.jump_initialized[e] = 1;
+        const float peak = fmaxf(t.jump_peak[e], hz);
+        t.jump_peak[e] = peak;
+        const float jump = peak - init;
+        atomicAdd(&acc->metric_sum[MJX_MT_PEAK_JUMP], peak);
+        atomicAdd(&acc->metric_cnt[MJX_MT_PEAK_JUMP], 1.f);
+        atomicAdd(&acc->metric_sum[MJX_MT_JUMP_HEIGHT], jump);
+        atomicAdd(&acc->metric_cnt[MJX_MT_JUMP_HEIGHT], 1.f);
+        f = expf(-((jump - p0) * (jump - p0)) / (p1 * p1));
+      } break;
+      case MJX_RW_EXPLOSIVE_TAKEOFF: {  // :73-108, p0 power threshold
+        bool in_contact = false;
+        for (int s = 0; s < t.nfeet; s++) in_contact |= sd[t.feet_found_adr[s]] > 0.f;
+        f = in_contact ? fmaxf(js.power - p0, 0.f) / 1000.f : 0.f;
+      } break;
+      case MJX_RW_SYNC_EXTENSION: f = js.jv_var; break;  // :111-139
+      case MJX_RW_VERTICAL_IMPULSE:  // :142-167
+        for (int s = 0; s < t.nfeet; s++) f += fmaxf(sd[t.feet_force_adr[s] + 2], 0.f);
+        f /= 500.f;
+        break;
+      case MJX_RW_AIR_TIME_BONUS: {  // :170-204, p0 min air time
+        float amin = 1e30f, in_air_t = 0.f, in_air_n = 0.f;
+        for (int s = 0; s < t.nfeet; s++) {
+          const float at = t.cur_air[(size_t)e * t.nfeet + s];
+          amin = fminf(amin, at);
+          if (at > 0.f) { in_air_t += at; in_air_n += 1.f; }
+        }
+        atomicAdd(&acc->metric_sum[MJX_MT_AIR_TIME], in_air_t);
+        atomicAdd(&acc->metric_cnt[MJX_MT_AIR_TIME], in_air_n);
+        f = fmaxf(expf((amin - p0) / p0) - 1.f, 0.f);
+      } break;
+      case MJX_RW_LANDING_BALANCE: {  // :207-270, p0 stability time; stateful, never reset
+        bool in_contact = false;
+        for (int s = 0; s < t.nfeet; s++) in_contact |= sd[t.feet_found_adr[s]] > 0.f;
+        const bool just_landed = t.was_in_air[e] && in_contact;
+        t.was_in_air[e] = !in_contact;
+        const bool upright = fabsf(r.grav_b.z + 1.f) < 0.2f;
+        const bool low_vel = sqrtf(r.lin_w.x * r.lin_w.x + r.lin_w.y * r.lin_w.y + r.lin_w.z * r.lin_w.z) < 0.5f &&
+                             sqrtf(r.ang_w.x * r.ang_w.x + r.ang_w.y * r.ang_w.y + r.ang_w.z * r.ang_w.z) < 0.5f;
+        const float tm = just_landed ? 0.f : t.landing_timer[e];
+        const float timer = (upright && low_vel && in_contact) ? tm + dt : 0.f;
+        t.landing_timer[e] = timer;
+        atomicAdd(&acc->metric_sum[MJX_MT_LANDING_SUCCESS], timer > p0 ? 1.f : 0.f);
+        atomicAdd(&acc->metric_cnt[MJX_MT_LANDING_SUCCESS], 1.f);
+        f = expf(timer / p0) - 1.f;
+      } break;
+      case MJX_RW_SYMMETRIC_LANDING: {  // :273-316: both feet in first contact
+        bool both = t.nfeet >= 2;
+        for (int s = 0; s < 2 && s < t.nfeet; s++) {
+          const float cc = t.cur_contact[(size_t)e * t.nfeet + s];
+          both = both && cc > 0.f && cc < dt + 1e-8f;
+        }
+        f = both ? 1.f : 0.f;
+      } break;
+      case MJX_RW_ACTION_ACC: f = js.acc2; break;        // envs/mdp/rewards.py:63-70
+      case MJX_RW_JOINT_TORQUES: f = js.torque2; break;  // envs/mdp/rewards.py:32-37
+      case MJX_RW_IS_ALIVE: f = terminated ? 0.f : 1.f; break;  // envs/mdp/rewards.py:22-24
     }
     float v = f * w * dt;
     if (!isfinite(v)) v = 0.f;  // nan_to_num
@@ -482,7 +585,13 @@ __global__ void k_reset(const mjxTaskDesc* __restrict__ T) {
   }
   // command manager reset: counter 0 then resample
   t.command_counter[e] = 0;
-  resample_command(t, e, step, D_CMD_RESET);
+  if (t.command_kind == MJX_CMD_TWIST) {
+    resample_command(t, e, step, D_CMD_RESET);
+  } else {  // JumpCommand._resample_command: the configured target height
+    t.cmd_time_left[e] = uniform(t.resampling_time[0], t.resampling_time[1], urand(seed, e, step, D_CMD_RESET));
+    t.command[e] = t.jump_target_height;
+    t.command_counter[e] += 1;
+  }
   // event manager reset: interval timers
   if (t.has_push)
     t.push_time_left[e] = uniform(t.push_interval[0], t.push_interval[1], urand(seed, e, step, D_CMD_RESET + 16));
@@ -511,6 +620,14 @@ __global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ a
   if (e >= t.nworld) return;
   const uint64_t step = *t.step_counter, seed = t.seed;
   const Root r = root_state(t, e);
+  if (t.command_kind == MJX_CMD_JUMP) {
+    // JumpCommand.compute (tasks/jump/mdp/commands.py:17-62): metrics["target_height"]
+    // filled, timer down (a 1e9 s period never elapses), no command update; no interval
+    // events in the jump task
+    t.metric_err_xy[e] = t.jump_target_height;
+    t.cmd_time_left[e] -= t.step_dt;
+    return;
+  }
   float* c = t.command + (size_t)e * 3;
   // ---- CommandTerm.compute: metrics, timer, resample, heading control (velocity_command.py)
   const float mcs = t.resampling_time[1] / t.step_dt;
@@ -549,8 +666,72 @@ __global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ a
 // ---- observations (observation_manager.py:154-208; velocity_env_cfg.py observation terms),
 // thread per (env, critic element) after k_observe has updated commands and pushes.  Policy
 // element i is the critic's element i (plus noise draw D_NOISE + i); the critic's extras follow.
+// jump layout (tasks/jump/jump_env_cfg.py:61-110): policy = [lin 3, ang 3, gravity 3, jpos,
+// jvel, actions, height 1, vertical velocity 1, contact nf, air time nf, command 1]; critic =
+// policy terms + [foot height nf, sign*log1p|force| 3nf]
+__device__ __forceinline__ void obs_jump(const mjxTaskDesc& t, int e, int i) {
+  const int nj = t.njoint, nf = t.nfeet;
+  const int nput = 9 + 3 * nj + 2 + 2 * nf + 1;
+  const float* sd = t.sensordata + (size_t)e * t.nsensordata;
+  float* co = t.obs_critic + (size_t)e * t.ncritic;
+  if (i < nput) {
+    float val, noise = 0.f;
+    if (i < 3) {
+      val = sd[t.imu_lin_vel_adr + i]; noise = t.noise_lin_vel;
+    } else if (i < 6) {
+      val = sd[t.imu_ang_vel_adr + i - 3]; noise = t.noise_ang_vel;
+    } else if (i < 9) {
+      const V3 g = qapply_inv(t.xquat + ((size_t)e * t.nbody + t.root_body) * 4, V3{0.f, 0.f, -1.f});
+      val = i == 6 ? g.x : i == 7 ? g.y : g.z;
+      noise = t.noise_gravity;
+    } else if (i < 9 + nj) {
+      const int j = i - 9;
+      val = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] - t.default_joint_pos[j];
+      noise = t.noise_joint_pos;
+    } else if (i < 9 + 2 * nj) {
+      val = t.qvel[(size_t)e * t.nv + t.joint_v_adr[i - 9 - nj]]; noise = t.noise_joint_vel;
+    } else if (i < 9 + 3 * nj) {
+      val = t.action[(size_t)e * nj + i - 9 - 2 * nj];
+    } else {
+      const int x = i - 9 - 3 * nj;
+      if (x == 0) {  // height_above_ground: root z (flat terrain height 0, observations.py:19-41)
+        val = t.xpos[((size_t)e * t.nbody + t.root_body) * 3 + 2];
+      } else if (x == 1) {  // vertical_velocity: root_link_lin_vel_w z
+        val = root_state(t, e).lin_w.z;
+      } else if (x < 2 + nf) {
+        val = sd[t.feet_found_adr[x - 2]] > 0.f ? 1.f : 0.f;
+      } else if (x < 2 + 2 * nf) {
+        val = t.cur_air[(size_t)e * nf + x - 2 - nf];
+      } else {
+        val = t.command[e];
+      }
+    }
+    co[i] = val;
+    t.obs_policy[(size_t)e * t.npolicy + i] =
+        t.corrupt_policy && noise > 0.f ? val + uniform(-noise, noise, urand(t.seed, e, *t.step_counter, D_NOISE + i)) : val;
+    return;
+  }
+  const int x = i - nput;
+  float v;
+  if (x < nf) {
+    v = t.site_xpos[((size_t)e * t.nsite + t.foot_site[x]) * 3 + 2];
+  } else {
+    const int y = x - nf, fs = y / 3, k = y % 3;
+    const float fv = sd[t.feet_force_adr[fs] + k];
+    v = copysignf(log1pf(fabsf(fv)), fv) * (fv != 0.f ? 1.f : 0.f);
+  }
+  co[i] = v;
+}
+
 __global__ void k_obs(const mjxTaskDesc* __restrict__ T) {
   const mjxTaskDesc& t = *T;
+  if (t.command_kind == MJX_CMD_JUMP) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= t.nworld * t.ncritic) return;
+    const int e = idx / t.ncritic;
+    obs_jump(t, e, idx - e * t.ncritic);
+    return;
+  }
   const int nj = t.njoint;
   const int nput = 9 + 3 * nj + 3;  // elements shared by the policy and critic groups
   const int nel = t.critic_extras ? nput + 6 * t.nfeet : nput;
@@ -682,10 +863,17 @@ int mjx_task_post(mjxTask* t, void* stream) {
 int mjx_task_reset(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_reset, t->dev); }
 int mjx_task_observe(mjxTask* t, void* stream) {
   if (!t) return task_fail("null task");
-  const int nj = t->host.njoint;
-  const int nel = 9 + 3 * nj + 3 + (t->host.critic_extras ? 6 * t->host.nfeet : 0);
-  if (nel > t->host.ncritic || 9 + 3 * nj + 3 > t->host.npolicy)
-    return task_fail("observation sizes do not match the velocity task layout");
+  const int nj = t->host.njoint, nf = t->host.nfeet;
+  int nel;
+  if (t->host.command_kind == MJX_CMD_JUMP) {
+    nel = t->host.ncritic;
+    if (t->host.npolicy != 9 + 3 * nj + 3 + 2 * nf || nel != t->host.npolicy + 4 * nf)
+      return task_fail("observation sizes do not match the jump task layout");
+  } else {
+    nel = 9 + 3 * nj + 3 + (t->host.critic_extras ? 6 * nf : 0);
+    if (nel > t->host.ncritic || 9 + 3 * nj + 3 > t->host.npolicy)
+      return task_fail("observation sizes do not match the velocity task layout");
+  }
   hipLaunchKernelGGL(mjxt::k_observe, dim3((t->nworld + mjxt::kBlock - 1) / mjxt::kBlock),
                      dim3(mjxt::kBlock), 0, (hipStream_t)stream, t->dev, t->acc);
   const long n = (long)t->nworld * nel;

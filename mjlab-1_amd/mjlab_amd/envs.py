@@ -236,14 +236,17 @@ class ManagerBasedRlEnv:
     self._use_graph = capture
     self._fused = None
     if fused and os.environ.get("MJX355_FUSED", "1") != "0":
-      from .fused import FusedVelocityStep
+      from .fused import FusedJumpStep, FusedVelocityStep
       from .fused_tracking import FusedTrackingStep
-      self._fused = FusedVelocityStep.build(self)
+      why = []
+      for kind, cls in (("velocity", FusedVelocityStep), ("jump", FusedJumpStep),
+                        ("tracking", FusedTrackingStep)):
+        self._fused = cls.build(self)
+        if self._fused is not None:
+          break
+        why.append(f"{kind}: {getattr(self, '_fused_unsupported', '')}")
       if self._fused is None:
-        why = getattr(self, "_fused_unsupported", "")
-        self._fused = FusedTrackingStep.build(self)
-        if self._fused is None:
-          self._fused_unsupported = f"velocity: {why}; tracking: {self._fused_unsupported}"
+        self._fused_unsupported = "; ".join(why)
       if self._fused is not None:
         self.extras["log"] = self._fused.log()
     self._graph = None

@@ -23,7 +23,7 @@ import math
 import numpy as np
 import torch
 
-from . import mdp
+from . import jump, mdp
 from ._lib import MjxError, check, lib
 
 MAXJ, MAXF, MAXT, MAXC = 64, 8, 24, 32
@@ -90,6 +90,10 @@ class TaskDesc(ctypes.Structure):
     ("last_time", _FP), ("peak_heights", _FP), ("obs_policy", _FP), ("obs_critic", _FP),
     ("log_reward", _FP), ("log_termination", _FP), ("log_command", _FP), ("log_metric", _FP),
     ("step_counter", _U64),
+    ("command_kind", ctypes.c_int), ("jump_target_height", ctypes.c_float),
+    ("actuator_force", _FP), ("act_ctrl", ctypes.c_int * MAXJ), ("explosive_joints", ctypes.c_uint64),
+    ("jump_peak", _FP), ("jump_initial", _FP), ("jump_initialized", _U8),
+    ("landing_timer", _FP), ("was_in_air", _U8),
   ]
 
 
@@ -100,8 +104,11 @@ _REWARD_KIND = {
   mdp.feet_clearance: 9, mdp.feet_slip: 11, mdp.soft_landing: 12, mdp.self_collision_cost: 13,
 }
 _METRIC_KEYS = ("Metrics/angular_momentum_mean", "Metrics/air_time_mean", "Metrics/peak_height_mean",
-                "Metrics/slip_velocity_mean", "Metrics/landing_force_mean")
-_METRIC_OF_KIND = {5: 0, 8: 1, 10: 2, 11: 3, 12: 4}
+                "Metrics/slip_velocity_mean", "Metrics/landing_force_mean",
+                "Metrics/peak_jump_height", "Metrics/jump_height", "Metrics/landing_success_rate")
+NMETRIC = len(_METRIC_KEYS)
+_METRIC_OF_KIND = {5: 0, 8: 1, 10: 2, 11: 3, 12: 4, 18: 1}
+_EXCESSIVE_FORCE = (jump.excessive_landing_force,)
 _POLICY = [("base_lin_vel", mdp.builtin_sensor), ("base_ang_vel", mdp.builtin_sensor),
            ("projected_gravity", mdp.projected_gravity), ("joint_pos", mdp.joint_pos_rel),
            ("joint_vel", mdp.joint_vel_rel), ("actions", mdp.last_action),
@@ -171,6 +178,109 @@ class FusedVelocityStep:
   # ------------------------------------------------------------------ descriptor
   def _make_desc(self, env):
     d = TaskDesc()
+    robot, sens = self._base(d, env)
+    scene, nj = env.scene, d.njoint
+    # rewards
+    rm = env.reward_manager
+    _need(len(rm._term_names) <= MAXT, "too many reward terms")
+    d.nreward = len(rm._term_names)
+    feet_sensor = None
+    site_names = None
+    orient_body = -1
+    self._metric_active = [False] * NMETRIC
+    for k, (name, c) in enumerate(zip(rm._term_names, rm._term_cfgs)):
+      f, p = c.func, c.params
+      d.reward_weight[k] = float(c.weight)
+      if isinstance(f, mdp.variable_posture):
+        kind = 3
+        d.reward_p0[k], d.reward_p1[k] = float(p.get("walking_threshold", 0.5)), float(p.get("running_threshold", 1.5))
+        for j in range(nj):
+          d.std_standing[j] = float(f.std_standing[j])
+          d.std_walking[j] = float(f.std_walking[j])
+          d.std_running[j] = float(f.std_running[j])
+        _need(f.std_standing.numel() == nj, "posture over all joints")
+      elif isinstance(f, mdp.feet_swing_height):
+        kind = 10
+        d.reward_p0[k], d.reward_p1[k] = float(p["target_height"]), float(p["command_threshold"])
+        feet_sensor = self._same(feet_sensor, p["sensor_name"])
+        site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
+        self._peak = f.peak_heights
+      else:
+        _need(f in _REWARD_KIND, f"reward term {name}")
+        kind = _REWARD_KIND[f]
+        if kind in (0, 1):
+          d.reward_p0[k] = float(p["std"])
+          _need(p["command_name"] == "twist", "command name")
+        elif kind in (2, 4):
+          orient_body = self._orient(d, k, kind, p, robot, orient_body)
+        elif kind == 5:
+          d.angmom_adr = sens[p["sensor_name"]][0]
+        elif kind == 8:
+          d.reward_p0[k], d.reward_p1[k] = float(p["threshold_min"]), float(p["threshold_max"])
+          d.reward_p2[k] = float(p["command_threshold"])
+          feet_sensor = self._same(feet_sensor, p["sensor_name"])
+        elif kind == 9:
+          d.reward_p0[k], d.reward_p1[k] = float(p["target_height"]), float(p["command_threshold"])
+          site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
+        elif kind == 11:
+          d.reward_p0[k] = float(p["command_threshold"])
+          feet_sensor = self._same(feet_sensor, p["sensor_name"])
+          site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
+        elif kind == 12:
+          d.reward_p0[k] = float(p.get("command_threshold", 0.05))
+          d.reward_p1[k] = float(p.get("command_name") is None)  # ungated
+          feet_sensor = self._same(feet_sensor, p["sensor_name"])
+        elif kind == 13:
+          s = scene[p["sensor_name"]]
+          d.selfcol_found_adr = self._slot_adrs(s, "found")[0]
+      d.reward_kind[k] = kind
+      if c.weight != 0.0 and kind in _METRIC_OF_KIND:
+        self._metric_active[_METRIC_OF_KIND[kind]] = True
+    d.orient_body = orient_body
+    self._feet(d, robot, feet_sensor, site_names)
+    self._terminations(d, env)
+    self._reward_buffers(d, env)
+    # command
+    cm = env.command_manager
+    _need(list(getattr(cm, "_terms", {}).keys()) == ["twist"], "single 'twist' command")
+    ct = cm._terms["twist"]
+    _need(isinstance(ct, mdp.UniformVelocityCommand), "UniformVelocityCommand")
+    cc = ct.cfg
+    _need(float(getattr(cc, "init_velocity_prob", 0.0)) == 0.0, "init_velocity_prob")
+    self._cmd_term = ct
+    self._set_command_ranges(d, cc)
+    d.rel_standing_envs, d.rel_heading_envs = float(cc.rel_standing_envs), float(cc.rel_heading_envs)
+    d.heading_stiffness, d.heading_command = float(cc.heading_control_stiffness), int(bool(cc.heading_command))
+    d.resampling_time[0], d.resampling_time[1] = map(float, cc.resampling_time_range)
+    d.command, d.heading_target = _ptr(ct.vel_command_b), _ptr(ct.heading_target)
+    d.heading_error, d.cmd_time_left = _ptr(ct.heading_error), _ptr(ct.time_left)
+    d.is_heading_env, d.is_standing_env = _ptr(ct.is_heading_env, _U8), _ptr(ct.is_standing_env, _U8)
+    d.command_counter = _ptr(ct.command_counter, _I64)
+    d.metric_err_xy, d.metric_err_yaw = _ptr(ct.metrics["error_vel_xy"]), _ptr(ct.metrics["error_vel_yaw"])
+    self._events(d, env)
+    # observations
+    om = env.observation_manager
+    groups = om._group_obs_term_names
+    _need(set(groups) == {"policy", "critic"}, "policy + critic groups")
+    pol = list(zip(groups["policy"], om._group_obs_term_cfgs["policy"]))
+    cri = list(zip(groups["critic"], om._group_obs_term_cfgs["critic"]))
+    _need([(nme, c.func) for nme, c in pol] == _POLICY, "policy terms")
+    base_c = [(nme, c.func) for nme, c in cri]
+    _need(base_c[:7] == _POLICY and base_c[7:] in ([], _CRITIC_EXTRA), "critic terms")
+    d.critic_extras = int(len(base_c) > 7)
+    if d.critic_extras:
+      _need(cri[8][1].params["sensor_name"] == feet_sensor and
+            tuple(cri[7][1].params["asset_cfg"].site_names) == site_names, "critic feet terms")
+    self._obs_noise(d, env, pol, cri, sens)
+    for i in (5, 6):
+      _need(pol[i][1].noise is None, "noise on actions/command")
+    d.npolicy = 9 + 3 * nj + 3
+    d.ncritic = d.npolicy + (6 * d.nfeet if d.critic_extras else 0)
+    self._io(d, env)
+    return d
+
+  def _base(self, d, env):
+    """Simulation pointers, the joint-position action, joints, default root state, origins."""
     sim, scene, m = env.sim, env.scene, env.sim.mj_model
     dev = torch.device(env.device)
     sd = sim.data
@@ -186,6 +296,7 @@ class FusedVelocityStep:
     (aterm,) = am._terms.values()
     _need(isinstance(aterm, mdp.JointPositionAction), "JointPositionAction only")
     robot = aterm._asset
+    self._robot = robot
     rdata = robot.data
     _need(float(rdata.encoder_bias.abs().max()) == 0.0 if rdata.encoder_bias.numel() else True,
           "encoder bias")
@@ -227,70 +338,22 @@ class FusedVelocityStep:
     # sensors
     sens = {name: (int(m.sensor_adr[i]), int(m.sensor_dim[i])) for i, name in enumerate(m.names["sensor"])}
     d.imu_lin_vel_adr = d.imu_ang_vel_adr = d.angmom_adr = d.selfcol_found_adr = -1
-    # rewards
-    rm = env.reward_manager
-    _need(len(rm._term_names) <= MAXT, "too many reward terms")
-    d.nreward = len(rm._term_names)
-    feet_sensor = None
-    site_names = None
-    orient_body = -1
-    self._metric_active = [False] * 5
-    for k, (name, c) in enumerate(zip(rm._term_names, rm._term_cfgs)):
-      f, p = c.func, c.params
-      d.reward_weight[k] = float(c.weight)
-      if isinstance(f, mdp.variable_posture):
-        kind = 3
-        d.reward_p0[k], d.reward_p1[k] = float(p.get("walking_threshold", 0.5)), float(p.get("running_threshold", 1.5))
-        for j in range(nj):
-          d.std_standing[j] = float(f.std_standing[j])
-          d.std_walking[j] = float(f.std_walking[j])
-          d.std_running[j] = float(f.std_running[j])
-        _need(f.std_standing.numel() == nj, "posture over all joints")
-      elif isinstance(f, mdp.feet_swing_height):
-        kind = 10
-        d.reward_p0[k], d.reward_p1[k] = float(p["target_height"]), float(p["command_threshold"])
-        feet_sensor = self._same(feet_sensor, p["sensor_name"])
-        site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
-        self._peak = f.peak_heights
-      else:
-        _need(f in _REWARD_KIND, f"reward term {name}")
-        kind = _REWARD_KIND[f]
-        if kind in (0, 1):
-          d.reward_p0[k] = float(p["std"])
-          _need(p["command_name"] == "twist", "command name")
-        elif kind in (2, 4):
-          ids = p.get("asset_cfg").body_ids if p.get("asset_cfg") is not None else slice(None)
-          body = self._body_of(robot, ids)
-          if kind == 2:
-            d.reward_p0[k] = float(p["std"])
-          if body is not None:
-            orient_body = self._same(orient_body if orient_body >= 0 else None, body)
-          else:
-            _need(kind == 2, "body_ang_vel needs a body")
-        elif kind == 5:
-          d.angmom_adr = sens[p["sensor_name"]][0]
-        elif kind == 8:
-          d.reward_p0[k], d.reward_p1[k] = float(p["threshold_min"]), float(p["threshold_max"])
-          d.reward_p2[k] = float(p["command_threshold"])
-          feet_sensor = self._same(feet_sensor, p["sensor_name"])
-        elif kind == 9:
-          d.reward_p0[k], d.reward_p1[k] = float(p["target_height"]), float(p["command_threshold"])
-          site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
-        elif kind == 11:
-          d.reward_p0[k] = float(p["command_threshold"])
-          feet_sensor = self._same(feet_sensor, p["sensor_name"])
-          site_names = self._same(site_names, tuple(p["asset_cfg"].site_names))
-        elif kind == 12:
-          d.reward_p0[k] = float(p["command_threshold"])
-          feet_sensor = self._same(feet_sensor, p["sensor_name"])
-        elif kind == 13:
-          s = scene[p["sensor_name"]]
-          d.selfcol_found_adr = self._slot_adrs(s, "found")[0]
-      d.reward_kind[k] = kind
-      if c.weight != 0.0 and kind in _METRIC_OF_KIND:
-        self._metric_active[_METRIC_OF_KIND[kind]] = True
-    d.orient_body = orient_body
-    # feet: contact sensor slots + sites
+    return robot, sens
+
+  def _orient(self, d, k, kind, p, robot, orient_body):
+    ids = p.get("asset_cfg").body_ids if p.get("asset_cfg") is not None else slice(None)
+    body = self._body_of(robot, ids)
+    if kind == 2:
+      d.reward_p0[k] = float(p["std"])
+    if body is not None:
+      return self._same(orient_body if orient_body >= 0 else None, body)
+    _need(kind == 2, "body_ang_vel needs a body")
+    return orient_body
+
+  def _feet(self, d, robot, feet_sensor, site_names):
+    """Feet: contact-sensor slots (found / force, air-time buffers) and foot sites."""
+    scene, n, dev = self.env.scene, self.env.num_envs, torch.device(self.env.device)
+    idx = robot.indexing
     _need(feet_sensor is not None and site_names is not None, "feet terms")
     fs = scene[feet_sensor]
     found, force = self._slot_adrs(fs, "found"), self._slot_adrs(fs, "force")
@@ -312,7 +375,9 @@ class FusedVelocityStep:
     if not hasattr(self, "_peak"):
       self._peak = torch.zeros(n, d.nfeet, device=dev)
     d.peak_heights = _ptr(self._peak)
-    # terminations
+
+  def _terminations(self, d, env):
+    scene, n, dev = env.scene, env.num_envs, torch.device(env.device)
     tm = env.termination_manager
     d.ntermination = len(tm._term_names)
     for k, (name, c) in enumerate(zip(tm._term_names, tm._term_cfgs)):
@@ -321,6 +386,14 @@ class FusedVelocityStep:
       elif c.func is mdp.bad_orientation:
         d.termination_kind[k] = 1
         d.termination_p0[k] = float(c.params["limit_angle"])
+      elif c.func is mdp.root_height_below_minimum:
+        d.termination_kind[k] = 3
+        _need(c.params.get("asset_cfg") is None or c.params["asset_cfg"].name == "robot", "root height asset")
+        d.termination_p0[k] = float(c.params["minimum_height"])
+      elif c.func in _EXCESSIVE_FORCE:
+        d.termination_kind[k] = 4
+        _need(scene[c.params["sensor_name"]] is self._feet_sensor, "impact sensor is the feet sensor")
+        d.termination_p0[k] = float(c.params.get("force_threshold", 2500.0))
       elif c.func is mdp.illegal_contact:
         d.termination_kind[k] = 2
         adrs = self._slot_adrs(scene[c.params["sensor_name"]], "found")
@@ -339,7 +412,11 @@ class FusedVelocityStep:
     d.time_outs = _ptr(tm._truncated_buf, _U8)
     self.reset_buf = torch.zeros(n, dtype=torch.bool, device=dev)
     d.reset_buf = _ptr(self.reset_buf, _U8)
-    # reward buffers: episode sums as rows of one [nreward, n] tensor
+    self._term_names = list(tm._term_names)
+
+  def _reward_buffers(self, d, env):
+    """Episode sums as rows of one [nreward, n] tensor; step reward / reward buffers; timing."""
+    rm, n, dev = env.reward_manager, env.num_envs, torch.device(env.device)
     self._episode_sums = torch.zeros(max(d.nreward, 1), n, device=dev)
     for k, name in enumerate(rm._term_names):
       self._episode_sums[k].copy_(rm._episode_sums[name])
@@ -352,24 +429,11 @@ class FusedVelocityStep:
     d.max_episode_length = min(int(env.max_episode_length), 2 ** 31 - 1)
     _need(env.episode_length_buf.dtype == torch.int64, "episode length dtype")
     d.episode_length = _ptr(env.episode_length_buf, _I64)
-    # command
-    cm = env.command_manager
-    _need(list(getattr(cm, "_terms", {}).keys()) == ["twist"], "single 'twist' command")
-    ct = cm._terms["twist"]
-    _need(isinstance(ct, mdp.UniformVelocityCommand), "UniformVelocityCommand")
-    cc = ct.cfg
-    _need(float(getattr(cc, "init_velocity_prob", 0.0)) == 0.0, "init_velocity_prob")
-    self._cmd_term = ct
-    self._set_command_ranges(d, cc)
-    d.rel_standing_envs, d.rel_heading_envs = float(cc.rel_standing_envs), float(cc.rel_heading_envs)
-    d.heading_stiffness, d.heading_command = float(cc.heading_control_stiffness), int(bool(cc.heading_command))
-    d.resampling_time[0], d.resampling_time[1] = map(float, cc.resampling_time_range)
-    d.command, d.heading_target = _ptr(ct.vel_command_b), _ptr(ct.heading_target)
-    d.heading_error, d.cmd_time_left = _ptr(ct.heading_error), _ptr(ct.time_left)
-    d.is_heading_env, d.is_standing_env = _ptr(ct.is_heading_env, _U8), _ptr(ct.is_standing_env, _U8)
-    d.command_counter = _ptr(ct.command_counter, _I64)
-    d.metric_err_xy, d.metric_err_yaw = _ptr(ct.metrics["error_vel_xy"]), _ptr(ct.metrics["error_vel_yaw"])
-    # events
+    self._reward_names = list(rm._term_names)
+
+  def _events(self, d, env):
+    """Reset events (root state + joint offsets) and the optional push interval event."""
+    n, dev = env.num_envs, torch.device(env.device)
     em = env.event_manager
     reset_terms = em._mode_term_cfgs.get("reset", [])
     funcs = [c.func for c in reset_terms]
@@ -397,33 +461,26 @@ class FusedVelocityStep:
       self._dummy_push = torch.zeros(n, device=dev)
       d.push_time_left = _ptr(self._dummy_push)
     _need(set(em._mode_term_cfgs) <= {"reset", "interval", "startup"}, "event modes")
-    # observations
+
+  def _obs_noise(self, d, env, pol, cri, sens):
+    """Shared proprioceptive head (lin vel, ang vel, gravity, joint pos / vel): sensors and
+    policy noise; no clip / scale anywhere, no critic corruption."""
     om = env.observation_manager
-    groups = om._group_obs_term_names
-    _need(set(groups) == {"policy", "critic"}, "policy + critic groups")
-    pol = list(zip(groups["policy"], om._group_obs_term_cfgs["policy"]))
-    cri = list(zip(groups["critic"], om._group_obs_term_cfgs["critic"]))
-    _need([(nme, c.func) for nme, c in pol] == _POLICY, "policy terms")
-    base_c = [(nme, c.func) for nme, c in cri]
-    _need(base_c[:7] == _POLICY and base_c[7:] in ([], _CRITIC_EXTRA), "critic terms")
     for _, c in pol + cri:
       _need(not c.clip and c.scale is None, "obs clip/scale")
     _need(pol[0][1].params["sensor_name"] == cri[0][1].params["sensor_name"], "sensor")
     d.imu_lin_vel_adr = sens[pol[0][1].params["sensor_name"]][0]
     d.imu_ang_vel_adr = sens[pol[1][1].params["sensor_name"]][0]
-    d.critic_extras = int(len(base_c) > 7)
-    if d.critic_extras:
-      _need(cri[8][1].params["sensor_name"] == feet_sensor and
-            tuple(cri[7][1].params["asset_cfg"].site_names) == site_names, "critic feet terms")
     for nme, c in cri:
       _need(c.noise is None or not om.cfg["critic"].enable_corruption, "critic noise")
     d.corrupt_policy = int(bool(om.cfg["policy"].enable_corruption))
     d.noise_lin_vel, d.noise_ang_vel, d.noise_gravity = (_noise(pol[i][1]) for i in range(3))
     d.noise_joint_pos, d.noise_joint_vel = _noise(pol[3][1]), _noise(pol[4][1])
-    for i in (5, 6):
-      _need(pol[i][1].noise is None, "noise on actions/command")
-    d.npolicy = 9 + 3 * nj + 3
-    d.ncritic = d.npolicy + (6 * d.nfeet if d.critic_extras else 0)
+
+  def _io(self, d, env):
+    """Observation buffers, action pointers, seed, log scalars."""
+    om, am, n, dev = env.observation_manager, env.action_manager, env.num_envs, torch.device(env.device)
+    rdata = self._robot.data
     _need(om.group_obs_dim["policy"] == (d.npolicy,) and om.group_obs_dim["critic"] == (d.ncritic,),
           "observation dims")
     self.obs = {"policy": torch.zeros(n, d.npolicy, device=dev),
@@ -436,12 +493,11 @@ class FusedVelocityStep:
     self.log_reward = torch.zeros(max(d.nreward, 1), device=dev)
     self.log_term = torch.zeros(max(d.ntermination, 1), device=dev)
     self.log_cmd = torch.zeros(2, device=dev)
-    self.log_metric = torch.zeros(5, device=dev)
+    self.log_metric = torch.zeros(NMETRIC, device=dev)
     self.step_counter = torch.zeros(1, dtype=torch.int64, device=dev)
     d.log_reward, d.log_termination = _ptr(self.log_reward), _ptr(self.log_term)
     d.log_command, d.log_metric = _ptr(self.log_cmd), _ptr(self.log_metric)
     d.step_counter = _ptr(self.step_counter, _U64)
-    self._reward_names, self._term_names = list(rm._term_names), list(tm._term_names)
     self._keep.extend([self._term_dones, self.reset_buf, self._episode_sums])
     return d
 
@@ -524,6 +580,161 @@ class FusedVelocityStep:
       out["Episode_Termination/" + name] = self.log_term[k]
     out["Metrics/twist/error_vel_xy"] = self.log_cmd[0]
     out["Metrics/twist/error_vel_yaw"] = self.log_cmd[1]
+    for i, key in enumerate(_METRIC_KEYS):
+      if self._metric_active[i]:
+        out[key] = self.log_metric[i]
+    return out
+
+
+# ============================================================================ jump task
+CMD_JUMP = 1
+_JUMP_REWARD_KIND = {
+  jump.explosive_takeoff: 15, jump.synchronized_extension: 16, jump.vertical_impulse: 17,
+  jump.air_time_bonus: 18, jump.symmetric_landing: 20, mdp.action_acc_l2: 21,
+  mdp.joint_torques_l2: 22, mdp.is_alive: 23, mdp.flat_orientation: 2,
+  mdp.angular_momentum_penalty: 5, mdp.soft_landing: 12, mdp.action_rate_l2: 7,
+  mdp.joint_pos_limits: 6,
+}
+_JUMP_POLICY = [("base_lin_vel", mdp.builtin_sensor), ("base_ang_vel", mdp.builtin_sensor),
+                ("projected_gravity", mdp.projected_gravity), ("joint_pos", mdp.joint_pos_rel),
+                ("joint_vel", mdp.joint_vel_rel), ("actions", mdp.last_action),
+                ("height_above_ground", jump.height_above_ground),
+                ("vertical_velocity", jump.vertical_velocity), ("contact_state", jump.foot_contact),
+                ("time_in_air", jump.foot_air_time), ("command", mdp.generated_commands)]
+_JUMP_CRITIC_EXTRA = [("foot_height", jump.foot_height), ("foot_contact_forces", jump.foot_contact_forces)]
+
+
+class FusedJumpStep(FusedVelocityStep):
+  """The jump task (tasks/jump/jump_env_cfg.py:36-354) on the same
+  fused kernels: command_kind MJX_CMD_JUMP selects JumpCommand, the jump reward / termination
+  kinds and the jump observation layout.  The stateful rewards (jump_height_reward,
+  landing_balance) run on their own objects' tensors, so a torch-side reader sees the same
+  peaks / timers."""
+
+  def _make_desc(self, env):
+    d = TaskDesc()
+    robot, sens = self._base(d, env)
+    scene, nj, dev = env.scene, d.njoint, torch.device(env.device)
+    d.command_kind = CMD_JUMP
+    idx = robot.indexing
+    ctrl_ids = idx.ctrl_ids.tolist()
+    _need(len(ctrl_ids) == nj and d.nu == nj, "one actuator per joint")
+    for j in range(nj):  # Entity.actuator_force = data.actuator_force[:, ctrl_ids] (scene.py)
+      d.act_ctrl[j] = ctrl_ids[j]
+    d.actuator_force = _ptr(env.sim.data.actuator_force)
+    # observations first: the feet sites come from the critic's foot_height term
+    om = env.observation_manager
+    groups = om._group_obs_term_names
+    _need(set(groups) == {"policy", "critic"}, "policy + critic groups")
+    pol = list(zip(groups["policy"], om._group_obs_term_cfgs["policy"]))
+    cri = list(zip(groups["critic"], om._group_obs_term_cfgs["critic"]))
+    _need([(nme, c.func) for nme, c in pol] == _JUMP_POLICY, "jump policy terms")
+    _need([(nme, c.func) for nme, c in cri] == _JUMP_POLICY + _JUMP_CRITIC_EXTRA, "jump critic terms")
+    feet_sensor = pol[8][1].params["sensor_name"]
+    for i in (9,):
+      _need(pol[i][1].params["sensor_name"] == feet_sensor, "jump obs sensor")
+    _need(cri[12][1].params["sensor_name"] == feet_sensor, "jump critic force sensor")
+    site_names = tuple(cri[11][1].params["asset_cfg"].site_names)
+    # rewards
+    rm = env.reward_manager
+    _need(len(rm._term_names) <= MAXT, "too many reward terms")
+    d.nreward = len(rm._term_names)
+    orient_body = -1
+    self._metric_active = [False] * NMETRIC
+    self._jump_height = self._landing = None
+    for k, (name, c) in enumerate(zip(rm._term_names, rm._term_cfgs)):
+      f, p = c.func, c.params
+      d.reward_weight[k] = float(c.weight)
+      if "sensor_name" in p and p["sensor_name"] != "robot/root_angmom":
+        _need(p["sensor_name"] == feet_sensor, f"{name}: feet sensor")
+      if isinstance(f, jump.jump_height_reward):
+        kind = 14
+        d.reward_p0[k], d.reward_p1[k] = float(p["target_height"]), float(p["std"])
+        self._jump_height = f
+        self._metric_active[5] = self._metric_active[6] = c.weight != 0.0
+      elif isinstance(f, jump.landing_balance):
+        kind = 19
+        d.reward_p0[k] = float(p.get("stability_time", 0.5))
+        _need(abs(f.step_dt - env.step_dt) < 1e-12, "landing timer dt")
+        self._landing = f
+        self._metric_active[7] = c.weight != 0.0
+      else:
+        _need(f in _JUMP_REWARD_KIND, f"jump reward term {name}")
+        kind = _JUMP_REWARD_KIND[f]
+        if kind == 2:
+          orient_body = self._orient(d, k, kind, p, robot, orient_body)
+        elif kind == 5:
+          d.angmom_adr = sens[p["sensor_name"]][0]
+        elif kind == 12:
+          d.reward_p0[k] = float(p.get("command_threshold", 0.05))
+          _need(p.get("command_name") is None, "jump soft_landing is ungated")
+          d.reward_p1[k] = 1.0
+        elif kind == 15:
+          d.reward_p0[k] = float(p.get("power_threshold", 500.0))
+          ac = p.get("asset_cfg")
+          ids = ac.joint_ids if ac is not None else slice(None)
+          ids = list(range(nj)) if isinstance(ids, slice) else [int(i) for i in ids]
+          d.explosive_joints = sum(1 << i for i in ids)
+        elif kind == 18:
+          d.reward_p0[k] = float(p.get("min_air_time", 0.2))
+      d.reward_kind[k] = kind
+      if c.weight != 0.0 and kind in _METRIC_OF_KIND:
+        self._metric_active[_METRIC_OF_KIND[kind]] = True
+    d.orient_body = orient_body
+    self._feet(d, robot, feet_sensor, site_names)
+    n = env.num_envs
+    if self._jump_height is None:
+      self._jump_height = jump.jump_height_reward(None, env)
+    if self._landing is None:
+      self._landing = jump.landing_balance(None, env)
+    jh, lb = self._jump_height, self._landing
+    d.jump_peak, d.jump_initial = _ptr(jh.peak_heights), _ptr(jh.initial_heights)
+    d.jump_initialized = _ptr(jh.initialized, _U8)
+    d.landing_timer, d.was_in_air = _ptr(lb.stability_timer), _ptr(lb.was_in_air, _U8)
+    self._terminations(d, env)
+    self._reward_buffers(d, env)
+    # command: JumpCommand (commands.py:17-62)
+    cm = env.command_manager
+    _need(list(getattr(cm, "_terms", {}).keys()) == ["jump"], "single 'jump' command")
+    ct = cm._terms["jump"]
+    _need(isinstance(ct, jump.JumpCommand), "JumpCommand")
+    self._cmd_term = ct
+    d.resampling_time[0], d.resampling_time[1] = map(float, ct.cfg.resampling_time_range)
+    d.jump_target_height = float(ct.cfg.target_height)
+    d.command, d.cmd_time_left = _ptr(ct.height_command), _ptr(ct.time_left)
+    d.command_counter = _ptr(ct.command_counter, _I64)
+    d.metric_err_xy, d.metric_err_yaw = _ptr(ct.metrics["target_height"]), _ptr(ct.metrics["peak_height"])
+    self._events(d, env)
+    _need(not d.has_push, "no interval events in the jump task")
+    self._obs_noise(d, env, pol, cri, sens)
+    for i in range(5, 11):
+      _need(pol[i][1].noise is None, "noise beyond the proprioceptive terms")
+    d.npolicy = 9 + 3 * nj + 2 + 2 * d.nfeet + 1
+    d.ncritic = d.npolicy + 4 * d.nfeet
+    self._io(d, env)
+    return d
+
+  def upload(self):
+    """Curricula move the target height (progressive_jump_height) and reward weights."""
+    self._desc.jump_target_height = float(self._cmd_term.cfg.target_height)
+    for k, c in enumerate(self.env.reward_manager._term_cfgs):
+      self._desc.reward_weight[k] = float(c.weight)
+    if self._task is not None:
+      self._L.mjx_task_destroy(self._task)
+    h = ctypes.c_void_p()
+    rc = self._L.mjx_task_create(ctypes.byref(self._desc), ctypes.byref(h))
+    if rc != 0:
+      raise MjxError(self._L.mjx_task_last_error().decode())
+    self._task = h
+
+  def log(self) -> dict:
+    out = {}
+    for k, name in enumerate(self._reward_names):
+      out["Episode_Reward/" + name] = self.log_reward[k]
+    for k, name in enumerate(self._term_names):
+      out["Episode_Termination/" + name] = self.log_term[k]
+    out["Metrics/jump/target_height"] = self.log_cmd[0]
+    out["Metrics/jump/peak_height"] = self.log_cmd[1]
     for i, key in enumerate(_METRIC_KEYS):
       if self._metric_active[i]:
         out[key] = self.log_metric[i]
