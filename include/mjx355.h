@@ -142,6 +142,16 @@ const char* mjx_field_name(const mjxSim* sim, int i);
 int mjx_expand_field(mjxSim* sim, const char* name, void* stream);
 int mjx_field_is_expanded(const mjxSim* sim, const char* name);
 
+/* Contact-sensor air-time tracking inside the step (ContactSensor._update_air_time_tracking,
+ * sensor/contact_sensor.py:327-367): after every integrated substep, for each of the `n`
+ * tracked slots (n <= 8) with its `found` value at sensordata[found_adr[i]], update the
+ * device buffers cur_air / last_air / cur_contact / last_contact [nworld, n] with the
+ * elapsed time = time - last_time[w], then last_time[w] = time.  mjx_forward does not
+ * update them.  found_adr is a host array; n = 0 turns tracking off.  Synchronises. */
+int mjx_sim_track_air_time(mjxSim* sim, int n, const int32_t* found_adr, float* cur_air,
+                           float* last_air, float* cur_contact, float* last_contact,
+                           float* last_time, void* stream);
+
 /* Diagnostics: per-sim counters (max contacts/rows seen, overflow events) as
  * int32[8] written to host `out`; synchronises the stream. */
 int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);

@@ -82,6 +82,9 @@ struct mjxSim_ {
   mjx::Lds lds_ph[3 + mjx::kRowClasses];  // per-phase LDS carves ([3 + k]: Newton row class k)
   int nrowclass = 0;
   int row_cap[mjx::kRowClasses] = {};
+  int nair = 0;  // contact air-time tracking (mjx_sim_track_air_time)
+  int air_found[mjx::kMaxAirSlots] = {};
+  float* air_buf[5] = {};
   int spec = 0;  // model specialisation in use (mjx::find_spec), 0 = generic kernels
   mjx::SideStream side{};  // streams of the Newton row classes (when classes are used)
   ~mjxSim_() {
@@ -118,6 +121,10 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.gF = s->gF;
   p.gstride = s->gstride;
   p.spec = s->spec;
+  p.nair = s->nair;
+  for (int i = 0; i < mjx::kMaxAirSlots; i++) p.air_found[i] = s->air_found[i];
+  p.air_cur = s->air_buf[0]; p.air_last = s->air_buf[1]; p.air_cc = s->air_buf[2];
+  p.air_lc = s->air_buf[3]; p.air_time = s->air_buf[4];
   return p;
 }
 
@@ -385,6 +392,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
 #undef X_INT
   reserve("__stats", sizeof(int32_t) * 8);
   reserve("__wstats", sizeof(int32_t) * 8 * (size_t)nworld);
+  reserve("__evtotal", sizeof(int32_t) * 4);
   reserve("__prof", sizeof(unsigned long long) * 48);
   reserve("__wtrace", sizeof(unsigned long long) * 8 * (size_t)nworld);
   hipError_t e = hipMalloc((void**)&s->gscr, sizeof(float) * (size_t)nworld * s->gstride);
@@ -420,6 +428,10 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   // (cumulative), [5] Newton iterations -- a zero-copy view for device-side logging
   s->fields["engine_counters"] = FieldInfo{s->dd.wstats, false, 8, 1, true, false};
   s->names.push_back("engine_counters");
+  // [1, 4]: contact-overflow / row-overflow / unsupported-pair events summed over worlds
+  s->dd.evtotal = (int32_t*)(base + offs[k++].second);
+  s->fields["engine_events"] = FieldInfo{s->dd.evtotal, false, 4, 1, false, false};
+  s->names.push_back("engine_events");
   s->dd.prof = (unsigned long long*)(base + offs[k++].second);
   // per-world phase start/end timestamps (s_memrealtime, 100 MHz; diagnostic MJX_STAMPS
   // build): [A0 A1 B0 B1 C0 C1 - -] as int32 pairs
@@ -499,6 +511,23 @@ int mjx_forward_masked(mjxSim* s, const uint8_t* mask, void* stream) {
   return 0;
 }
 
+int mjx_sim_track_air_time(mjxSim* s, int n, const int32_t* found_adr, float* cur_air,
+                           float* last_air, float* cur_contact, float* last_contact,
+                           float* last_time, void* stream) {
+  if (!s) return fail("null sim");
+  if (n < 0 || n > mjx::kMaxAirSlots) return fail("air-time tracking: 0 <= n <= 8 slots");
+  if (n > 0 && (!found_adr || !cur_air || !last_air || !cur_contact || !last_contact || !last_time))
+    return fail("air-time tracking: null buffer");
+  for (int i = 0; i < n; i++)
+    if (found_adr[i] < 0 || found_adr[i] >= s->d.nsensordata)
+      return fail("air-time tracking: found address outside sensordata");
+  s->nair = n;
+  for (int i = 0; i < mjx::kMaxAirSlots; i++) s->air_found[i] = i < n ? found_adr[i] : 0;
+  float* b[5] = {cur_air, last_air, cur_contact, last_contact, last_time};
+  for (int i = 0; i < 5; i++) s->air_buf[i] = n > 0 ? b[i] : nullptr;
+  return sync_params(s, stream);
+}
+
 int mjx_reset(mjxSim* s, const uint8_t* mask, void* stream) {
   if (!s) return fail("null sim");
   hipError_t e = mjx::launch_reset(s->d, s->dm, s->dd, mask, s->nworld, (hipStream_t)stream);
@@ -530,7 +559,7 @@ int mjx_field(mjxSim* s, const char* cname, DLManagedTensor** out) {
   if (it == s->fields.end()) return fail("unknown field '" + name + "'");
   const FieldInfo& fi = it->second;
   void* ptr = fi.ptr;
-  int64_t lead = s->nworld;
+  int64_t lead = fi.per_world ? s->nworld : 1;
   if (fi.model) {
     int ws = 0;
     ptr = const_cast<void*>(model_field_ptr(s, name.substr(6), &ws));

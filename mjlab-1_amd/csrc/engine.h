@@ -16,6 +16,7 @@ constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
 constexpr int kRowClasses = 2;   // Newton row classes below the full capacity
+constexpr int kMaxAirSlots = 8;  // contact-sensor slots with air-time tracking
 
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
@@ -68,6 +69,8 @@ struct DData {
 #undef X_INT
   int32_t* stats;   // [8] reduced engine counters (filled by mjx_sim_stats)
   int32_t* wstats;  // [nworld][8] per-world counters (no cross-world atomics in the kernels)
+  int32_t* evtotal; // [4] overflow / unsupported-pair events over all worlds (an atomic per
+                    // event, and events are rare: no per-substep cross-world traffic)
   unsigned long long* prof;  // [48] stage cycle sums (diagnostic -DMJX_STAMPS build)
   unsigned long long* wtrace;  // [nworld][8] per-world phase start/end s_memrealtime (MJX_STAMPS)
 };
@@ -127,6 +130,11 @@ struct Params {
                  // phase C straight from global memory (not staged in LDS)
   int gstride;
   int spec;      // model specialisation (find_spec) whose kernels launch_step uses
+  // contact-sensor air-time tracking (mjx_sim_track_air_time): phase C of every integrated
+  // substep updates nair slots per world from sensordata[air_found[i]]
+  int nair;
+  int air_found[kMaxAirSlots];
+  float *air_cur, *air_last, *air_cc, *air_lc, *air_time;
 };
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of

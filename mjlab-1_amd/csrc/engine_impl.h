@@ -2566,6 +2566,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
                     : (ints[3] >> (lane - 2)) & 1;
         const int old = ws[lane];
         ws[lane] = (lane >= 2 && lane <= 4) ? old + v : max(old, v);
+        if (lane >= 2 && lane <= 4 && v) atomicAdd(D.evtotal + lane - 2, v);
       }
     }
     STAMP(12);
@@ -2617,6 +2618,25 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.qacc_warmstart[(size_t)w * nv + i] = S[L.qacc_ws + i];
       }
       if (lane == 0) D.time[w] = time;
+      // contact-sensor air time (ContactSensor._update_air_time_tracking,
+      // sensor/contact_sensor.py:327-367): the found values this phase stored above are
+      // read back after a workgroup fence (other lanes wrote them)
+      const int nair = P->nair;
+      if (nair > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const float el = time - P->air_time[w];
+        if (lane < nair) {
+          const size_t i = (size_t)w * nair + lane;
+          const bool contact = D.sensordata[(size_t)w * d.nsensordata + P->air_found[lane]] > 0.f;
+          const float ca = P->air_cur[i], cc = P->air_cc[i];
+          if (ca > 0.f && contact) P->air_last[i] = ca + el;
+          P->air_cur[i] = contact ? 0.f : ca + el;
+          if (cc > 0.f && !contact) P->air_lc[i] = cc + el;
+          P->air_cc[i] = contact ? cc + el : 0.f;
+        }
+        if (lane == 0) P->air_time[w] = time;
+      }
     }
     STAMP(13);
   }

@@ -19,7 +19,7 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
            "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile", "mjx_sim_spec",
-           "mjx_forward_masked",
+           "mjx_forward_masked", "mjx_sim_track_air_time",
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
@@ -65,7 +65,14 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_spec.argtypes = [vp]
   L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
+  if hasattr(L, "mjx_sim_track_air_time"):
+    L.mjx_sim_track_air_time.argtypes = [vp, ci, ctypes.POINTER(ctypes.c_int32)] + [vp] * 6
+  missing = [n for n in EXPORTS if not hasattr(L, n)]
+  if missing and not os.environ.get("MJX355_LIB"):  # MJX355_LIB: A/B against an older build
+    raise MjxError(f"{LIB_PATH} lacks {missing}: rebuild it (make -C mjlab-1_amd/csrc)")
   for name in EXPORTS:
+    if not hasattr(L, name):
+      continue
     if name.startswith(("mjx_task_", "mjx_track_")):
       continue  # bound by mjlab_amd.fused / mjlab_amd.fused_tracking
     if name not in ("mjx_last_error", "mjx_field_name", "mjx_model_desc_size"):

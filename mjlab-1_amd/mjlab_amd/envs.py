@@ -340,8 +340,7 @@ class ManagerBasedRlEnv:
     as device scalars: no host sync."""
     ev = getattr(self, "_sim_events", None)
     if ev is None:
-      ev = self._sim_events = torch.zeros(3, dtype=torch.int64, device=self.device)
-    torch.sum(self.sim.engine_counters[:, 2:5], dim=0, out=ev)
+      ev = self._sim_events = self.sim.overflow_events()
     log["Sim/contact_overflow"] = ev[0]
     log["Sim/row_overflow"] = ev[1]
     log["Sim/unsupported_pairs"] = ev[2]

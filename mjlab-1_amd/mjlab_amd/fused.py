@@ -174,6 +174,7 @@ class FusedVelocityStep:
     self._task = None
     self._desc = self._make_desc(env)
     self.upload()
+    self._engine_air = self._track_air_time()
 
   # ------------------------------------------------------------------ descriptor
   def _make_desc(self, env):
@@ -528,6 +529,24 @@ class FusedVelocityStep:
     hd = r.heading if r.heading is not None else (0.0, 0.0)
     d.heading[0], d.heading[1] = map(float, hd)
 
+  def _track_air_time(self) -> bool:
+    """Hand the feet air-time buffers to the engine (mjx_sim_track_air_time): phase C of
+    every substep then updates them, replacing the per-substep task kernel.  False with an
+    older engine build (A/B runs), which keeps k_substep."""
+    sim, d = self.env.sim, self._desc
+    tl = lib()
+    if not hasattr(tl, "mjx_sim_track_air_time") or d.nfeet == 0:
+      return False
+    adr = (ctypes.c_int32 * d.nfeet)(*[d.feet_found_adr[i] for i in range(d.nfeet)])
+    air = self._feet_sensor._air
+    ptrs = [ctypes.c_void_p(air[k].data_ptr()) for k in
+            ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time", "last_time")]
+    for k in ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time", "last_time"):
+      _need(air[k].is_contiguous() and air[k].dtype == torch.float32, "air-time buffers")
+    stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
+    check(tl.mjx_sim_track_air_time(sim._sim, d.nfeet, adr, *ptrs, stream))
+    return True
+
   # ------------------------------------------------------------------ device handle
   def upload(self):
     """(Re)create the device copy of the descriptor (after a curriculum changed command
@@ -560,8 +579,9 @@ class FusedVelocityStep:
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
     self._ok(L.mjx_task_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
     for _ in range(env.cfg.decimation):
-      sim.step()
-      self._ok(L.mjx_task_substep(self._task, stream))
+      sim.step()  # the engine updates the feet air times (mjx_sim_track_air_time)
+      if not self._engine_air:
+        self._ok(L.mjx_task_substep(self._task, stream))
     self._ok(L.mjx_task_post(self._task, stream))
     mask = ctypes.c_void_p(self.reset_buf.data_ptr())
     check(lib().mjx_reset(sim._sim, mask, stream))

@@ -283,9 +283,11 @@ class Simulation:
     return self.field("engine_counters")
 
   def overflow_events(self) -> torch.Tensor:
-    """Device [3] tensor: total contact-overflow, row-overflow and unsupported-pair
-    events over all worlds since creation (no host sync)."""
-    return self.engine_counters[:, 2:5].sum(dim=0)
+    """Device [3] int32 view: total contact-overflow, row-overflow and unsupported-pair
+    events over all worlds since creation (kept by the engine; no kernel, no host sync)."""
+    if "engine_events" not in self._field_names:  # an older engine build (scripts/ab.sh)
+      return self.engine_counters[:, 2:5].sum(dim=0)
+    return self.field("engine_events")[0, :3]
 
   def stats(self) -> dict:
     """Engine counters: max contacts/rows seen, overflow and unsupported-pair events."""

@@ -169,3 +169,21 @@ def test_env_graph_step(task, gpu_device):
     assert torch.isfinite(v).all()
   assert torch.isfinite(rew).all()
   assert env.sim.stats()["unsupported"] == 0
+
+
+def test_overflow_event_total_matches_world_counters(gpu_device):
+  """engine_events (one atomic per overflow event) equals the per-world cumulative
+  counters summed over worlds; an 8-row capacity forces row overflow."""
+  from mjlab_amd.scenes import load_scene
+  from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+  m = load_scene("g1_velocity")
+  sim = Simulation(16, SimulationCfg(nconmax=48, njmax=8, mujoco=MujocoCfg(timestep=m.timestep)),
+                   m, gpu_device)
+  _keyframe(sim, m, gpu_device, jitter=0.1)
+  for _ in range(6):
+    sim.step()
+  torch.cuda.synchronize()
+  per_world = sim.engine_counters[:, 2:5].sum(dim=0)
+  total = sim.overflow_events()
+  assert total.tolist() == per_world.tolist()
+  assert int(total[1]) > 0
