@@ -32,29 +32,33 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   struct Slot { int Lds::*f; int n; int mask; };
   const Slot all[] = {
     {&Lds::ints, 8, A | B | Cp},
-    {&Lds::qpos, d.nq, A | Cp}, {&Lds::qvel, nv, A | Cp}, {&Lds::ctrl, d.nu, A},
-    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, A}, {&Lds::xfrc, 6 * nb, 0},  // xfrc read from HBM (rare)
-    {&Lds::xpos, 3 * nb, A}, {&Lds::xquat, 4 * nb, A}, {&Lds::xmat, 9 * nb, A},
-    {&Lds::xipos, 3 * nb, A}, {&Lds::ximat, 9 * nb, A}, {&Lds::xanchor, 3 * d.njnt, A},
-    {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, A}, {&Lds::subtree_com, 3 * nb, A | Cp},
+    // ctrl, qfrc_applied, subtree masses, qfrc_bias / passive and actuator length / velocity
+    // live in lane registers in phase A; body rotations as quaternions (xmat / ximat are
+    // formed where used)
+    {&Lds::qpos, d.nq, A | Cp}, {&Lds::qvel, nv, A | Cp}, {&Lds::ctrl, d.nu, 0},
+    {&Lds::qacc_ws, nv, B | Cp}, {&Lds::qfrc_applied, nv, 0}, {&Lds::xfrc, 6 * nb, 0},  // xfrc read from HBM (rare)
+    {&Lds::xpos, 3 * nb, A}, {&Lds::xquat, 4 * nb, A}, {&Lds::xmat, 9 * nb, 0},
+    {&Lds::xipos, 3 * nb, A}, {&Lds::ximat, 9 * nb, 0}, {&Lds::xanchor, 3 * d.njnt, A},
+    {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, 0}, {&Lds::subtree_com, 3 * nb, A | Cp},
     {&Lds::cinert, 10 * nb, A}, {&Lds::crb, 10 * nb, A}, {&Lds::cvel, 6 * nb, A | Cp},
     {&Lds::cacc, 6 * nb, A | Cp}, {&Lds::stlin, 3 * nb, A}, {&Lds::stang, 3 * nb, A},
     {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
     {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
     {&Lds::M, nv * nv, A | B}, {&Lds::H, nv * nv, A | B},
-    {&Lds::qfrc_bias, nv, A}, {&Lds::qfrc_passive, nv, A}, {&Lds::qfrc_act, nv, A},
+    {&Lds::qfrc_bias, nv, 0}, {&Lds::qfrc_passive, nv, 0}, {&Lds::qfrc_act, nv, A},
     {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
     {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
     {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
-    {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, A}, {&Lds::act_vel, d.nu, A},
+    {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
-    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, A | Cp},
+    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, Cp},
+    {&Lds::con_n, 3 * C, A},  // phase A: unit normals (cframe() rebuilds the frame)
     {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_kb, 2 * C, A}, {&Lds::con_imp, C, A},
     {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
     {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
     {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
-    {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R, A},
+    {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R > nb ? R : nb, A},
     {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, 0},
     {&Lds::red, 5 * kWave, B},
     // column-block broadcast buffer of the blocked Cholesky (rows_chol): 4 floats per lane;
@@ -94,32 +98,49 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   }
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,
-    // collision, contacts, rows.  Two aliases follow from it:
-    //  - M and H (the smooth solve's in-place factor) live in the contact/row block, which
-    //    is first written by collision, after the smooth solve;
-    //  - geom frames (computed at the start of collision) live in [cinert crb cacc
-    //    xanchor xaxis], all dead once RNE has run.
+    // collision, contacts, rows.  The aliases follow from it:
+    //  - joint anchors / axes (dead after cdof), then M and H (the smooth solve's in-place
+    //    factor) live in the contact/row block, which is first written by collision, after
+    //    the smooth solve;
+    //  - the subtree momenta (written after RNE, read back before the geom frames), then
+    //    the geom frames (computed at the start of collision) live in [cinert crb cacc],
+    //    dead once RNE has run.
     auto group = [&](std::initializer_list<int Lds::*> fs) {
       const int start = o;
       for (auto f : fs) take(f);
       return std::make_pair(start, o - start);
     };
     auto g1 = group({&Lds::con_g1, &Lds::con_g2, &Lds::con_key, &Lds::con_dist, &Lds::con_pos,
-                     &Lds::con_frame, &Lds::con_mu, &Lds::con_kb, &Lds::con_imp,
+                     &Lds::con_n, &Lds::con_mu, &Lds::con_kb, &Lds::con_imp,
                      &Lds::con_imargin, &Lds::con_dim, &Lds::con_efc, &Lds::efc_aref, &Lds::efc_D,
                      &Lds::efc_cid});
     // M (assembled after CRB, copied to the B/C packs at once, factored in place by the
     // smooth solve) is dead before collision: M and H share the contact/row block too.
     if (g1.second >= nv * nv) L.M = L.H = g1.first;
-    auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc, &Lds::xanchor, &Lds::xaxis});
+    // joint anchors / axes: from kinematics to cdof, before M is assembled; the kinematics
+    // ancestor-pointer scratch sits in efc_cid, past them
+    const int nj3 = (3 * d.njnt + 3) & ~3;
+    if (g1.second >= 2 * nj3 && L.efc_cid >= g1.first + 2 * nj3) {
+      L.xanchor = g1.first;
+      L.xaxis = g1.first + nj3;
+    }
+    auto g2 = group({&Lds::cinert, &Lds::crb, &Lds::cacc});
+    // subtree momenta in the cinert slot (crb holds their mass scratch)
+    const int nb3 = (3 * nb + 3) & ~3;
+    if (10 * nb >= 2 * nb3) {
+      L.stlin = L.cinert;
+      L.stang = L.cinert + nb3;
+    }
     const int gp = (3 * d.ngeom_lds + 3) & ~3;
     if (g2.second >= gp + 9 * d.ngeom_lds) {
       L.gxpos = g2.first;
       L.gxmat = g2.first + gp;
     }
     // both phase-A factorizations (implicit-integration factor, smooth solve) run after RNE
-    // and before the geom frames are computed: the same dead group holds the Cholesky buffer
-    if (g2.second >= 4 * kWave) L.chol = g2.first;
+    // and before the geom frames are computed: the same dead group holds the Cholesky buffer,
+    // at its tail (the subtree momenta at its head are live across the factorizations)
+    const int mom_end = L.stlin == L.cinert ? g2.first + 2 * nb3 : g2.first;
+    if (g2.first + g2.second - 4 * kWave >= mom_end) L.chol = g2.first + g2.second - 4 * kWave;
   }
   const int bit = 1 << ph;
   for (const Slot& sp : all)

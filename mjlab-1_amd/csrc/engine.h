@@ -85,7 +85,7 @@ struct Lds {
   int qfrc_bias, qfrc_passive, qfrc_act, qfrc_smooth, qacc_smooth, x, Mx, grad, srch, Ms,
       qfrc_con, vtmp, act_force, act_len, act_vel;
   int con_g1, con_g2, con_key, con_dist, con_pos, con_frame, con_mu, con_kb,
-      con_imp, con_imargin, con_dim, con_efc;
+      con_imp, con_imargin, con_dim, con_efc, con_n;
   int efc_J, efc_aref, efc_D, efc_jar, efc_Js, efc_force, efc_cid, efc_act, hdiag;
   int red;      // 5*kWave scratch (J^T w partial sums)
   int chol;     // 4*NR floats: column blocks of the blocked Cholesky (rows_chol)

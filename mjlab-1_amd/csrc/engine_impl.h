@@ -550,6 +550,18 @@ struct ConOut {
   const Lds* L;
   int cap;
 };
+// Contact frame (mju_makeFrame) from the unit normal: rows n, t, b.  Phase A keeps only the
+// normal in LDS and rebuilds the tangents where they are used (same arithmetic every time).
+struct CFrame { V3 n, t, b; };
+__device__ __forceinline__ CFrame cframe(V3 n) {
+  CFrame f;
+  f.n = n;
+  V3 t = fabsf(n.y) < 0.5f ? V3{0, 1, 0} : V3{0, 0, 1};
+  t = t - n * dot(n, t);
+  f.t = t * (1.0f / fmaxf(norm(t), MINVAL));
+  f.b = cross(n, f.t);
+  return f;
+}
 __device__ __forceinline__ void append(const ConOut& co, int key, int g1, int g2, float dist,
                                        V3 pos, V3 n) {
   int slot = atomicAdd(&co.ints[0], 1);
@@ -564,7 +576,7 @@ __device__ __forceinline__ void append(const ConOut& co, int key, int g1, int g2
   Si[L.con_g2 + slot] = g2;
   co.S[L.con_dist + slot] = dist;
   st3(co.S + L.con_pos + 3 * slot, pos);
-  st3(co.S + L.con_frame + 9 * slot, n);
+  st3(co.S + L.con_n + 3 * slot, n);
 }
 __device__ __forceinline__ int plane_sphere(const ConOut& co, int key, int g1, int g2, V3 pp,
                                             V3 n, V3 c, float r, float margin) {
@@ -613,11 +625,9 @@ __device__ __forceinline__ HFrame hfield_frame(const DModel& m, const float* S, 
                                                const float* gpos, const float* gquat, int g) {
   HFrame f;
   const int b = m.geom_bodyid[g];
-  const float* Rb = S + L.xmat + 9 * b;
-  f.p = v3(S + L.xpos + 3 * b) + mulv(Rb, v3(gpos + 3 * g));
-  float Rg[9];
-  qmat(Rg, q4(gquat + 4 * g));
-  mat3mul(f.R, Rb, Rg);
+  const Q4 qb = q4(S + L.xquat + 4 * b);
+  f.p = v3(S + L.xpos + 3 * b) + qrot(qb, v3(gpos + 3 * g));
+  qmat(f.R, qmul(qb, q4(gquat + 4 * g)));
   return f;
 }
 __device__ __forceinline__ int hfield_sphere(const ConOut& co, int key, int g1, int g2,
@@ -1032,14 +1042,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     // rows go straight into LDS (LDS-DMA), model records into registers, then one wait
     // (copied loop by loop, each load-then-LDS-store would wait out a global latency).
     for (int i = lane; i < nvp; i += kWave) {
-      if (i >= nv) { S[L.qvel + i] = 0.f; S[L.qfrc_applied + i] = 0.f; }  // DMA fills i < nv
-      S[L.qfrc_bias + i] = 0.f; S[L.qfrc_passive + i] = 0.f; S[L.qfrc_act + i] = 0.f;
+      if (i >= nv) S[L.qvel + i] = 0.f;  // DMA fills i < nv
+      S[L.qfrc_act + i] = 0.f;
       S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f;
     }
     dma_row(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
     dma_row(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
-    dma_row(S + L.qfrc_applied, D.qfrc_applied + (size_t)w * nv, nv, lane);
-    dma_row(S + L.ctrl, D.ctrl + (size_t)w * nu, nu, lane);
+    // lane-aligned inputs stay in registers (lane u: ctrl[u], lane i: qfrc_applied[i])
+    const float ctrl_u = lane < nu ? D.ctrl[(size_t)w * nu + lane] : 0.f;
+    const float qapp_i = lane < nv ? D.qfrc_applied[(size_t)w * nv + lane] : 0.f;
     SUBSTAMP(15);
     float* Jg = gw + LB.efc_J;
     const BodyPtrs BP{body_pos, body_quat, body_ipos, body_iquat, body_mass, body_inertia,
@@ -1084,7 +1095,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     //     chain reaches an absolute frame -- ceil(log2(depth)) rounds of one LDS round trip
     //     instead of one per tree level;
     // (3) after the body frames: anchors / axes to the world by the parent frame.
-    int* par = Si + L.stmass;  // scratch ancestor pointers (stmass is written after kinematics)
+    int* par = Si + L.efc_cid;  // scratch ancestor pointers (the row block is dead until rows)
     bool absb = false;
     V3 kpos = {0.f, 0.f, 0.f};
     Q4 kq = {1.f, 0.f, 0.f, 0.f};
@@ -1159,22 +1170,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     if (bl) st4(S + L.xquat + 4 * B.b, qnorm(kq));
     sync();
     SUBSTAMP(14);
-    if (bl) {
-      const int b = B.b;
-      float* R = S + L.xmat + 9 * b;
-      qmat(R, q4(S + L.xquat + 4 * b));
-      st3(S + L.xipos + 3 * b, v3(S + L.xpos + 3 * b) + mulv(R, B.ipos));
-      float Ri[9];
-      qmat(Ri, B.iquat);
-      mat3mul(S + L.ximat + 9 * b, R, Ri);
-    }
-    sync();
+    // body rotations stay quaternions in LDS (xmat / ximat are formed where used)
+    const Q4 xq = bl ? q4(S + L.xquat + 4 * B.b) : Q4{1.f, 0.f, 0.f, 0.f};
+    if (bl) st3(S + L.xipos + 3 * B.b, v3(S + L.xpos + 3 * B.b) + qrot(xq, B.ipos));
     if (bl && !absb) {  // (3): joint anchors / axes from the parent frame to the world
-      const float* Rp = S + L.xmat + 9 * B.p;
+      const Q4 qp = q4(S + L.xquat + 4 * B.p);
       const V3 pp = v3(S + L.xpos + 3 * B.p);
       for (int k = B.j0; k < B.j0 + B.jn; k++) {
-        st3(S + L.xanchor + 3 * k, pp + mulv(Rp, v3(S + L.xanchor + 3 * k)));
-        st3(S + L.xaxis + 3 * k, mulv(Rp, v3(S + L.xaxis + 3 * k)));
+        st3(S + L.xanchor + 3 * k, pp + qrot(qp, v3(S + L.xanchor + 3 * k)));
+        st3(S + L.xaxis + 3 * k, qrot(qp, v3(S + L.xaxis + 3 * k)));
       }
     }
     {
@@ -1182,17 +1186,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       const float* squat = MF(site_quat);
       for (int s = lane; s < d.nsite; s += kWave) {
         int b = m.site_bodyid[s];
-        const float* R = S + L.xmat + 9 * b;
-        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + mulv(R, v3(spos + 3 * s)));
-        float Rs[9];
-        qmat(Rs, q4(squat + 4 * s));
-        mat3mul(S + L.sxmat + 9 * s, R, Rs);
+        const Q4 qb = q4(S + L.xquat + 4 * b);
+        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + qrot(qb, v3(spos + 3 * s)));
+        qmat(S + L.sxmat + 9 * s, qmul(qb, q4(squat + 4 * s)));
       }
     }
     STAMP(0);
     // =========================================================== com / cinert / cdof
     // Subtree sums as broadcast loops: lane b adds body c's term when c is in its subtree
     // (B.sub); every lane reads the same LDS address per c, no level-by-level syncs.
+    float stm = 0.f;  // subtree mass of this lane's body
     {
       float* mx = S + L.crb;  // scratch [nb][4] = (m * xipos, m); crb is written below
       if (bl) {
@@ -1211,7 +1214,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       sync();
       if (bl) {
         const int b = B.b;
-        S[L.stmass + b] = acc.w;
+        stm = acc.w;
         const V3 c = acc.w > MINVAL ? V3{acc.x, acc.y, acc.z} * (1.0f / acc.w) : v3(S + L.xipos + 3 * b);
         st3(S + L.subtree_com + 3 * b, c);
       }
@@ -1224,7 +1227,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         for (int i = 0; i < 10; i++) c[i] = 0;
       } else {
       V3 off = v3(S + L.subtree_com + 3 * B.root);
-      const float* R = S + L.ximat + 9 * b;
+      float R[9];  // ximat
+      qmat(R, qmul(xq, B.iquat));
       const float I[3] = {B.inert.x, B.inert.y, B.inert.z};
       float full[9];
 #pragma unroll
@@ -1246,7 +1250,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     }
     // cdof: lane per body over its joints
     for (int k = B.j0; bl && k < B.j0 + B.jn; k++) {
-      const int b = B.b;
       const JntRec J = jnt_of(m, BP, B, k);
       const int dof = J.da;
       V3 rel = v3(S + L.subtree_com + 3 * B.root) - v3(S + L.xanchor + 3 * k);
@@ -1257,7 +1260,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           for (int j = 0; j < 6; j++) c[j] = 0;
           c[3 + i] = 1;
         }
-        const float* R = S + L.xmat + 9 * b;
+        float R[9];
+        qmat(R, xq);
         for (int i = 0; i < 3; i++) {
           float* c = S + L.cdof + 6 * (dof + 3 + i);
           V3 ax = {R[i], R[3 + i], R[6 + i]};
@@ -1414,14 +1418,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
     }
     sync();
+    // lane i < nv: qfrc_bias / qfrc_passive of dof i in registers
+    float qbias_i = 0.f, qpass_i = 0.f;
     if (lane < nv) {
       const int i = lane;
-      S[L.qfrc_bias + i] = dot6(S + L.cdof + 6 * i, S + L.cacc + 6 * Dr.body);  // cfrc
+      qbias_i = dot6(S + L.cdof + 6 * i, S + L.cacc + 6 * Dr.body);  // cfrc
       float pf = -Dr.damp * S[L.qvel + i];
       if ((Dr.jt == JNT_HINGE || Dr.jt == JNT_SLIDE) && Dr.stiff != 0.f)
         pf -= Dr.stiff * (S[L.qpos + Dr.qa] - Dr.qs);
-      S[L.qfrc_passive + i] = pf;
-      S[L.qfrc_act + i] = 0.f;
+      qpass_i = pf;
     }
     sync();
     // actuation: position / motor actuators on joints
@@ -1429,18 +1434,20 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       const int u = lane;
       const float g = Ar.gear;
       float len = g * S[L.qpos + Ar.qa], vel = g * S[L.qvel + Ar.dof];
-      float c = S[L.ctrl + u];
+      float c = ctrl_u;
       if (Ar.ctrllim) c = fminf(fmaxf(c, Ar.cr0), Ar.cr1);
       float f = Ar.gain * c + Ar.b0 + Ar.b1 * len + Ar.b2 * vel;
       if (Ar.forcelim) f = fminf(fmaxf(f, Ar.fr0), Ar.fr1);
       S[L.act_force + u] = f;
-      S[L.act_len + u] = len;
-      S[L.act_vel + u] = vel;
+      if (last) {
+        D.actuator_length[(size_t)w * nu + u] = len;
+        D.actuator_velocity[(size_t)w * nu + u] = vel;
+      }
       atomicAdd(S + L.qfrc_act + Ar.dof, g * f);
     }
     sync();
-    for (int i = lane; i < nv; i += kWave) {
-      float f = S[L.qfrc_passive + i] - S[L.qfrc_bias + i] + S[L.qfrc_applied + i] + S[L.qfrc_act + i];
+    for (int i = lane; i < nv; i += kWave) {  // nv <= 64: one pass, lane i
+      float f = qpass_i - qbias_i + qapp_i + S[L.qfrc_act + i];
       if (any_xfrc) {
         uint64_t bm = m.dof_bodymask[i];
         const float* cd = S + L.cdof + 6 * i;
@@ -1462,7 +1469,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
       V3 vc = v3(cv + 3) + cross(v3(cv), rel);
       st3(S + L.stlin + 3 * b, vc);  // body com velocity; subtree sums below
-      const float* Ri = S + L.ximat + 9 * b;
+      float Ri[9];  // ximat
+      qmat(Ri, qmul(xq, B.iquat));
       V3 wl = mulTv(Ri, v3(cv));
       V3 hl = {B.inert.x * wl.x, B.inert.y * wl.y, B.inert.z * wl.z};
       st3(S + L.stang + 3 * b, mulv(Ri, hl));
@@ -1522,13 +1530,29 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       }
       sync();  // every lane's reads precede the in-place writes
       if (bl) {
-        const float sm = S[L.stmass + B.b];
+        const float sm = stm;
         const V3 V = sm > MINVAL ? pv * (1.0f / sm) : vown;
         st3(S + L.stlin + 3 * B.b, V);
         st3(S + L.stang + 3 * B.b, hs + cx - cross(mr, V));
       }
       sync();
     }
+    // the subtree momenta live in the RNE scratch, which the geom frames take next: their
+    // sensors and outputs are written now
+    for (int s = lane; s < d.nsensor; s += kWave) {
+      if (m.sensor_type[s] != SENS_SUBTREEANGMOM) continue;
+      float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
+      const int obj = m.sensor_objid[s];
+      out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+    }
+    if (last) {
+      const size_t wb = (size_t)w * nb;
+      for (int i = lane; i < 3 * nb; i += kWave) {
+        D.subtree_linvel[wb * 3 + i] = S[L.stlin + i];
+        D.subtree_angmom[wb * 3 + i] = S[L.stang + i];
+      }
+    }
+    sync();
     STAMP(8);
     if (lane == 0) { ints[0] = 0; ints[1] = 0; ints[2] = 0; ints[3] = 0; }
     // geom frames (here, not in kinematics: their LDS aliases regions dead after RNE)
@@ -1538,11 +1562,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int sl = lane; sl < d.ngeom_lds; sl += kWave) {
         const int g = m.lds_geom[sl];
         int b = m.geom_bodyid[g];
-        const float* R = S + L.xmat + 9 * b;
-        st3(S + L.gxpos + 3 * sl, v3(S + L.xpos + 3 * b) + mulv(R, v3(gpos + 3 * g)));
-        float Rg[9];
-        qmat(Rg, q4(gquat + 4 * g));
-        mat3mul(S + L.gxmat + 9 * sl, R, Rg);
+        const Q4 qb = q4(S + L.xquat + 4 * b);
+        st3(S + L.gxpos + 3 * sl, v3(S + L.xpos + 3 * b) + qrot(qb, v3(gpos + 3 * g)));
+        qmat(S + L.gxmat + 9 * sl, qmul(qb, q4(gquat + 4 * g)));
       }
     }
     sync();
@@ -1705,7 +1727,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       if (lane < ncon) {
         g1 = Si[L.con_g1 + idx]; g2 = Si[L.con_g2 + idx]; dist = S[L.con_dist + idx];
         px = S[L.con_pos + 3 * idx]; py = S[L.con_pos + 3 * idx + 1]; pz = S[L.con_pos + 3 * idx + 2];
-        nx = S[L.con_frame + 9 * idx]; ny = S[L.con_frame + 9 * idx + 1]; nz = S[L.con_frame + 9 * idx + 2];
+        nx = S[L.con_n + 3 * idx]; ny = S[L.con_n + 3 * idx + 1]; nz = S[L.con_n + 3 * idx + 2];
       }
       sync();
       if (lane < ncon) {
@@ -1715,15 +1737,10 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           Si[L.con_key + lane] = b1 | b2 << 8 | m.body_rootid[b1] << 16 | m.body_rootid[b2] << 24;
         }
         S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
-        // contact frame (mju_makeFrame) from the normal
+        // contact frame (mju_makeFrame): the unit normal; tangents by cframe() at use
         V3 n = {nx, ny, nz};
         n = n * (1.0f / fmaxf(norm(n), MINVAL));
-        V3 t = fabsf(n.y) < 0.5f ? V3{0, 1, 0} : V3{0, 0, 1};
-        t = t - n * dot(n, t);
-        t = t * (1.0f / fmaxf(norm(t), MINVAL));
-        V3 b = cross(n, t);
-        float* fr = S + L.con_frame + 9 * lane;
-        st3(fr, n); st3(fr + 3, t); st3(fr + 6, b);
+        st3(S + L.con_n + 3 * lane, n);
         // contact parameters (mj_contactParam semantics)
         const float* fri = MF(geom_friction);
         const float* sref = MF(geom_solref);
@@ -1856,14 +1873,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
             jd = jd + clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r2(cb)));
           if (b1 > 0 && ((bm >> b1) & 1ull))
             jd = jd - (clin + cross(cang, pos - v3(S + L.subtree_com + 3 * cb_r1(cb))));
-          const float* fr = S + L.con_frame + 9 * c;
-          float jn = fr[0] * jd.x + fr[1] * jd.y + fr[2] * jd.z;
+          const CFrame F = cframe(v3(S + L.con_n + 3 * c));
+          float jn = dot(F.n, jd);
           int r0 = Si[L.con_efc + c];
           if (Si[L.con_dim + c] == 1) {
             Jg[r0 * nvp + i] = jn;
           } else {
-            float jt1 = fr[3] * jd.x + fr[4] * jd.y + fr[5] * jd.z;
-            float jt2 = fr[6] * jd.x + fr[7] * jd.y + fr[8] * jd.z;
+            float jt1 = dot(F.t, jd);
+            float jt2 = dot(F.b, jd);
             float mu0 = S[L.con_mu + 2 * c], mu1 = S[L.con_mu + 2 * c + 1];
             Jg[(r0 + 0) * nvp + i] = jn + mu0 * jt1;
             Jg[(r0 + 1) * nvp + i] = jn - mu0 * jt1;
@@ -1911,13 +1928,13 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           V3 pc = v3(S + L.con_pos + 3 * c);
           const int cb = Si[L.con_key + c];
           V3 v = point_vel_r(S, L, cb_b2(cb), cb_r2(cb), pc) - point_vel_r(S, L, cb_b1(cb), cb_r1(cb), pc);
-          const float* fr = S + L.con_frame + 9 * c;
-          vel = fr[0] * v.x + fr[1] * v.y + fr[2] * v.z;
+          const CFrame F = cframe(v3(S + L.con_n + 3 * c));
+          vel = dot(F.n, v);
           if (type != EFC_FRICTIONLESS) {
             int kr = r - Si[L.con_efc + c];
-            const float* t = fr + 3 * (1 + (kr >> 1));
+            const V3 t = (kr >> 1) ? F.b : F.t;
             float mu = S[L.con_mu + 2 * c + (kr >> 1)];
-            vel += ((kr & 1) ? -mu : mu) * (t[0] * v.x + t[1] * v.y + t[2] * v.z);
+            vel += ((kr & 1) ? -mu : mu) * dot(t, v);
           }
         }
         S[L.efc_D + r] = 1.0f / Rr;
@@ -1959,7 +1976,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         }
         out[0] = r.x; out[1] = r.y; out[2] = r.z;
       } else if (type == SENS_SUBTREEANGMOM) {
-        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+        // written right after the subtree momenta (phase A; their LDS is reused since)
       } else if (type == SENS_FRAMEPOS) {
         const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
         out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
@@ -2047,13 +2064,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.xpos[wb * 3 + i] = S[L.xpos + i];
         D.xipos[wb * 3 + i] = S[L.xipos + i];
         D.subtree_com[wb * 3 + i] = S[L.subtree_com + i];
-        D.subtree_linvel[wb * 3 + i] = S[L.stlin + i];
-        D.subtree_angmom[wb * 3 + i] = S[L.stang + i];
       }
       for (int i = lane; i < 4 * nb; i += kWave) D.xquat[wb * 4 + i] = S[L.xquat + i];
-      for (int i = lane; i < 9 * nb; i += kWave) {
-        D.xmat[wb * 9 + i] = S[L.xmat + i];
-        D.ximat[wb * 9 + i] = S[L.ximat + i];
+      if (bl) {  // lane per body: xmat and ximat from the quaternions
+        float R[9], Ri[9];
+        qmat(R, xq);
+        qmat(Ri, qmul(xq, B.iquat));
+        float* om = D.xmat + (wb + B.b) * 9;
+        float* oi = D.ximat + (wb + B.b) * 9;
+#pragma unroll
+        for (int t = 0; t < 9; t++) { om[t] = R[t]; oi[t] = Ri[t]; }
       }
       for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
       // lane per geom: one model-index load per lane up front, not one per element (a
@@ -2077,17 +2097,12 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       for (int i = lane; i < nv; i += kWave) {
         size_t k = (size_t)w * nv + i;
         D.qacc_smooth[k] = S[L.qacc_smooth + i];
-        D.qfrc_bias[k] = S[L.qfrc_bias + i];
-        D.qfrc_passive[k] = S[L.qfrc_passive + i];
+        D.qfrc_bias[k] = qbias_i;  // lane i (nv <= 64)
+        D.qfrc_passive[k] = qpass_i;
         D.qfrc_actuator[k] = S[L.qfrc_act + i];
         D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
       }
-      for (int u = lane; u < nu; u += kWave) {
-        size_t k = (size_t)w * nu + u;
-        D.actuator_force[k] = S[L.act_force + u];
-        D.actuator_length[k] = S[L.act_len + u];
-        D.actuator_velocity[k] = S[L.act_vel + u];
-      }
+      for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
       size_t wc = (size_t)w * d.nconmax;
       for (int c = lane; c < d.nconmax; c += kWave) {
         bool v = c < ncon;
@@ -2095,7 +2110,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
         D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
         for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
-        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? S[L.con_frame + 9 * c + t] : 0.f;
+        const CFrame F = cframe(v ? v3(S + L.con_n + 3 * c) : V3{0.f, 0.f, 1.f});
+        const float fr[9] = {F.n.x, F.n.y, F.n.z, F.t.x, F.t.y, F.t.z, F.b.x, F.b.y, F.b.z};
+        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? fr[t] : 0.f;
       }
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
@@ -2120,7 +2137,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
     cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
     cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
     cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
-    cp4(gc + LC.con_frame, S + L.con_frame, (9 * C + 3) & ~3, lane);
+    for (int c = lane; c < C; c += kWave) {  // C pack: the full contact frames
+      const CFrame F = cframe(c < ncon ? v3(S + L.con_n + 3 * c) : V3{0.f, 0.f, 1.f});
+      float* fr = gc + LC.con_frame + 9 * c;
+      st3(fr, F.n); st3(fr + 3, F.t); st3(fr + 6, F.b);
+    }
     cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
     cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
     cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
@@ -2463,7 +2484,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         }
         out[0] = r.x; out[1] = r.y; out[2] = r.z;
       } else if (type == SENS_SUBTREEANGMOM) {
-        out[0] = S[L.stang + 3 * obj]; out[1] = S[L.stang + 3 * obj + 1]; out[2] = S[L.stang + 3 * obj + 2];
+        // written right after the subtree momenta (phase A; their LDS is reused since)
       } else if (type == SENS_FRAMEPOS) {
         const float* p = m.sensor_objtype[s] == OBJ_SITE ? S + L.sxpos + 3 * obj : S + L.xpos + 3 * obj;
         out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
