@@ -40,3 +40,17 @@ for ph, name in ((0, "A"), (1, "B"), (2, "C")):
       m = niter == it
       if m.any():
         print(f"   niter {it:2d}: {m.sum():5d} worlds dur med {np.median(d[m]):6.1f} max {d[m].max():6.1f}  nefc mean {nefc[m].mean():.1f}")
+# concurrency profile: resident worlds per phase over the substep (10 us bins), and the
+# time-average against the whole span -- low tails mean idle CUs at kernel boundaries
+span_end = max(us(tr[:, ph, 1]).max() for ph in range(3))
+bins = np.arange(0.0, span_end + 10.0, 10.0)
+print("t_us   " + "  ".join(f"{n:>5s}" for n in ("A", "B", "C")))
+act = []
+for ph in range(3):
+  s, e = us(tr[:, ph, 0]), us(tr[:, ph, 1])
+  act.append([int(((s < b + 10) & (e > b)).sum()) for b in bins])
+for i, b in enumerate(bins):
+  if i % 3 == 0:
+    print(f"{b:6.0f} " + "  ".join(f"{act[ph][i]:5d}" for ph in range(3)))
+tot = np.array(act).sum(axis=0)
+print(f"mean resident worlds over the span: {tot.mean():.0f} (peak {tot.max()})")
