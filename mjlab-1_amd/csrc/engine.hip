@@ -266,10 +266,15 @@ int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
     return 0;
   };
   if ((size_t)make_lds(d, 1).total * 4 <= (size_t)160 * 1024 / top) return 0;  // no need
-  // class 1 at the register-bound residency, class 2 at two thirds of it (when that still
-  // beats the full carve by a margin: measured, a class at <= 5 worlds/CU does not pay)
-  for (int w : {top, (2 * top) / 3}) {
-    if (w < 8) continue;
+  // one class at 5/6 of the register-bound residency (10 worlds/CU for the G1 Newton
+  // kernel), the rest at full capacity.  Measured (G1 4096, B span per substep): one class
+  // at 44 / 52 / 60 / 64 / 72 / 84 rows 202 / 196 / 197 / 197 / 203 / 198 us; two classes
+  // (44+84, 44+64, 60+100) 207-216 us -- concurrent class launches crowd each other out
+  // A class that at most doubles the full carve's residency does not repay the classify
+  // launch and the fork/join (Go1 8192: full carve 8 worlds/CU, B + gaps 136 -> 153 us)
+  const int full_per_cu = (int)((size_t)160 * 1024 / ((size_t)make_lds(d, 1).total * 4));
+  for (int w : {(5 * top) / 6}) {
+    if (w < 8 || 2 * full_per_cu > w) continue;
     const int r = cap_for(w);
     if (r > 0 && (n == 0 || r > caps[n - 1]) && n < kRowClasses) caps[n++] = r;
   }
