@@ -321,6 +321,35 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   m->dm.sensor_geommask1 = (const uint32_t*)p;
   if (upload(desc->sensor_geommask2, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask2 = (const uint32_t*)p;
+  {
+    // transposed single-slot contact-sensor masks (engine.h geom_csmask1/2); more than 64
+    // such sensors: ncsens = 0 and phase C matches sensor by sensor (serial path)
+    std::vector<int32_t> cs;
+    for (int s = 0; s < d.nsensor; s++)
+      if (desc->sensor_type[s] == mjx::SENS_CONTACT && desc->sensor_intprm[3 * s + 2] <= 1) cs.push_back(s);
+    const int ng = std::max(d.ngeom, 1);
+    std::vector<uint64_t> g1(ng, 0), g2(ng, 0);
+    if (cs.size() <= 64) {
+      for (size_t k = 0; k < cs.size(); k++) {
+        const uint32_t* a = desc->sensor_geommask1 + mjx::kMaskWords * cs[k];
+        const uint32_t* b = desc->sensor_geommask2 + mjx::kMaskWords * cs[k];
+        for (int g = 0; g < d.ngeom; g++) {
+          if ((a[g >> 5] >> (g & 31)) & 1u) g1[g] |= 1ull << k;
+          if ((b[g >> 5] >> (g & 31)) & 1u) g2[g] |= 1ull << k;
+        }
+      }
+      m->dm.ncsens = (int)cs.size();
+    } else {
+      m->dm.ncsens = 0;
+    }
+    if (cs.empty()) cs.push_back(0);
+    if (upload(cs.data(), sizeof(int32_t) * cs.size(), &p)) { delete m; return -1; }
+    m->dm.cs_sensor = (const int32_t*)p;
+    if (upload(g1.data(), sizeof(uint64_t) * g1.size(), &p)) { delete m; return -1; }
+    m->dm.geom_csmask1 = (const uint64_t*)p;
+    if (upload(g2.data(), sizeof(uint64_t) * g2.size(), &p)) { delete m; return -1; }
+    m->dm.geom_csmask2 = (const uint64_t*)p;
+  }
   *out = m;
   return 0;
 }

@@ -18,6 +18,15 @@ constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (reg
 constexpr int kRowClasses = 2;   // Newton row classes below the full capacity
 constexpr int kMaxAirSlots = 8;  // contact-sensor slots with air-time tracking
 
+enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
+enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
+enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
+enum { SENS_GYRO = 0, SENS_VELOCIMETER = 1, SENS_ACCELEROMETER = 2, SENS_SUBTREEANGMOM = 3,
+       SENS_CONTACT = 4, SENS_FRAMEPOS = 5, SENS_FRAMEQUAT = 6, SENS_JOINTPOS = 7,
+       SENS_JOINTVEL = 8 };
+enum { OBJ_SITE = 6 };
+enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
+
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
   int nhfield, nhfielddata, nlevel, nchild, nmocap;
@@ -58,6 +67,13 @@ struct DModel {
   const int32_t* hf_partner;
   const uint32_t* sensor_geommask1;
   const uint32_t* sensor_geommask2;
+  // single-slot contact sensors, transposed (host-derived): geom_csmask{1,2}[g] bit k is set
+  // when geom g is in the primary / secondary set of the k-th such sensor (cs_sensor[k]); a
+  // contact then finds every sensor it matches from two 64-bit loads per geom
+  int ncsens;
+  const int32_t* cs_sensor;
+  const uint64_t* geom_csmask1;
+  const uint64_t* geom_csmask2;
 };
 
 struct DData {

@@ -34,14 +34,6 @@ namespace mjx {
 #define MINIMP 0.0001f
 #define MAXIMP 0.9999f
 
-enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
-enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
-enum { JNT_FREE = 0, JNT_BALL = 1, JNT_SLIDE = 2, JNT_HINGE = 3 };
-enum { SENS_GYRO = 0, SENS_VELOCIMETER = 1, SENS_ACCELEROMETER = 2, SENS_SUBTREEANGMOM = 3,
-       SENS_CONTACT = 4, SENS_FRAMEPOS = 5, SENS_FRAMEQUAT = 6, SENS_JOINTPOS = 7,
-       SENS_JOINTVEL = 8 };
-enum { OBJ_SITE = 6 };
-enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE = 3 };
 
 // --------------------------------------------------------------------------- device math
 struct V3 { float x, y, z; };
@@ -904,20 +896,25 @@ __device__ __forceinline__ V3 point_vel_r(const float* S, const Lds& L, int b, i
 }
 
 // mjSENS_CONTACT with one slot (sensor/contact_sensor.py:16-97, 472-533), one wave per
-// world, lane = contact: match by the geom masks, then found = popcount(ballot), netforce =
-// wave sums of the signed world-frame forces, and for mindist / maxforce / none the
-// single selected contact is the wave argmin of its key (ties -> lowest contact index).
+// world, lane = contact: every sensor the contact matches comes from two transposed geom
+// masks (one load pair per contact, not one per sensor), then per sensor found =
+// popcount(ballot), netforce = wave sums of the signed world-frame forces, and for mindist /
+// maxforce / none the single selected contact is the wave argmin of its key (ties ->
+// lowest contact index).
 __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* Si, const Lds& L,
                                                      const DModel& m, const Dims& d, float* sd,
                                                      int ncon, int lane) {
   const int c = lane;
   const bool valid = c < ncon;
-  int g1 = 0, g2 = 0;
   V3 fg = {0, 0, 0}, fc = {0, 0, 0};
   float dist = 0.f;
+  // the sensors this contact matches, all at once: bit k of m1 (m2) = sensor k with the
+  // contact's geom 1 (geom 2) as its primary (geom_csmask1/2, host-derived)
+  uint64_t m1 = 0, m2 = 0;
   if (valid) {
-    g1 = Si[L.con_g1 + c];
-    g2 = Si[L.con_g2 + c];
+    const int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+    m1 = m.geom_csmask1[g1] & m.geom_csmask2[g2];
+    m2 = m.geom_csmask1[g2] & m.geom_csmask2[g1];
     dist = S[L.con_dist + c];
     const int r0 = Si[L.con_efc + c];
     if (Si[L.con_dim + c] == 1) {
@@ -929,19 +926,12 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     }
     fg = mulTv(S + L.con_frame + 9 * c, fc);
   }
-  for (int s = 0; s < d.nsensor; s++) {
-    if (m.sensor_type[s] != SENS_CONTACT) continue;
+  for (int k = 0; k < m.ncsens; k++) {
+    const int s = m.cs_sensor[k];
     const int32_t* ip = m.sensor_intprm + 3 * s;
-    if (ip[2] > 1) continue;  // multi-slot: serial path
     const int bits = ip[0], reduce = ip[1];
     float* out = sd + m.sensor_adr[s];
-    const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
-    const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
-    bool a1 = false, a2 = false;
-    if (valid) {
-      a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
-      a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
-    }
+    const bool a1 = (m1 >> k) & 1ull, a2 = (m2 >> k) & 1ull;
     const bool match = a1 || a2;
     const unsigned long long bal = __ballot(match);
     const float found = (float)__popcll(bal);
@@ -956,16 +946,19 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
       }
       continue;
     }
-    // one slot: the matching contact with the smallest key
-    float key = reduce == REDUCE_MINDIST ? dist
-              : reduce == REDUCE_MAXFORCE ? -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z)
-              : (float)c;
-    if (!match) key = FLT_MAX;
-    float kmin = key;
+    // one slot: the matching contact with the smallest key (ties -> lowest contact index)
+    int sel = -1;
+    if (reduce == REDUCE_NONE) {
+      sel = bal ? __ffsll((long long)bal) - 1 : -1;  // key = contact index
+    } else {
+      float key = reduce == REDUCE_MINDIST ? dist : -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z);
+      if (!match) key = FLT_MAX;
+      float kmin = key;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) kmin = fminf(kmin, __shfl_xor(kmin, o));
-    const unsigned long long win = __ballot(match && key == kmin);
-    const int sel = win ? __ffsll((long long)win) - 1 : -1;
+      for (int o = 32; o > 0; o >>= 1) kmin = fminf(kmin, __shfl_xor(kmin, o));
+      const unsigned long long win = __ballot(match && key == kmin);
+      sel = win ? __ffsll((long long)win) - 1 : -1;
+    }
     if (lane == 0) for (int i = 0; i < dim; i++) out[i] = 0.f;
     if (sel >= 0 && lane == sel) {
       const float sg = a1 ? 1.f : -1.f;
@@ -1954,8 +1947,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       int type = m.sensor_type[s];
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
-      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
-      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
+      // there are more than 64 of them (no transposed masks)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -2462,8 +2456,9 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       int type = m.sensor_type[s];
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
-      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave)
-      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1) continue;
+      // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
+      // there are more than 64 of them (no transposed masks)
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
