@@ -127,9 +127,9 @@ class ActorCritic(nn.Module):
     std = self.std.expand_as(mean) if self.noise_std_type == "scalar" else torch.exp(self.log_std).expand_as(mean)
     self.distribution = Normal(mean, std)
 
-  def act(self, obs: dict) -> torch.Tensor:
+  def act(self, obs: dict, sample: bool = True) -> torch.Tensor | None:
     self._update_distribution(self.actor_obs_normalizer(self.get_actor_obs(obs)))
-    return self.distribution.sample()
+    return self.distribution.sample() if sample else None
 
   def act_inference(self, obs: dict) -> torch.Tensor:
     return self.actor(self.actor_obs_normalizer(self.get_actor_obs(obs)))
@@ -202,7 +202,9 @@ class PPO:
     self.device = device
     self.policy = policy.to(device)
     self.learning_rate = learning_rate
-    self.optimizer = torch.optim.Adam(self.policy.parameters(), lr=learning_rate)
+    # fused Adam on the GPU: one kernel per step instead of one per parameter tensor
+    fused = torch.device(device).type == "cuda"
+    self.optimizer = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, fused=fused)
     self.clip_param, self.num_learning_epochs, self.num_mini_batches = clip_param, num_learning_epochs, num_mini_batches
     self.value_loss_coef, self.entropy_coef = value_loss_coef, entropy_coef
     self.gamma, self.lam, self.max_grad_norm = gamma, lam, max_grad_norm
@@ -210,22 +212,60 @@ class PPO:
     self.normalize_advantage_per_mini_batch = normalize_advantage_per_mini_batch
     self.multi_gpu = multi_gpu and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     self.storage: RolloutStorage | None = None
-    self._values = self._obs = None
+    self.graph_act = True  # GPU: rollout-time policy evaluation as one graph replay
+    self._act_graph = self._act_key = self._gobs = self._gout = None
 
   def init_storage(self, num_envs: int, num_transitions: int, obs: dict, num_actions: int):
     self.storage = RolloutStorage(num_envs, num_transitions, obs, num_actions, self.device)
+
+  def _act_core(self, obs: dict, eps: torch.Tensor | None = None):
+    if eps is None:
+      actions = self.policy.act(obs).detach()
+    else:  # reparameterised draw from given standard normals (the graphed path)
+      self.policy.act(obs, sample=False)
+      actions = (self.policy.action_mean + self.policy.action_std * eps).detach()
+    return (actions, self.policy.evaluate(obs).detach(),
+            self.policy.get_actions_log_prob(actions).detach().unsqueeze(-1),
+            self.policy.action_mean.detach(), self.policy.action_std.detach())
 
   def act(self, obs: dict) -> torch.Tensor:
     s, t = self.storage, self.storage.step
     for k, v in obs.items():  # the env's graph outputs are overwritten by the next step
       s.observations[k][t].copy_(v)
-    actions = self.policy.act(obs).detach()
-    s.actions[t].copy_(actions)
-    s.values[t].copy_(self.policy.evaluate(obs).detach())
-    s.actions_log_prob[t].copy_(self.policy.get_actions_log_prob(actions).detach().unsqueeze(-1))
-    s.mu[t].copy_(self.policy.action_mean.detach())
-    s.sigma[t].copy_(self.policy.action_std.detach())
-    return actions
+    if self.graph_act and torch.device(self.device).type == "cuda":
+      out = self._act_graphed(obs)
+    else:
+      out = self._act_core(obs)
+    for dst, src in zip((s.actions, s.values, s.actions_log_prob, s.mu, s.sigma), out):
+      dst[t].copy_(src)
+    return out[0]
+
+  def _act_graphed(self, obs: dict):
+    """The rollout-time policy evaluation (actor + critic MLPs, action draw, log-prob) as
+    one HIP graph replay on static input / output buffers: ~40 small launches per env step
+    become one.  The standard normals are drawn outside the graph (one launch) and the
+    action is mean + std * eps inside it -- the same distribution as Normal.sample().
+    Re-recorded when the observation groups change shape."""
+    key = tuple((k, tuple(v.shape)) for k, v in obs.items())
+    if self._act_graph is None or self._act_key != key:
+      self._gobs = {k: v.detach().clone() for k, v in obs.items()}
+      na = self.storage.actions.shape[-1]
+      self._geps = torch.zeros(self.storage.N, na, device=self.device)
+      side = torch.cuda.Stream(device=self.device)
+      side.wait_stream(torch.cuda.current_stream(self.device))
+      with torch.cuda.stream(side):
+        for _ in range(2):  # warm-up (allocator, lazy init) before recording
+          self._act_core(self._gobs, self._geps)
+      torch.cuda.current_stream(self.device).wait_stream(side)
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g):
+        self._gout = self._act_core(self._gobs, self._geps)
+      self._act_graph, self._act_key = g, key
+    for k, v in obs.items():
+      self._gobs[k].copy_(v)
+    self._geps.normal_()
+    self._act_graph.replay()
+    return self._gout
 
   def process_env_step(self, obs: dict, rewards: torch.Tensor, dones: torch.Tensor, extras: dict):
     s, t = self.storage, self.storage.step

@@ -28,6 +28,13 @@ def test_ppo_iterations_on_the_env(gpu_device, tmp_path):
   assert int(runner.alg.policy.actor_obs_normalizer.count) == 3 * 24 * 512
   moved = sum(float((a - b).abs().max()) for a, b in zip(before, runner.alg.policy.parameters()))
   assert moved > 0
+  # the graph-replayed rollout evaluation equals the eager one (values, means, std)
+  obs = vec.get_observations()
+  with torch.inference_mode():
+    graphed = [t.clone() for t in runner.alg._act_graphed(obs)]
+    eager = runner.alg._act_core(obs, runner.alg._geps)  # same standard normals
+    for i in range(5):
+      torch.testing.assert_close(graphed[i], eager[i], rtol=1e-5, atol=1e-5)
   ckpt = tmp_path / "model_3.pt"
   assert ckpt.exists()
   runner2 = OnPolicyRunner(vec, cfg, device=gpu_device)
