@@ -253,10 +253,13 @@ class ManagerBasedRlEnv:
     self._static_action = torch.zeros(self.num_envs, self.action_manager.total_action_dim,
                                       device=self.device)
 
+  @torch.inference_mode(False)
   def _capture(self, action: torch.Tensor):
     """Run one real sync-free step (it also warms the allocator and lazy tensors), then
     record the step into a HIP graph.  Recording executes nothing, so the env advances
-    exactly one step per call, as in eager mode."""
+    exactly one step per call, as in eager mode.  Recorded outside inference mode (a
+    runner steps the env inside it): tensors made here are updated in place by every
+    later step, and the capture registers the CUDA generator's graph state."""
     if self._fused is not None:
       self._fused.upload()  # command ranges may have changed (curriculum)
     self._static_action.copy_(action)

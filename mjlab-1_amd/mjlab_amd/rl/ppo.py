@@ -248,24 +248,32 @@ class PPO:
     Re-recorded when the observation groups change shape."""
     key = tuple((k, tuple(v.shape)) for k, v in obs.items())
     if self._act_graph is None or self._act_key != key:
-      self._gobs = {k: v.detach().clone() for k, v in obs.items()}
-      na = self.storage.actions.shape[-1]
-      self._geps = torch.zeros(self.storage.N, na, device=self.device)
-      side = torch.cuda.Stream(device=self.device)
-      side.wait_stream(torch.cuda.current_stream(self.device))
-      with torch.cuda.stream(side):
-        for _ in range(2):  # warm-up (allocator, lazy init) before recording
-          self._act_core(self._gobs, self._geps)
-      torch.cuda.current_stream(self.device).wait_stream(side)
-      g = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(g):
-        self._gout = self._act_core(self._gobs, self._geps)
-      self._act_graph, self._act_key = g, key
+      self._record_act(obs, key)
     for k, v in obs.items():
       self._gobs[k].copy_(v)
     self._geps.normal_()
     self._act_graph.replay()
     return self._gout
+
+  @torch.inference_mode(False)
+  @torch.no_grad()
+  def _record_act(self, obs: dict, key) -> None:
+    # recorded outside inference mode: the first capture of a process registers the CUDA
+    # generator's graph state tensors, and inference tensors there break every later
+    # capture made outside inference mode (e.g. the env's own step graph)
+    self._gobs = {k: v.detach().clone() for k, v in obs.items()}
+    na = self.storage.actions.shape[-1]
+    self._geps = torch.zeros(self.storage.N, na, device=self.device)
+    side = torch.cuda.Stream(device=self.device)
+    side.wait_stream(torch.cuda.current_stream(self.device))
+    with torch.cuda.stream(side):
+      for _ in range(2):  # warm-up (allocator, lazy init) before recording
+        self._act_core(self._gobs, self._geps)
+    torch.cuda.current_stream(self.device).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      self._gout = self._act_core(self._gobs, self._geps)
+    self._act_graph, self._act_key = g, key
 
   def process_env_step(self, obs: dict, rewards: torch.Tensor, dones: torch.Tensor, extras: dict):
     s, t = self.storage, self.storage.step

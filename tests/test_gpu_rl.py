@@ -44,3 +44,12 @@ def test_ppo_iterations_on_the_env(gpu_device, tmp_path):
   a1 = runner.get_inference_policy()(obs)
   a2 = runner2.get_inference_policy()(obs)
   torch.testing.assert_close(a1, a2)
+  # graphs recorded during the rollout (inside inference mode) leave later captures made
+  # outside it usable (the CUDA generator's graph state is not an inference tensor)
+  x = torch.zeros(8, device=gpu_device)
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    x.add_(1.0)
+  g.replay()
+  torch.cuda.synchronize()
+  assert float(x.sum()) == 8.0
