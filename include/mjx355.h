@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MJX_ABI_VERSION 2
+#define MJX_ABI_VERSION 3
 
 /* geom types (MuJoCo mjtGeom numbering) */
 enum { MJX_GEOM_PLANE = 0, MJX_GEOM_HFIELD = 1, MJX_GEOM_SPHERE = 2, MJX_GEOM_CAPSULE = 3,
@@ -48,7 +48,6 @@ enum { MJX_OBJ_NONE = 0, MJX_OBJ_BODY = 1, MJX_OBJ_XBODY = 2, MJX_OBJ_JOINT = 3,
 enum { MJX_REDUCE_NONE = 0, MJX_REDUCE_MINDIST = 1, MJX_REDUCE_MAXFORCE = 2,
        MJX_REDUCE_NETFORCE = 3 };
 enum { MJX_INT_EULER = 0, MJX_INT_IMPLICITFAST = 1 };
-#define MJX_MASK_WORDS 16 /* contact-sensor geom masks: 512 geoms */
 
 /* Host-side compiled model (fp64 / int32).  Field names follow mjModel.  Array
  * widths per element are in the trailing comment.  Filled by the Python scene
@@ -58,6 +57,7 @@ typedef struct mjxModelDesc_ {
   int abi_version;
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
   int nhfield, nhfielddata, nlevel;
+  int nmaskword; /* 32-bit words per contact-sensor geom mask: ceil(ngeom / 32) */
   int iterations, ls_iterations, integrator, cone;
   double timestep, tolerance, ls_tolerance, impratio, meaninertia;
   double gravity[3];
@@ -93,8 +93,10 @@ typedef struct mjxModelDesc_ {
   /* sensors */
   const int32_t *sensor_type, *sensor_objtype, *sensor_objid, *sensor_reftype, *sensor_refid,
       *sensor_adr, *sensor_dim, *sensor_intprm /*3*/;
-  const uint32_t *sensor_geommask1 /*MASK_WORDS*/, *sensor_geommask2 /*MASK_WORDS*/;
-  /* static broadphase: candidate geom pairs, geom1 has the lower geom type */
+  const uint32_t *sensor_geommask1 /*nmaskword*/, *sensor_geommask2 /*nmaskword*/;
+  /* static broadphase: candidate geom pairs, geom1 has the lower geom type.  Pairs with a
+   * static terrain geom (a heightfield, or a box on a body welded to the world) come last,
+   * grouped by that geom: the engine culls them per geom block (terrain broadphase). */
   const int32_t *pair_geom1, *pair_geom2;
   /* heightfields */
   const int32_t *hfield_nrow, *hfield_ncol, *hfield_adr;

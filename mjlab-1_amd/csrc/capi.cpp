@@ -6,6 +6,7 @@
 // ctypes; INTEGRATION.md shows the same binding for other hosts.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -69,8 +70,8 @@ struct mjxModel_ {
   std::map<std::string, std::pair<int64_t, int64_t>> float_dims;  // count, width
   std::map<std::string, std::pair<int64_t, int64_t>> int_dims;
   // static world frames of heightfield geoms (terrain bodies are welded to the world)
-  std::vector<int> hf_static_geoms;
-  std::vector<float> hf_static_xpos, hf_static_xmat;
+  std::vector<int> static_geoms;
+  std::vector<float> static_xpos, static_xmat;
 };
 
 struct mjxSim_ {
@@ -237,42 +238,57 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     m->dm.body_dofmask = (const uint64_t*)p;
   }
   {
-    // Heightfield broadphase tables.  The pair list is [regular pairs | hfield pairs], the
-    // hfield pairs grouped by hfield geom (the scene compiler emits them that way).
+    // Terrain broadphase tables.  The pair list is [regular pairs | terrain pairs], the
+    // terrain pairs grouped by their static terrain geom (the scene compiler emits them that
+    // way): a heightfield, or a box on a body welded to the world.  Those geoms keep no LDS
+    // frame; their world frames and AABBs are static and derived here.
     const int ng = desc->ngeom, np = desc->npair;
+    if (desc->nmaskword < (ng + 31) / 32) { delete m; return fail("nmaskword < ceil(ngeom / 32)"); }
+    m->dm.nmaskword = desc->nmaskword;
+    auto is_static = [&](int g) {
+      const int t = desc->geom_type[g];
+      return t == mjx::GEOM_HFIELD ||
+             (t == mjx::GEOM_BOX && desc->body_weldid[desc->geom_bodyid[g]] == 0);
+    };
     std::vector<int> geom_lds(ng > 0 ? ng : 1, -1), lds_geom;
     for (int g = 0; g < ng; g++)
-      if (desc->geom_type[g] != 1) { geom_lds[g] = (int)lds_geom.size(); lds_geom.push_back(g); }
+      if (!is_static(g)) { geom_lds[g] = (int)lds_geom.size(); lds_geom.push_back(g); }
+    d.ngeom_lds = (int)lds_geom.size();
     if (lds_geom.empty()) lds_geom.push_back(0);
-    d.ngeom_lds = 0;
-    for (int g = 0; g < ng; g++) d.ngeom_lds += desc->geom_type[g] != 1;
     int nreg = 0;
-    while (nreg < np && desc->geom_type[desc->pair_geom1[nreg]] != 1 &&
-           desc->geom_type[desc->pair_geom2[nreg]] != 1) nreg++;
-    std::vector<int> hf_geom, hf_adr, partner;
-    std::vector<char> seen(ng > 0 ? ng : 1, 0);
+    while (nreg < np && !is_static(desc->pair_geom1[nreg]) && !is_static(desc->pair_geom2[nreg])) nreg++;
+    std::vector<int> st_geom, st_adr, partner;
+    std::vector<char> seen(ng > 0 ? ng : 1, 0), done(ng > 0 ? ng : 1, 0);
     for (int q = nreg; q < np; q++) {
       const int g1 = desc->pair_geom1[q], g2 = desc->pair_geom2[q];
-      if (desc->geom_type[g1] != 1 || desc->geom_type[g2] == 1) {
+      if (is_static(g1) == is_static(g2)) {
         delete m;
-        return fail("pair list: heightfield pairs (hfield first) must follow all regular pairs");
+        return fail("pair list: terrain pairs (one static terrain geom each) must follow all regular pairs");
       }
-      if (hf_geom.empty() || hf_geom.back() != g1) {
-        for (int h : hf_geom)
-          if (h == g1) { delete m; return fail("pair list: hfield pair blocks must be contiguous"); }
-        hf_geom.push_back(g1);
-        hf_adr.push_back(q);
+      const int sg = is_static(g1) ? g1 : g2, pg = is_static(g1) ? g2 : g1;
+      if (desc->geom_type[sg] == mjx::GEOM_HFIELD ? sg != g1 : sg != g2) {
+        delete m;
+        return fail("pair list: a terrain pair must keep MuJoCo's geom-type order");
       }
-      if (!seen[g2]) { seen[g2] = 1; partner.push_back(g2); }
+      if (st_geom.empty() || st_geom.back() != sg) {
+        if (done[sg]) { delete m; return fail("pair list: terrain pair blocks must be contiguous"); }
+        done[sg] = 1;
+        st_geom.push_back(sg);
+        st_adr.push_back(q);
+      }
+      if (!seen[pg]) { seen[pg] = 1; partner.push_back(pg); }
     }
-    hf_adr.push_back(np);
+    st_adr.push_back(np);
     d.npair = nreg;
     d.npair_all = np;
-    d.nhfgeom = (int)hf_geom.size();
-    d.nhfpartner = (int)partner.size();
-    // static frames of every hfield geom (for D.geom_xpos / geom_xmat; kernels recompute)
+    d.nstatic = (int)st_geom.size();
+    d.nstpartner = (int)partner.size();
+    // static world frames of the terrain geoms (D.geom_xpos / geom_xmat, AABBs)
+    std::vector<float> aabb((size_t)6 * std::max((int)st_geom.size(), 1), 0.f);
+    std::vector<int> st_slot(ng > 0 ? ng : 1, -1);
+    for (size_t k = 0; k < st_geom.size(); k++) st_slot[st_geom[k]] = (int)k;
     for (int g = 0; g < ng; g++) {
-      if (desc->geom_type[g] != 1) continue;
+      if (!is_static(g)) continue;
       int b = desc->geom_bodyid[g];
       if (desc->body_weldid[b] != 0) {
         delete m;
@@ -301,25 +317,60 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
       for (auto it = chain.rbegin(); it != chain.rend(); ++it)
         step(desc->body_pos + 3 * *it, desc->body_quat + 4 * *it);
       step(desc->geom_pos + 3 * g, desc->geom_quat + 4 * g);
-      m->hf_static_geoms.push_back(g);
-      for (int i = 0; i < 3; i++) m->hf_static_xpos.push_back((float)x[i]);
-      for (int i = 0; i < 9; i++) m->hf_static_xmat.push_back((float)R[i]);
+      m->static_geoms.push_back(g);
+      for (int i = 0; i < 3; i++) m->static_xpos.push_back((float)x[i]);
+      for (int i = 0; i < 9; i++) m->static_xmat.push_back((float)R[i]);
+      const int k = st_slot[g];
+      if (k < 0) continue;
+      // local box: a box's half sizes; a heightfield's [-sx, sx] x [-sy, sy] x [-base, zmax]
+      double e[3], c[3] = {0, 0, 0};
+      if (desc->geom_type[g] == mjx::GEOM_BOX) {
+        for (int i = 0; i < 3; i++) e[i] = desc->geom_size[3 * g + i];
+      } else {
+        const double* hs = desc->hfield_size + 4 * desc->geom_dataid[g];
+        e[0] = hs[0]; e[1] = hs[1]; e[2] = 0.5 * (hs[2] + hs[3]);
+        c[2] = 0.5 * (hs[2] - hs[3]);
+      }
+      const double mg = desc->geom_margin[g];
+      for (int i = 0; i < 3; i++) {
+        const double cw = x[i] + R[3 * i] * c[0] + R[3 * i + 1] * c[1] + R[3 * i + 2] * c[2];
+        const double hw = std::fabs(R[3 * i]) * e[0] + std::fabs(R[3 * i + 1]) * e[1] +
+                          std::fabs(R[3 * i + 2]) * e[2] + mg;
+        // rounded outward so the fp32 cull never rejects what the fp64 bounds admit
+        aabb[6 * k + i] = std::nextafter((float)(cw - hw), -INFINITY);
+        aabb[6 * k + 3 + i] = std::nextafter((float)(cw + hw), INFINITY);
+      }
     }
-    if (hf_geom.empty()) { hf_geom.push_back(0); partner.push_back(0); }
+    const int nchunk = std::max(1, (d.nstatic + mjx::kStaticChunk - 1) / mjx::kStaticChunk);
+    std::vector<float> chunk((size_t)6 * nchunk);
+    for (int c = 0; c < nchunk; c++) {
+      float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int k = c * mjx::kStaticChunk; k < std::min(d.nstatic, (c + 1) * mjx::kStaticChunk); k++)
+        for (int i = 0; i < 3; i++) {
+          lo[i] = std::min(lo[i], aabb[6 * k + i]);
+          hi[i] = std::max(hi[i], aabb[6 * k + 3 + i]);
+        }
+      for (int i = 0; i < 3; i++) { chunk[6 * c + i] = lo[i]; chunk[6 * c + 3 + i] = hi[i]; }
+    }
+    if (st_geom.empty()) { st_geom.push_back(0); partner.push_back(0); }
     if (upload(geom_lds.data(), sizeof(int) * geom_lds.size(), &p)) { delete m; return -1; }
     m->dm.geom_lds = (const int32_t*)p;
     if (upload(lds_geom.data(), sizeof(int) * lds_geom.size(), &p)) { delete m; return -1; }
     m->dm.lds_geom = (const int32_t*)p;
-    if (upload(hf_geom.data(), sizeof(int) * hf_geom.size(), &p)) { delete m; return -1; }
-    m->dm.hf_geom = (const int32_t*)p;
-    if (upload(hf_adr.data(), sizeof(int) * hf_adr.size(), &p)) { delete m; return -1; }
-    m->dm.hf_pairadr = (const int32_t*)p;
+    if (upload(st_geom.data(), sizeof(int) * st_geom.size(), &p)) { delete m; return -1; }
+    m->dm.st_geom = (const int32_t*)p;
+    if (upload(st_adr.data(), sizeof(int) * st_adr.size(), &p)) { delete m; return -1; }
+    m->dm.st_pairadr = (const int32_t*)p;
     if (upload(partner.data(), sizeof(int) * partner.size(), &p)) { delete m; return -1; }
-    m->dm.hf_partner = (const int32_t*)p;
+    m->dm.st_partner = (const int32_t*)p;
+    if (upload(aabb.data(), sizeof(float) * aabb.size(), &p)) { delete m; return -1; }
+    m->dm.st_aabb = (const float*)p;
+    if (upload(chunk.data(), sizeof(float) * chunk.size(), &p)) { delete m; return -1; }
+    m->dm.st_chunk_aabb = (const float*)p;
   }
-  if (upload(desc->sensor_geommask1, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
+  if (upload(desc->sensor_geommask1, sizeof(uint32_t) * (size_t)desc->nmaskword * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask1 = (const uint32_t*)p;
-  if (upload(desc->sensor_geommask2, sizeof(uint32_t) * mjx::kMaskWords * d.nsensor, &p)) { delete m; return -1; }
+  if (upload(desc->sensor_geommask2, sizeof(uint32_t) * (size_t)desc->nmaskword * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask2 = (const uint32_t*)p;
   {
     // transposed single-slot contact-sensor masks (engine.h geom_csmask1/2); more than 64
@@ -331,8 +382,8 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     std::vector<uint64_t> g1(ng, 0), g2(ng, 0);
     if (cs.size() <= 64) {
       for (size_t k = 0; k < cs.size(); k++) {
-        const uint32_t* a = desc->sensor_geommask1 + mjx::kMaskWords * cs[k];
-        const uint32_t* b = desc->sensor_geommask2 + mjx::kMaskWords * cs[k];
+        const uint32_t* a = desc->sensor_geommask1 + (size_t)desc->nmaskword * cs[k];
+        const uint32_t* b = desc->sensor_geommask2 + (size_t)desc->nmaskword * cs[k];
         for (int g = 0; g < d.ngeom; g++) {
           if ((a[g >> 5] >> (g & 31)) & 1u) g1[g] |= 1ull << k;
           if ((b[g >> 5] >> (g & 31)) & 1u) g2[g] |= 1ull << k;
@@ -485,12 +536,12 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   e = mjx::prepare_step(host_params(s));
   if (e != hipSuccess) { delete s; return fail(std::string("prepare: ") + hipGetErrorString(e)); }
   // heightfield geom frames are static: write them once for every world
-  for (size_t k = 0; k < model->hf_static_geoms.size(); k++) {
-    const int g = model->hf_static_geoms[k];
+  for (size_t k = 0; k < model->static_geoms.size(); k++) {
+    const int g = model->static_geoms[k];
     std::vector<float> px((size_t)nworld * 3), pm((size_t)nworld * 9);
     for (int w = 0; w < nworld; w++) {
-      for (int i = 0; i < 3; i++) px[(size_t)w * 3 + i] = model->hf_static_xpos[3 * k + i];
-      for (int i = 0; i < 9; i++) pm[(size_t)w * 9 + i] = model->hf_static_xmat[9 * k + i];
+      for (int i = 0; i < 3; i++) px[(size_t)w * 3 + i] = model->static_xpos[3 * k + i];
+      for (int i = 0; i < 9; i++) pm[(size_t)w * 9 + i] = model->static_xmat[9 * k + i];
     }
     e = hipMemcpy2D(s->dd.geom_xpos + 3 * g, sizeof(float) * 3 * d.ngeom, px.data(),
                     sizeof(float) * 3, sizeof(float) * 3, nworld, hipMemcpyHostToDevice);

@@ -11,12 +11,12 @@
 namespace mjx {
 
 constexpr int kWave = 64;        // CDNA wavefront width
-constexpr int kMaskWords = 16;   // contact-sensor geom masks (512 geoms)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
 constexpr int kRowClasses = 2;   // Newton row classes below the full capacity
 constexpr int kMaxAirSlots = 8;  // contact-sensor slots with air-time tracking
+constexpr int kStaticChunk = 64; // terrain geoms per broadphase chunk
 
 enum { EFC_LIMIT = 0, EFC_FRICTIONLESS = 1, EFC_PYRAMIDAL = 2 };
 enum { GEOM_PLANE = 0, GEOM_HFIELD = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_BOX = 6 };
@@ -30,10 +30,10 @@ enum { REDUCE_NONE = 0, REDUCE_MINDIST = 1, REDUCE_MAXFORCE = 2, REDUCE_NETFORCE
 struct Dims {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, nsensor, nsensordata, npair;
   int nhfield, nhfielddata, nlevel, nchild, nmocap;
-  int ngeom_lds;  // geoms whose world frames phase A keeps in LDS (all but heightfields)
-  int npair_all;  // pair list length: [0, npair) regular pairs, [npair, npair_all) hfield pairs
-  int nhfgeom;    // heightfield geoms with candidate pairs (blocks of the hfield pair tail)
-  int nhfpartner; // distinct geoms paired with a heightfield (their union AABB culls hfields)
+  int ngeom_lds;  // geoms whose world frames phase A keeps in LDS (all but static terrain geoms)
+  int npair_all;  // pair list length: [0, npair) regular pairs, [npair, npair_all) terrain pairs
+  int nstatic;    // static terrain geoms (heightfields, world-welded boxes) with candidate pairs
+  int nstpartner; // distinct geoms paired with a terrain geom (their union AABB culls terrain)
   int nconmax;  // contacts per world held in LDS
   int njmax;    // constraint rows per world held in LDS
 };
@@ -56,15 +56,20 @@ struct DModel {
   const uint64_t* dof_ancmask;  // bit j set: dof j is dof i itself or an ancestor (host-derived)
   const uint64_t* body_submask;  // bit c set: body c is in body b's subtree (b included)
   const uint64_t* body_dofmask;  // bit j set: dof j moves body b (dofs of b and its ancestors)
-  // host-derived heightfield broadphase tables (capi.cpp): LDS frame slot per geom (-1 for
-  // hfields, whose static frames are computed on the fly), its inverse, hfield geoms with
-  // pairs, their pair blocks [hf_pairadr[i], hf_pairadr[i+1]) in the pair tail, and the
-  // distinct partner geoms
+  // host-derived terrain broadphase tables (capi.cpp).  Static terrain geoms (heightfields,
+  // boxes welded to the world) keep no LDS frame: geom_lds = -1, lds_geom its inverse over
+  // the others.  st_geom lists the terrain geoms with pairs, in pair-tail order; their pair
+  // blocks are [st_pairadr[i], st_pairadr[i+1]); st_aabb holds each one's world AABB (lo xyz,
+  // hi xyz, margin included) and st_chunk_aabb the union over chunks of kStaticChunk
+  // consecutive ones; st_partner lists the distinct partner geoms.
   const int32_t* geom_lds;
   const int32_t* lds_geom;
-  const int32_t* hf_geom;
-  const int32_t* hf_pairadr;
-  const int32_t* hf_partner;
+  const int32_t* st_geom;
+  const int32_t* st_pairadr;
+  const int32_t* st_partner;
+  const float* st_aabb;
+  const float* st_chunk_aabb;
+  int nmaskword;  // 32-bit words per contact-sensor geom mask
   const uint32_t* sensor_geommask1;
   const uint32_t* sensor_geommask2;
   // single-slot contact sensors, transposed (host-derived): geom_csmask{1,2}[g] bit k is set

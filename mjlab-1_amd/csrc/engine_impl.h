@@ -690,6 +690,95 @@ __device__ __forceinline__ int hfield_sphere(const ConOut& co, int key, int g1, 
   return 1;
 }
 
+// Box narrowphase (terrain boxes welded to the world; oracle/oracle.c col_box_sphere /
+// col_box_capsule, same arithmetic in fp64).  Signed distance of a box-frame point to the box
+// of half sizes s (negative inside).
+__device__ __forceinline__ float box_sd(V3 q, V3 s) {
+  const float dx = fabsf(q.x) - s.x, dy = fabsf(q.y) - s.y, dz = fabsf(q.z) - s.z;
+  const float ox = fmaxf(dx, 0.f), oy = fmaxf(dy, 0.f), oz = fmaxf(dz, 0.f);
+  return sqrtf(ox * ox + oy * oy + oz * oz) + fminf(fmaxf(dx, fmaxf(dy, dz)), 0.f);
+}
+// Sphere (geom g1, centre `loc` in the box frame F) against the box (geom g2), MuJoCo's
+// sphere-box contact: outside, the box point nearest the centre; inside, the face of least
+// penetration.  Normal from the sphere to the box, position midway between the surfaces.
+constexpr float kBoxFaceTie = 1e-5f;
+__device__ __forceinline__ int box_sphere(const ConOut& co, int key, int g1, int g2,
+                                          const HFrame& F, V3 s, V3 loc, float r, float margin) {
+  const V3 cl = {fminf(fmaxf(loc.x, -s.x), s.x), fminf(fmaxf(loc.y, -s.y), s.y),
+                 fminf(fmaxf(loc.z, -s.z), s.z)};
+  const V3 dv = cl - loc;
+  const float dist = norm(dv);
+  if (dist - r > margin) return 0;
+  V3 n, pos;
+  float cd;
+  if (dist > MINVAL) {
+    n = dv * (1.0f / dist);
+    pos = (cl + loc + n * r) * 0.5f;
+    cd = dist - r;
+  } else {
+    // centre inside: the face of least penetration, faces within kBoxFaceTie of it tied and
+    // taken in the order +z -z +x -x +y -y (terrain tops first).  A segment search inside
+    // the box ends on such ties (box_capsule): the order keeps fp32 and fp64 on one face.
+    const float f[6] = {s.z - loc.z, loc.z + s.z, s.x - loc.x, loc.x + s.x, s.y - loc.y, loc.y + s.y};
+    float least = f[0];
+#pragma unroll
+    for (int i = 1; i < 6; i++) least = fminf(least, f[i]);
+    int k = 5;
+#pragma unroll
+    for (int i = 4; i >= 0; i--)
+      if (f[i] <= least + kBoxFaceTie) k = i;
+    const float sg = (k & 1) ? 1.f : -1.f;  // a + face pushes the sphere out along +axis
+    const int ax = k < 2 ? 2 : (k < 4 ? 0 : 1);
+    n = {ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f};
+    pos = loc + n * (0.5f * (r - f[k]));
+    cd = -f[k] - r;
+  }
+  append(co, key, g1, g2, cd, F.p + mulv(F.R, pos), mulv(F.R, n));
+  return 1;
+}
+// Capsule (geom g1: centre cw, unit axis aw, half length hl, radius r; world frame) against
+// the box: sphere-box contacts at points of the capsule segment.  The signed box distance
+// along the segment is convex; its minimiser (golden-section search, fixed iteration count)
+// gives a contact only when it is deeper than both segment ends by kBoxMidEps (the segment
+// crosses a box edge or corner), together with the deeper end; otherwise the two ends are
+// the contact points (a capsule lying along a face), as plane-capsule.  At most 2 contacts.
+constexpr float kBoxMidEps = 1e-4f;
+constexpr int kBoxGolden = 28;
+__device__ __forceinline__ int box_capsule(const ConOut& co, int key, int g1, int g2,
+                                           const HFrame& F, V3 s, V3 cw, V3 aw, float hl,
+                                           float r, float margin) {
+  const V3 c = mulTv(F.R, cw - F.p), a = mulTv(F.R, aw);
+  if (box_sd(c, s) - hl - r > margin) return 0;
+  const V3 e0 = c - a * hl, e1 = c + a * hl;
+  const float sd0 = box_sd(e0, s), sd1 = box_sd(e1, s);
+  const float ig = 0.6180339887f;
+  float lo = -hl, hi = hl;
+  float x1 = hi - ig * (hi - lo), x2 = lo + ig * (hi - lo);
+  float f1 = box_sd(c + a * x1, s), f2 = box_sd(c + a * x2, s);
+  for (int it = 0; it < kBoxGolden; it++) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1;
+      x1 = hi - ig * (hi - lo);
+      f1 = box_sd(c + a * x1, s);
+    } else {
+      lo = x1; x1 = x2; f1 = f2;
+      x2 = lo + ig * (hi - lo);
+      f2 = box_sd(c + a * x2, s);
+    }
+  }
+  const float tm = 0.5f * (lo + hi);
+  const V3 em = c + a * tm;
+  int n = 0;
+  if (box_sd(em, s) < fminf(sd0, sd1) - kBoxMidEps) {
+    n += box_sphere(co, key, g1, g2, F, s, em, r, margin);
+    n += box_sphere(co, key + n, g1, g2, F, s, sd0 <= sd1 ? e0 : e1, r, margin);
+  } else {
+    n += box_sphere(co, key, g1, g2, F, s, e0, r, margin);
+    n += box_sphere(co, key + n, g1, g2, F, s, e1, r, margin);
+  }
+  return n;
+}
+
 // --------------------------------------------------------------------------- impedance
 __device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
   float dmin = fminf(MAXIMP, fmaxf(MINIMP, si[0])), dmax = fminf(MAXIMP, fmaxf(MINIMP, si[1]));
@@ -1621,17 +1710,30 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           V3 pa, pb;
           seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
           sphere_sphere(co, key, g1, g2, pa, s1[0], pb, s2[0], margin);
+        } else if (t2 == GEOM_BOX && (t1 == GEOM_SPHERE || t1 == GEOM_CAPSULE)) {
+          HFrame F;
+          F.p = p2;
+#pragma unroll
+          for (int i = 0; i < 9; i++) F.R[i] = S[L.gxmat + 9 * l2 + i];
+          if (t1 == GEOM_SPHERE) {
+            box_sphere(co, key, g1, g2, F, v3(s2), mulTv(F.R, p1 - F.p), s1[0], margin);
+          } else {
+            const float* R1 = S + L.gxmat + 9 * l1;
+            box_capsule(co, key, g1, g2, F, v3(s2), p1, V3{R1[2], R1[5], R1[8]}, s1[1], s1[0], margin);
+          }
         } else {
           atomicOr(&ints[3], 4);
         }
       }
-      // heightfield pairs: the union AABB of the hfield partners (bounding spheres) culls
-      // the hfield geoms (lane per hfield), then lanes take the pairs of each overlapping
-      // hfield block.  A terrain of many sub-terrain hfields costs ~1 block per world.
-      if (d.nhfgeom > 0) {
+      // terrain pairs: chunks of kStaticChunk terrain geoms, then the geoms themselves, are
+      // culled by their static world AABBs (capi.cpp) against the union AABB of the partner
+      // geoms' bounding spheres; lanes then take the pairs of each overlapping geom.  A
+      // terrain of thousands of boxes or hundreds of hfield patches costs ~1-2 chunks and a
+      // few geom blocks per world.
+      if (d.nstatic > 0) {
         float lo0 = 1e30f, lo1 = 1e30f, lo2 = 1e30f, hi0 = -1e30f, hi1 = -1e30f, hi2 = -1e30f;
-        for (int i = lane; i < d.nhfpartner; i += kWave) {
-          const int g = m.hf_partner[i];
+        for (int i = lane; i < d.nstpartner; i += kWave) {
+          const int g = m.st_partner[i];
           const V3 c = v3(S + L.gxpos + 3 * m.geom_lds[g]);
           const float r = grb[g] + gmargin[g];
           lo0 = fminf(lo0, c.x - r); lo1 = fminf(lo1, c.y - r); lo2 = fminf(lo2, c.z - r);
@@ -1639,55 +1741,78 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         }
         lo0 = wave_min(lo0); lo1 = wave_min(lo1); lo2 = wave_min(lo2);
         hi0 = wave_max(hi0); hi1 = wave_max(hi1); hi2 = wave_max(hi2);
+        auto overlap = [&](const float* bb) {
+          return bb[0] <= hi0 && bb[3] >= lo0 && bb[1] <= hi1 && bb[4] >= lo1 && bb[2] <= hi2 &&
+                 bb[5] >= lo2;
+        };
         const float* gpos = MF(geom_pos);
         const float* gquat = MF(geom_quat);
         const float* hsz_all = MF(hfield_size);
         const float* hdat_all = MF(hfield_data);
         int trunc = 0;
-        for (int base = 0; base < d.nhfgeom; base += kWave) {
-          bool act = false;
-          const int i = base + lane;
-          if (i < d.nhfgeom) {
-            const int g = m.hf_geom[i];
-            const HFrame F = hfield_frame(m, S, L, gpos, gquat, g);
-            const float* hs = hsz_all + 4 * m.geom_dataid[g];
-            // local box [-sx, sx] x [-sy, sy] x [-base, z_max] -> world AABB
-            const float ex = hs[0], ey = hs[1], ez = 0.5f * (hs[2] + hs[3]);
-            const V3 cw = F.p + mulv(F.R, V3{0, 0, 0.5f * (hs[2] - hs[3])});
-            const float wx = fabsf(F.R[0]) * ex + fabsf(F.R[1]) * ey + fabsf(F.R[2]) * ez;
-            const float wy = fabsf(F.R[3]) * ex + fabsf(F.R[4]) * ey + fabsf(F.R[5]) * ez;
-            const float wz = fabsf(F.R[6]) * ex + fabsf(F.R[7]) * ey + fabsf(F.R[8]) * ez;
-            act = cw.x - wx <= hi0 && cw.x + wx >= lo0 && cw.y - wy <= hi1 &&
-                  cw.y + wy >= lo1 && cw.z - wz <= hi2 && cw.z + wz >= lo2;
-          }
-          unsigned long long bal = __ballot(act);
-          while (bal) {
-            const int j = base + __ffsll((long long)bal) - 1;
-            bal &= bal - 1;
-            const int hg = m.hf_geom[j];
-            const HFrame F = hfield_frame(m, S, L, gpos, gquat, hg);
-            const int hid = m.geom_dataid[hg];
-            const float* hs = hsz_all + 4 * hid;
-            const float* hd = hdat_all + m.hfield_adr[hid];
-            const int nr = m.hfield_nrow[hid], nc = m.hfield_ncol[hid];
-            for (int p = m.hf_pairadr[j] + lane; p < m.hf_pairadr[j + 1]; p += kWave) {
-              const int g2 = m.pair_geom2[p];
-              const int t2 = m.geom_type[g2];
-              const int l2 = m.geom_lds[g2];
-              const V3 p2 = v3(S + L.gxpos + 3 * l2);
-              const float* s2 = gsize + 3 * g2;
-              const float margin = fmaxf(gmargin[hg], gmargin[g2]);
-              const int key = p * 8;
-              if (t2 == GEOM_SPHERE) {
-                hfield_sphere(co, key, hg, g2, F, hd, hs, nr, nc, p2, s2[0], margin, &trunc);
-              } else if (t2 == GEOM_CAPSULE) {
-                const float* R2 = S + L.gxmat + 9 * l2;
-                const V3 ax = {R2[2], R2[5], R2[8]};
-                int k = key;
-                k += hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 + ax * s2[1], s2[0], margin, &trunc);
-                hfield_sphere(co, k, hg, g2, F, hd, hs, nr, nc, p2 - ax * s2[1], s2[0], margin, &trunc);
-              } else {
-                atomicOr(&ints[3], 4);
+        static_assert(kStaticChunk == kWave, "lane per terrain geom of a chunk");
+        const int nchunk = (d.nstatic + kStaticChunk - 1) / kStaticChunk;
+        for (int cb = 0; cb < nchunk; cb += kWave) {
+          const int c = cb + lane;
+          unsigned long long cbal = __ballot(c < nchunk && overlap(m.st_chunk_aabb + 6 * c));
+          while (cbal) {
+            const int ch = cb + __ffsll((long long)cbal) - 1;
+            cbal &= cbal - 1;
+            const int i = ch * kStaticChunk + lane;
+            unsigned long long bal = __ballot(i < d.nstatic && overlap(m.st_aabb + 6 * i));
+            while (bal) {
+              const int j = ch * kStaticChunk + __ffsll((long long)bal) - 1;
+              bal &= bal - 1;
+              const int sg = m.st_geom[j];
+              const HFrame F = hfield_frame(m, S, L, gpos, gquat, sg);
+              if (m.geom_type[sg] == GEOM_HFIELD) {
+                const int hid = m.geom_dataid[sg];
+                const float* hs = hsz_all + 4 * hid;
+                const float* hd = hdat_all + m.hfield_adr[hid];
+                const int nr = m.hfield_nrow[hid], nc = m.hfield_ncol[hid];
+                for (int p = m.st_pairadr[j] + lane; p < m.st_pairadr[j + 1]; p += kWave) {
+                  const int g2 = m.pair_geom2[p];
+                  const int t2 = m.geom_type[g2];
+                  const int l2 = m.geom_lds[g2];
+                  const V3 p2 = v3(S + L.gxpos + 3 * l2);
+                  const float* s2 = gsize + 3 * g2;
+                  const float margin = fmaxf(gmargin[sg], gmargin[g2]);
+                  const int key = p * 8;
+                  if (t2 == GEOM_SPHERE) {
+                    hfield_sphere(co, key, sg, g2, F, hd, hs, nr, nc, p2, s2[0], margin, &trunc);
+                  } else if (t2 == GEOM_CAPSULE) {
+                    const float* R2 = S + L.gxmat + 9 * l2;
+                    const V3 ax = {R2[2], R2[5], R2[8]};
+                    int k = key;
+                    k += hfield_sphere(co, k, sg, g2, F, hd, hs, nr, nc, p2 + ax * s2[1], s2[0], margin, &trunc);
+                    hfield_sphere(co, k, sg, g2, F, hd, hs, nr, nc, p2 - ax * s2[1], s2[0], margin, &trunc);
+                  } else {
+                    atomicOr(&ints[3], 4);
+                  }
+                }
+              } else {  // box welded to the world: its partner is geom 1 (lower geom type)
+                const float* bb = m.st_aabb + 6 * j;
+                const V3 bs = v3(gsize + 3 * sg);
+                for (int p = m.st_pairadr[j] + lane; p < m.st_pairadr[j + 1]; p += kWave) {
+                  const int g1 = m.pair_geom1[p];
+                  const int t1 = m.geom_type[g1];
+                  const int l1 = m.geom_lds[g1];
+                  const V3 p1 = v3(S + L.gxpos + 3 * l1);
+                  const float margin = fmaxf(gmargin[sg], gmargin[g1]);
+                  const float rr = grb[g1] + margin;
+                  if (p1.x + rr < bb[0] || p1.x - rr > bb[3] || p1.y + rr < bb[1] ||
+                      p1.y - rr > bb[4] || p1.z + rr < bb[2] || p1.z - rr > bb[5]) continue;
+                  const float* s1 = gsize + 3 * g1;
+                  const int key = p * 8;
+                  if (t1 == GEOM_SPHERE) {
+                    box_sphere(co, key, g1, sg, F, bs, mulTv(F.R, p1 - F.p), s1[0], margin);
+                  } else if (t1 == GEOM_CAPSULE) {
+                    const float* R1 = S + L.gxmat + 9 * l1;
+                    box_capsule(co, key, g1, sg, F, bs, p1, V3{R1[2], R1[5], R1[8]}, s1[1], s1[0], margin);
+                  } else {
+                    atomicOr(&ints[3], 4);
+                  }
+                }
               }
             }
           }
@@ -1981,8 +2106,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       } else if (type == SENS_CONTACT) {
         const int32_t* ip = m.sensor_intprm + 3 * s;
         int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
-        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
-        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        const uint32_t* mk1 = m.sensor_geommask1 + m.nmaskword * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + m.nmaskword * s;
         int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
         int dim = m.sensor_dim[s];
         for (int i = 0; i < dim; i++) out[i] = 0.f;
@@ -2490,8 +2615,8 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       } else if (type == SENS_CONTACT) {
         const int32_t* ip = m.sensor_intprm + 3 * s;
         int bits = ip[0], reduce = ip[1], nslot = min(ip[2], 8);
-        const uint32_t* mk1 = m.sensor_geommask1 + kMaskWords * s;
-        const uint32_t* mk2 = m.sensor_geommask2 + kMaskWords * s;
+        const uint32_t* mk1 = m.sensor_geommask1 + m.nmaskword * s;
+        const uint32_t* mk2 = m.sensor_geommask2 + m.nmaskword * s;
         int fdim = ((bits & 1) || (bits & 8)) ? 1 : 3;
         int dim = m.sensor_dim[s];
         for (int i = 0; i < dim; i++) out[i] = 0.f;

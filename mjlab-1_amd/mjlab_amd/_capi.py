@@ -11,14 +11,14 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _I = ctypes.POINTER(ctypes.c_int32)
 _D = ctypes.POINTER(ctypes.c_double)
 _U64 = ctypes.POINTER(ctypes.c_uint64)
 _U32 = ctypes.POINTER(ctypes.c_uint32)
 
 _INT_SCALARS = ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "nsite", "nsensor", "nsensordata",
-                "npair", "nhfield", "nhfielddata", "nlevel", "iterations", "ls_iterations",
+                "npair", "nhfield", "nhfielddata", "nlevel", "nmaskword", "iterations", "ls_iterations",
                 "integrator", "cone"]
 _REAL_SCALARS = ["timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia"]
 # (name, ctype) in header order
@@ -72,6 +72,9 @@ def make_desc(model) -> tuple[ModelDesc, list]:
   for n in _INT_SCALARS:
     if n == "nlevel":
       d.nlevel = int(len(model.arrays["level_start"]) - 1)
+    elif n == "nmaskword":
+      mk = np.asarray(model.arrays["sensor_geommask1"])
+      d.nmaskword = int(mk.shape[1]) if mk.ndim == 2 else max(1, (model.ngeom + 31) // 32)
     else:
       setattr(d, n, int(getattr(model, n)))
   for n in _REAL_SCALARS:

@@ -43,7 +43,6 @@ CONTACT_FIELD_DIM = {"found": 1, "force": 3, "torque": 3, "dist": 1, "pos": 3, "
 CONTACT_FIELD_BIT = {"found": 0, "force": 1, "torque": 2, "dist": 3, "pos": 4, "normal": 5,
                      "tangent": 6}
 CONTACT_REDUCE = {"none": 0, "mindist": 1, "maxforce": 2, "netforce": 3}
-MASK_WORDS = 16  # contact-sensor geom masks: up to 512 geoms
 
 MINVAL = 1e-15
 
@@ -104,6 +103,15 @@ class HFieldSpec:
   pos: tuple
   size: tuple                  # (sx/2, sy/2, z_max, base)
   data: np.ndarray             # (nrow, ncol) float in [0,1]
+
+
+@dataclass
+class BoxSpec:
+  """Static box geom of a generated terrain (`terrains/primitive_terrains.py`): world
+  position and half sizes (MuJoCo box size)."""
+  name: str
+  pos: tuple
+  size: tuple
 
 
 @dataclass
@@ -209,12 +217,16 @@ def _inertial(b: XBody):
 
 def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
                   hfields: list[HFieldSpec] | None = None,
+                  terrain_geoms: list | None = None,
                   contact_sensors: list[ContactSensorSpec] = (),
                   timestep=0.002, iterations=100, ls_iterations=50, tolerance=1e-8,
                   ls_tolerance=0.01, impratio=1.0, integrator="implicitfast",
                   gravity=(0.0, 0.0, -9.81), cone="pyramidal") -> Model:
   """Assemble and compile a scene.  Body/geom ordering follows MuJoCo's depth-first
-  spec order: world, terrain, then each attached entity."""
+  spec order: world, terrain, then each attached entity.  terrain: "plane", "generator"
+  (terrain_geoms: the TerrainGenerator's HFieldSpec / BoxSpec geoms in generation order,
+  on the static `terrain` body, `terrains/terrain_generator.py:93-114`), "hfield" (the
+  same with heightfields only) or "none"."""
   if cone != "pyramidal":
     raise NotImplementedError("only pyramidal friction cones are supported")
   B = _Builder()
@@ -245,13 +257,20 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     tb = B.add_body("terrain", 0, np.zeros(3), np.array([1.0, 0, 0, 0]), None)
     from .mjcf import _GEOM_DEFAULTS
     add_geom(tb, "terrain", dict(_GEOM_DEFAULTS, type="plane", size=(0.0, 0.0, 0.01)), None)
-  elif terrain == "hfield":
+  elif terrain in ("hfield", "generator"):
     tb = B.add_body("terrain", 0, np.zeros(3), np.array([1.0, 0, 0, 0]), None)
     from .mjcf import _GEOM_DEFAULTS
-    for hi, hf in enumerate(hfields or []):
-      g = add_geom(tb, hf.name, dict(_GEOM_DEFAULTS, type="hfield", pos=hf.pos,
-                                      size=(hf.size[0], hf.size[1], hf.size[2])), None)
-      g["hfield"] = hi
+    tgeoms = list(terrain_geoms if terrain_geoms is not None else (hfields or []))
+    hfields = [t for t in tgeoms if isinstance(t, HFieldSpec)]
+    hi = 0
+    for tg in tgeoms:
+      if isinstance(tg, HFieldSpec):
+        g = add_geom(tb, tg.name, dict(_GEOM_DEFAULTS, type="hfield", pos=tg.pos,
+                                        size=(tg.size[0], tg.size[1], tg.size[2])), None)
+        g["hfield"] = hi
+        hi += 1
+      else:
+        add_geom(tb, tg.name, dict(_GEOM_DEFAULTS, type="box", pos=tg.pos, size=tg.size), None)
   elif terrain is not None and terrain != "none":
     raise ValueError(f"unknown terrain {terrain}")
 
@@ -514,40 +533,39 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
       A["actuator_forcelimited"][i] = 1
       A["actuator_forcerange"][i] = (-a["effort"], a["effort"])
 
-  # collision candidate pairs (static broadphase filter, MuJoCo filterBodyPair rules)
+  # collision candidate pairs (static broadphase filter, MuJoCo filterBodyPair rules),
+  # vectorised over the geom pairs i < j (a generated terrain has thousands of geoms)
   body_names = m.names["body"]
   excl = set()
   for b1, b2 in excludes:
     i1, i2 = body_names.index(b1), body_names.index(b2)
     excl.add((min(i1, i2), max(i1, i2)))
+  gtype = A["geom_type"]
+  ct, ca = A["geom_contype"], A["geom_conaffinity"]
+  wg = weldid[A["geom_bodyid"]]
+  pwg = weldid[A["body_parentid"][wg]]
+  ok = ((ct[:, None] & ca[None, :]) | (ct[None, :] & ca[:, None])) != 0
+  ok &= wg[:, None] != wg[None, :]
+  ok &= ~((wg[:, None] != 0) & (wg[None, :] != 0) & ((wg[:, None] == pwg[None, :]) | (wg[None, :] == pwg[:, None])))
+  pl, hfT = GEOM_TYPES["plane"], GEOM_TYPES["hfield"]
+  flat = (gtype == pl) | (gtype == hfT)
+  ok &= ~(flat[:, None] & flat[None, :])  # plane-plane, hfield-plane, hfield-hfield
+  ii, jj = np.nonzero(np.triu(ok, 1))
   pairs = []
-  for i in range(m.ngeom):
-    for j in range(i + 1, m.ngeom):
-      gi, gj = geoms[i], geoms[j]
-      if not ((gi["contype"] & gj["conaffinity"]) or (gj["contype"] & gi["conaffinity"])):
-        continue
-      bi, bj = gi["body"], gj["body"]
-      wi, wj = weldid[bi], weldid[bj]
-      if wi == wj:
-        continue
-      pwi, pwj = weldid[A["body_parentid"][wi]], weldid[A["body_parentid"][wj]]
-      if wi != 0 and wj != 0 and (wi == pwj or wj == pwi):
-        continue
-      if (min(bi, bj), max(bi, bj)) in excl:
-        continue
-      ti, tj = gi["type"], gj["type"]
-      if ti == GEOM_TYPES["plane"] and tj == GEOM_TYPES["plane"]:
-        continue
-      if ti == GEOM_TYPES["hfield"] and tj in (GEOM_TYPES["plane"], GEOM_TYPES["hfield"]):
-        continue
-      if tj == GEOM_TYPES["hfield"] and ti == GEOM_TYPES["plane"]:
-        continue
-      a, b = (i, j) if ti <= tj else (j, i)
-      pairs.append((a, b))
-  # heightfield pairs last, grouped by hfield geom (the engine's hfield broadphase walks
-  # them as per-hfield blocks; capi.cpp checks the layout)
-  hf = GEOM_TYPES["hfield"]
-  pairs.sort(key=lambda pr: (geoms[pr[0]]["type"] == hf, pr[0] if geoms[pr[0]]["type"] == hf else 0))
+  for i, j in zip(ii.tolist(), jj.tolist()):
+    bi, bj = int(A["geom_bodyid"][i]), int(A["geom_bodyid"][j])
+    if excl and (min(bi, bj), max(bi, bj)) in excl:
+      continue
+    pairs.append((i, j) if gtype[i] <= gtype[j] else (j, i))
+  # static terrain pairs last, grouped by their static geom (a heightfield, or a box welded
+  # to the world): the engine's terrain broadphase walks them as per-geom blocks behind
+  # chunk / geom bounding-box culls; capi.cpp checks the layout
+  static = (gtype == hfT) | ((gtype == GEOM_TYPES["box"]) & (wg == 0))
+  def tail_key(pr):
+    a, b = pr
+    sg = a if static[a] else (b if static[b] else -1)
+    return (sg >= 0, sg)
+  pairs.sort(key=tail_key)
   m.npair = len(pairs)
   A["pair_geom1"] = np.array([p[0] for p in pairs], np.int32)
   A["pair_geom2"] = np.array([p[1] for p in pairs], np.int32)
@@ -573,14 +591,15 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
   snames = []
   smask1, smask2 = [], []
   adr = 0
+  nmw = max(1, (m.ngeom + 31) // 32)  # mask words per sensor (mjxModelDesc.nmaskword)
 
   def push(t, ot, oi, rt, ri, dim, intprm=(0, 0, 0), name="", mk1=None, mk2=None):
     nonlocal adr
     stype.append(t); sobjtype.append(ot); sobjid.append(oi); sreftype.append(rt)
     srefid.append(ri); sadr.append(adr); sdim.append(dim); sint.append(intprm)
     snames.append(name)
-    smask1.append(mk1 if mk1 is not None else np.zeros(MASK_WORDS, np.uint32))
-    smask2.append(mk2 if mk2 is not None else np.zeros(MASK_WORDS, np.uint32))
+    smask1.append(mk1 if mk1 is not None else np.zeros(nmw, np.uint32))
+    smask2.append(mk2 if mk2 is not None else np.zeros(nmw, np.uint32))
     adr += dim
 
   for tag, attrs, name in xml_sensors:
@@ -606,12 +625,10 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     return out
 
   def geom_mask(mode, name):
-    mk = np.zeros(MASK_WORDS, np.uint32)
+    mk = np.zeros(nmw, np.uint32)
     if name is None:
       mk[:] = 0xFFFFFFFF
       return mk
-    if m.ngeom > 32 * MASK_WORDS:
-      raise ValueError("contact sensors support at most 128 geoms")
     if mode == "geom":
       gs = [m.names["geom"].index(name)]
     elif mode == "body":
@@ -647,8 +664,8 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
   A["sensor_adr"] = np.array(sadr, np.int32)
   A["sensor_dim"] = np.array(sdim, np.int32)
   A["sensor_intprm"] = np.array(sint, np.int32).reshape(-1, 3)
-  A["sensor_geommask1"] = np.array(smask1, np.uint32).reshape(-1, MASK_WORDS)
-  A["sensor_geommask2"] = np.array(smask2, np.uint32).reshape(-1, MASK_WORDS)
+  A["sensor_geommask1"] = np.array(smask1, np.uint32).reshape(-1, nmw)
+  A["sensor_geommask2"] = np.array(smask2, np.uint32).reshape(-1, nmw)
   m.names["sensor"] = snames
 
   # keyframe "init_state" (src/mjlab/entity/entity.py:170-207)

@@ -36,6 +36,8 @@ class SceneCfg:
   env_spacing: float = 2.0
   entities: dict = field(default_factory=lambda: {"robot": {"soft_joint_pos_limit_factor": 0.9}})
   contact_sensors: dict = field(default_factory=dict)
+  # generator terrains (TerrainImporterCfg.max_init_terrain_level): highest initial level
+  max_init_terrain_level: int | None = None
 
 
 @dataclass(kw_only=True)
@@ -96,7 +98,8 @@ class ManagerBasedRlEnv:
     self._fused = None
     model = load_scene(cfg.scene.scene_name)
     self.scene = Scene(model, cfg.scene.num_envs, device, cfg.scene.entities,
-                       cfg.scene.contact_sensors, cfg.scene.env_spacing)
+                       cfg.scene.contact_sensors, cfg.scene.env_spacing,
+                       max_init_terrain_level=cfg.scene.max_init_terrain_level)
     self.sim = Simulation(num_envs=cfg.scene.num_envs, cfg=cfg.sim, model=model, device=device)
     self.scene.initialize(self.sim.mj_model, self.sim.model, self.sim.data)
     self.common_step_counter = 0
@@ -205,6 +208,7 @@ class ManagerBasedRlEnv:
     return self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs
 
   def _reset_masked(self, mask: torch.Tensor) -> None:
+    self.curriculum_manager.compute_masked(mask)
     self.sim.reset_masked(mask)
     self.scene.reset_masked(mask)
     if "reset" in self.event_manager.available_modes:
@@ -280,7 +284,8 @@ class ManagerBasedRlEnv:
 
   def step(self, action: torch.Tensor):
     if getattr(self, "sync_free", False):
-      self.curriculum_manager.compute(env_ids=None)
+      # per-env curriculum terms (terrain levels) run on the reset mask inside the step
+      self.curriculum_manager.compute(env_ids=None, skip_masked=True)
       self._sim_step_counter += self.cfg.decimation
       self.common_step_counter += 1
       if not self._use_graph:
@@ -462,7 +467,25 @@ def make_velocity_env_cfg(scene_name: str) -> ManagerBasedRlEnvCfg:
 
 def unitree_g1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/g1/env_cfgs.py:20-175` (flat)."""
-  cfg = make_velocity_env_cfg("g1_velocity")
+  return _g1_velocity_cfg("g1_velocity", play)
+
+
+def unitree_g1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/config/g1/env_cfgs.py:20-148` (rough): the flat G1 task on the
+  box-stair terrain grid in curriculum layout (`velocity_env_cfg.py:318-324`,
+  max_init_terrain_level 5) with the terrain-level curriculum
+  (`velocity_env_cfg.py:296-300`).  Play mode keeps the training terrain (the
+  reference re-generates a smaller random grid for play)."""
+  cfg = _g1_velocity_cfg("g1_velocity_rough", play)
+  cfg.scene.max_init_terrain_level = 5
+  cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
+                                                        params={"command_name": "twist"}),
+                    **cfg.curriculum}
+  return cfg
+
+
+def _g1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
+  cfg = make_velocity_env_cfg(scene_name)
   cfg.scene.contact_sensors = {
     "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
     "self_collision": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
@@ -553,6 +576,7 @@ def _jump_g1_hfield(play: bool = False):
 
 TASKS = {
   "Mjlab-Velocity-Flat-Unitree-G1": unitree_g1_flat_env_cfg,
+  "Mjlab-Velocity-Rough-Unitree-G1": unitree_g1_rough_env_cfg,
   "Mjlab-Velocity-Flat-Unitree-Go1": unitree_go1_flat_env_cfg,
   "Mjlab-Tracking-Flat-Unitree-G1": _tracking_g1,
   "Mjlab-Jump-Flat-Unitree-G1": _jump_g1,

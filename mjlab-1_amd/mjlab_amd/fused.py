@@ -583,6 +583,13 @@ class FusedVelocityStep:
       if not self._engine_air:
         self._ok(L.mjx_task_substep(self._task, stream))
     self._ok(L.mjx_task_post(self._task, stream))
+    # per-env curriculum terms (terrain levels) of the resetting envs, before the reset
+    # events read the env origins (the reference's _reset_idx order)
+    cur = env.curriculum_manager
+    cur.compute_masked(self.reset_buf)
+    for name, state in getattr(cur, "_curriculum_state", {}).items():
+      if isinstance(state, torch.Tensor):
+        env.extras.setdefault("log", {})[f"Curriculum/{name}"] = state
     mask = ctypes.c_void_p(self.reset_buf.data_ptr())
     check(lib().mjx_reset(sim._sim, mask, stream))
     self._ok(L.mjx_task_reset(self._task, stream))

@@ -829,21 +829,35 @@ class CurriculumManager(ManagerBase):
   def reset_masked(self, mask) -> dict:
     return self.reset(None)
 
-  def compute(self, env_ids=None) -> None:
+  def compute(self, env_ids=None, skip_masked: bool = False) -> None:
+    """skip_masked: leave out the terms with a mask form (per-env terms such as the terrain
+    levels), which the sync-free step runs on its reset mask (compute_masked)."""
     if env_ids is None:
       env_ids = slice(None)
     for name, c in zip(self._term_names, self._term_cfgs):
+      if skip_masked and hasattr(c.func, "masked"):
+        continue
       self._curriculum_state[name] = c.func(self._env, env_ids, **c.params)
+
+  def compute_masked(self, mask) -> None:
+    """The mask forms of the per-env terms, for the envs resetting this step (the
+    reference runs them in _reset_idx, before the reset events read the env origins)."""
+    for name, c in zip(self._term_names, self._term_cfgs):
+      if hasattr(c.func, "masked"):
+        self._curriculum_state[name] = c.func.masked(self._env, mask, **c.params)
 
 
 class NullCurriculumManager:
   active_terms: list = []
+
+  def compute(self, env_ids=None, skip_masked: bool = False) -> None:
+    pass
+
+  def compute_masked(self, mask) -> None:
+    pass
 
   def reset(self, env_ids=None):
     return {}
 
   def reset_masked(self, mask):
     return {}
-
-  def compute(self, env_ids=None):
-    pass

@@ -657,6 +657,38 @@ class UniformVelocityCommand(CommandTerm):
 
 
 # =========================================================================== curriculum
+def _terrain_moves(env, ids, command_name, asset_name="robot"):
+  """`tasks/velocity/mdp/curriculums.py:30-64`: walked farther than half a patch -> up;
+  less than half the commanded distance over an episode -> down."""
+  terrain = env.scene.terrain
+  root = env.scene[asset_name].data.root_link_pos_w[ids, :2]
+  dist = torch.norm(root - env.scene.env_origins[ids, :2], dim=1)
+  up = dist > terrain.size[0] / 2
+  cmd = env.command_manager.get_command(command_name)[ids, :2]
+  down = (dist < torch.norm(cmd, dim=1) * env.max_episode_length_s * 0.5) & ~up
+  return up, down
+
+
+def terrain_levels_vel(env, env_ids, command_name: str, asset_cfg=None):
+  """Terrain-level curriculum (`curriculums.py:30-64`) for the resetting envs env_ids;
+  returns the mean terrain level."""
+  terrain = env.scene.terrain
+  up, down = _terrain_moves(env, env_ids, command_name, asset_cfg.name if asset_cfg else "robot")
+  terrain.update_env_origins(env_ids, up, down)
+  return torch.mean(terrain.terrain_levels.float())
+
+
+def _terrain_levels_vel_masked(env, mask, command_name: str, asset_cfg=None):
+  """The same over a reset mask (sync-free / graph-captured step)."""
+  terrain = env.scene.terrain
+  up, down = _terrain_moves(env, slice(None), command_name, asset_cfg.name if asset_cfg else "robot")
+  terrain.update_env_origins_masked(mask, up, down)
+  return terrain.mean_level
+
+
+terrain_levels_vel.masked = _terrain_levels_vel_masked
+
+
 def commands_vel(env, env_ids, command_name: str, velocity_stages: list):
   cfg = env.command_manager.get_term(command_name).cfg
   for st in velocity_stages:

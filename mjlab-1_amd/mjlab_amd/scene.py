@@ -558,11 +558,56 @@ class ContactSensor:
     return (a > 0.0) & (a < dt + abs_tol)
 
 
+class Terrain:
+  """The env-origin state of a generated terrain (`terrains/terrain_importer.py:186-244`):
+  sub-terrain spawn origins [rows, cols, 3], each env's level (row) and type (column), and
+  the level moves of the terrain curriculum.  `update_env_origins_masked` is the
+  sync-free form (reset mask, no host sync) of `update_env_origins`."""
+
+  def __init__(self, terrain_origins, size, num_envs: int, device: str, max_init_terrain_level=None):
+    from .terrains import curriculum_env_origins
+    o, lv, ty = curriculum_env_origins(terrain_origins, num_envs, max_init_terrain_level)
+    self.terrain_origins = torch.as_tensor(np.asarray(terrain_origins), dtype=torch.float32, device=device)
+    self.env_origins = o.to(device)
+    self.terrain_levels, self.terrain_types = lv.to(device), ty.to(device)
+    self.max_terrain_level = int(self.terrain_origins.shape[0])
+    self.size = size
+    self.mean_level = torch.zeros((), device=device)
+
+  def update_env_origins(self, env_ids, move_up, move_down):
+    lv = self.terrain_levels[env_ids] + 1 * move_up - 1 * move_down
+    lv = torch.where(lv >= self.max_terrain_level,
+                     torch.randint_like(lv, self.max_terrain_level), torch.clip(lv, 0))
+    self.terrain_levels[env_ids] = lv
+    self.env_origins[env_ids] = self.terrain_origins[self.terrain_levels[env_ids],
+                                                     self.terrain_types[env_ids]]
+
+  def update_env_origins_masked(self, mask, move_up, move_down):
+    lv = self.terrain_levels + move_up.long() - move_down.long()
+    lv = torch.where(lv >= self.max_terrain_level,
+                     torch.randint_like(lv, self.max_terrain_level), lv.clamp(min=0))
+    self.terrain_levels.copy_(torch.where(mask, lv, self.terrain_levels))
+    self.env_origins.copy_(torch.where(mask.unsqueeze(1),
+                                       self.terrain_origins[self.terrain_levels, self.terrain_types],
+                                       self.env_origins))
+    self.mean_level.copy_(self.terrain_levels.float().mean())
+
+  def randomize_env_origins(self, env_ids) -> None:
+    """`terrain_importer.py:203-222` (play mode)."""
+    rows, cols = self.terrain_origins.shape[:2]
+    n = len(env_ids)
+    self.terrain_levels[env_ids] = torch.randint(0, rows, (n,), device=self.env_origins.device)
+    self.terrain_types[env_ids] = torch.randint(0, cols, (n,), device=self.env_origins.device)
+    self.env_origins[env_ids] = self.terrain_origins[self.terrain_levels[env_ids],
+                                                     self.terrain_types[env_ids]]
+
+
 class Scene:
   """Entities + sensors + env origins for a compiled scene (scene/scene.py)."""
 
   def __init__(self, mj_model, num_envs: int, device: str, entities: dict[str, dict],
-               contact_sensors: dict[str, dict], env_spacing: float = 2.0):
+               contact_sensors: dict[str, dict], env_spacing: float = 2.0,
+               max_init_terrain_level: int | None = None):
     self._m = mj_model
     self.num_envs = num_envs
     self.device = device
@@ -583,13 +628,15 @@ class Scene:
           slots.append((prim, fld, int(adr[i]), int(dim[i])))
       self._sensors[cname] = ContactSensor(cname, slots, spec["fields"], spec.get("num_slots", 1),
                                            spec.get("track_air_time", False))
+    self.terrain = None
     if "terrain_origins" in mj_model.arrays:
       # generator terrain: curriculum origins over the sub-terrain spawn points
       # (terrain_importer.py:224-244), drawn from torch's global RNG like the reference
-      from .terrains import curriculum_env_origins
-      o, lv, ty = curriculum_env_origins(mj_model.arrays["terrain_origins"], num_envs)
-      self.env_origins = o.to(device)
-      self.terrain_levels, self.terrain_types = lv.to(device), ty.to(device)
+      size = tuple(float(v) for v in mj_model.arrays.get("terrain_size", (8.0, 8.0)))
+      self.terrain = Terrain(mj_model.arrays["terrain_origins"], size, num_envs, device,
+                             max_init_terrain_level)
+      self.env_origins = self.terrain.env_origins
+      self.terrain_levels, self.terrain_types = self.terrain.terrain_levels, self.terrain.terrain_types
       return
     # env origins on a grid (terrain_importer.py:246-261)
     rows = int(np.ceil(num_envs / int(np.sqrt(num_envs))))

@@ -95,10 +95,28 @@ def build_g1_jump_hfield(xml_path: str) -> Model:
   heightfield sub-terrains (terrains.hf_rough_terrains_cfg); spawn origins are stored
   with the model (`terrain_origins`, [rows, cols, 3])."""
   from .terrains import TerrainGenerator, hf_rough_terrains_cfg
-  hfields, origins = TerrainGenerator(hf_rough_terrains_cfg(seed=0)).generate()
+  cfg = hf_rough_terrains_cfg(seed=0)
+  hfields, origins = TerrainGenerator(cfg).generate()
   m = compile_scene([_g1_entity(xml_path, init=az.G1_JUMP_CROUCH)], terrain="hfield",
                     hfields=hfields, contact_sensors=_g1_jump_sensors(), **JUMP_SIM)
   m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  m.arrays["terrain_size"] = np.asarray(cfg.size, np.float64)
+  return m
+
+
+def build_g1_velocity_rough(xml_path: str) -> Model:
+  """`Mjlab-Velocity-Rough-Unitree-G1` (`tasks/velocity/config/g1/env_cfgs.py:20-56`,
+  `velocity_env_cfg.py:318-324`): the G1 velocity scene on ROUGH_TERRAINS_CFG in curriculum
+  layout -- 80 flat box patches, 120 pyramid / inverted-pyramid stair patches of 25 boxes,
+  the 20 m border; 3084 static boxes.  The reference draws the generator seed at random;
+  the compiled asset fixes it (seed 0)."""
+  from .terrains import TerrainGenerator, rough_terrains_cfg
+  cfg = rough_terrains_cfg(seed=0, curriculum=True)
+  geoms, origins = TerrainGenerator(cfg).generate()
+  m = compile_scene([_g1_entity(xml_path)], terrain="generator", terrain_geoms=geoms,
+                    contact_sensors=_g1_contact_sensors(), **VELOCITY_SIM)
+  m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  m.arrays["terrain_size"] = np.asarray(cfg.size, np.float64)
   return m
 
 
@@ -108,6 +126,7 @@ SCENE_BUILDERS = {
   "g1_jump": ("unitree_g1/xmls/g1.xml", build_g1_jump),
   "g1_jump_hfield": ("unitree_g1/xmls/g1.xml", build_g1_jump_hfield),
   "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
+  "g1_velocity_rough": ("unitree_g1/xmls/g1.xml", build_g1_velocity_rough),
 }
 
 

@@ -1,19 +1,23 @@
-"""Procedural heightfield terrains (config 5).
+"""Procedural terrains (row a30, config 5; row f3, box-stair rough terrain).
 
-Restates the reference's heightfield sub-terrain generators and the random-layout terrain
-grid: `src/mjlab/terrains/heightfield_terrains.py:104-499` (HfPyramidSlopedTerrainCfg,
-HfRandomUniformTerrainCfg, HfWaveTerrainCfg) and `terrains/terrain_generator.py:93-249`
-(TerrainGenerator: per-patch sub-terrain choice by proportion and difficulty, patch corner
-placement with the grid centred at the origin, spawn origins), plus the curriculum env
-origins of `terrains/terrain_importer.py:224-244`.  Same integer-pixel arithmetic, int16
-elevation grids and [0, 1] normalisation, so the elevation data, hfield sizes, geom
-positions and spawn origins are the reference's for the same seed.
+Restates the reference's terrain generators:
+  * heightfield sub-terrains, `src/mjlab/terrains/heightfield_terrains.py:104-499`
+    (HfPyramidSlopedTerrainCfg, HfRandomUniformTerrainCfg, HfWaveTerrainCfg) -- same
+    integer-pixel arithmetic, int16 elevation grids and [0, 1] normalisation;
+  * box sub-terrains, `terrains/primitive_terrains.py:52-376` (BoxFlatTerrainCfg,
+    BoxPyramidStairsTerrainCfg, BoxInvertedPyramidStairsTerrainCfg) with the plane / border
+    helpers of `terrains/utils.py:11-108`;
+  * the grid, `terrains/terrain_generator.py:62-249` (TerrainGenerator: random layout by
+    proportion and difficulty, or the curriculum layout -- type per column, difficulty
+    rising along rows; patch corners with the grid centred at the origin; spawn origins;
+    the 4-box border around the grid), and ROUGH_TERRAINS_CFG (`terrains/config.py:7-57`);
+  * the curriculum env origins of `terrains/terrain_importer.py:186-244`.
+For the same seed the geoms, sizes, positions and spawn origins are the reference's.
 
-The output is scene data for the compiler (`compiler.model.HFieldSpec`): the engine sees
-one hfield geom per patch on the static `terrain` body (MuJoCo's layout: nrow =
-noise.shape[0], ncol = noise.shape[1], data row-major).  Visual-only parts (textures,
-materials, lights) are not generated.  A zero-width border adds no boxes (MuJoCo rejects
-zero-size boxes); a positive border is out of scope (box narrowphase vs capsules).
+The output is scene data for the compiler (`compiler.model.HFieldSpec` / `BoxSpec`), in
+generation order on the static `terrain` body, named terrain_<k> as the reference names
+them.  Visual-only parts (colours, materials, lights) are not generated.  A zero-width grid
+border adds no boxes (MuJoCo rejects zero-size boxes).
 """
 
 from __future__ import annotations
@@ -22,7 +26,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .compiler.model import HFieldSpec
+from .compiler.model import BoxSpec, HFieldSpec
 
 
 @dataclass(kw_only=True)
@@ -185,6 +189,103 @@ class HfWaveTerrainCfg(SubTerrainCfg):
                    geom_z=lambda h: -h / 2, spawn_z=lambda h: 0.0)
 
 
+def _plane_box(size, height, center_zero=True, thickness=1.0):
+  """`terrains/utils.py:11-33` make_plane: a finite plane as one box."""
+  z = height - thickness / 2.0
+  pos = (0.0, 0.0, z) if center_zero else (size[0] / 2.0, size[1] / 2.0, z)
+  return [(pos, (size[0] / 2.0, size[1] / 2.0, thickness / 2.0))]
+
+
+def _border_boxes(size, inner, height, position):
+  """`terrains/utils.py:36-108` make_border: top, bottom, left, right boxes around
+  `inner` (centred at `position`) out to `size`."""
+  tx, ty = (size[0] - inner[0]) / 2.0, (size[1] - inner[1]) / 2.0
+  half_tb = (size[0] / 2.0, ty / 2.0, height / 2.0)
+  half_lr = (tx / 2.0, inner[1] / 2.0, height / 2.0)
+  return [((position[0], position[1] + inner[1] / 2.0 + ty / 2.0, position[2]), half_tb),
+          ((position[0], position[1] - inner[1] / 2.0 - ty / 2.0, position[2]), half_tb),
+          ((position[0] - inner[0] / 2.0 - tx / 2.0, position[1], position[2]), half_lr),
+          ((position[0] + inner[0] / 2.0 + tx / 2.0, position[1], position[2]), half_lr)]
+
+
+@dataclass(kw_only=True)
+class BoxFlatTerrainCfg(SubTerrainCfg):
+  """`primitive_terrains.py:52-63`: one 1 m thick box whose top is z = 0."""
+
+  def function(self, difficulty, rng):
+    origin = np.array([self.size[0] / 2, self.size[1] / 2, 0.0])
+    return _plane_box(self.size, 0.0, center_zero=False), origin
+
+
+@dataclass(kw_only=True)
+class BoxPyramidStairsTerrainCfg(SubTerrainCfg):
+  """`primitive_terrains.py:66-222`: rings of 4 boxes climbing to a central platform
+  (each step `step_width` wide, `step_height` higher), optional border boxes."""
+  border_width: float = 0.0
+  step_height_range: tuple[float, float]
+  step_width: float
+  platform_width: float = 1.0
+  holes: bool = False
+
+  def _steps(self, difficulty):
+    h = self.step_height_range[0] + difficulty * (self.step_height_range[1] - self.step_height_range[0])
+    nx = (self.size[0] - 2 * self.border_width - self.platform_width) // (2 * self.step_width) + 1
+    ny = (self.size[1] - 2 * self.border_width - self.platform_width) // (2 * self.step_width) + 1
+    return h, int(min(nx, ny))
+
+  def _ring(self, k, tsize, center, box_z, box_height):
+    """The 4 boxes of step k: top, bottom (along x), right, left (along y)."""
+    sw = self.step_width
+    if self.holes:
+      bsize = (self.platform_width, self.platform_width)
+    else:
+      bsize = (tsize[0] - 2 * k * sw, tsize[1] - 2 * k * sw)
+    off = (k + 0.5) * sw
+    half_x = (bsize[0] / 2.0, sw / 2.0, box_height / 2.0)
+    ylen = bsize[1] if self.holes else bsize[1] - 2 * sw
+    half_y = (sw / 2.0, ylen / 2.0, box_height / 2.0)
+    return [((center[0], center[1] + tsize[1] / 2.0 - off, box_z), half_x),
+            ((center[0], center[1] - tsize[1] / 2.0 + off, box_z), half_x),
+            ((center[0] + tsize[0] / 2.0 - off, center[1], box_z), half_y),
+            ((center[0] - tsize[0] / 2.0 + off, center[1], box_z), half_y)]
+
+  def _border(self, h, z):
+    if self.border_width > 0.0 and not self.holes:
+      inner = (self.size[0] - 2 * self.border_width, self.size[1] - 2 * self.border_width)
+      return _border_boxes(self.size, inner, h, (0.5 * self.size[0], 0.5 * self.size[1], z))
+    return []
+
+  def function(self, difficulty, rng):
+    h, n = self._steps(difficulty)
+    boxes = self._border(h, -h / 2)
+    c = (0.5 * self.size[0], 0.5 * self.size[1], 0.0)
+    ts = (self.size[0] - 2 * self.border_width, self.size[1] - 2 * self.border_width)
+    for k in range(n):
+      boxes += self._ring(k, ts, c, c[2] + k * h / 2.0, (k + 2) * h)
+    sw = self.step_width
+    boxes.append(((c[0], c[1], c[2] + n * h / 2),
+                  ((ts[0] - 2 * n * sw) / 2.0, (ts[1] - 2 * n * sw) / 2.0, (n + 2) * h / 2.0)))
+    return boxes, np.array([c[0], c[1], (n + 1) * h])
+
+
+@dataclass(kw_only=True)
+class BoxInvertedPyramidStairsTerrainCfg(BoxPyramidStairsTerrainCfg):
+  """`primitive_terrains.py:225-376`: the same rings stepping down into a pit."""
+
+  def function(self, difficulty, rng):
+    h, n = self._steps(difficulty)
+    total = (n + 1) * h
+    boxes = self._border(h, -0.5 * h)
+    c = (0.5 * self.size[0], 0.5 * self.size[1], 0.0)
+    ts = (self.size[0] - 2 * self.border_width, self.size[1] - 2 * self.border_width)
+    for k in range(n):
+      boxes += self._ring(k, ts, c, c[2] - total / 2 - (k + 1) * h / 2.0, total - (k + 1) * h)
+    sw = self.step_width
+    boxes.append(((c[0], c[1], c[2] - total - h / 2),
+                  ((ts[0] - 2 * n * sw) / 2.0, (ts[1] - 2 * n * sw) / 2.0, h / 2.0)))
+    return boxes, np.array([c[0], c[1], -(n + 1) * h])
+
+
 @dataclass(kw_only=True)
 class TerrainGeneratorCfg:
   """`terrain_generator.py:50-64`."""
@@ -200,35 +301,58 @@ class TerrainGeneratorCfg:
 
 
 class TerrainGenerator:
-  """`terrain_generator.py:67-249`: patch grid centred at the origin; random layout
+  """`terrain_generator.py:62-249`: patch grid centred at the origin; random layout
   (per-patch proportion draw + uniform difficulty) or curriculum layout (type per column,
-  difficulty rising along rows).  `generate()` returns the hfields (with world positions)
-  and the [num_rows, num_cols, 3] spawn origins."""
+  difficulty rising along rows), then the border boxes.  `generate()` returns the terrain
+  geoms (HFieldSpec / BoxSpec, world positions, generation order) and the
+  [num_rows, num_cols, 3] spawn origins."""
 
   def __init__(self, cfg: TerrainGeneratorCfg):
     if len(cfg.sub_terrains) == 0:
       raise ValueError("At least one sub_terrain must be specified.")
-    if cfg.border_width > 0:
-      raise NotImplementedError("terrain border boxes are out of scope (see module docstring)")
     self.cfg = cfg
     for sub in cfg.sub_terrains.values():
       sub.size = cfg.size
     seed = cfg.seed if cfg.seed is not None else np.random.randint(0, 10000)
     self.np_rng = np.random.default_rng(seed)
     self.terrain_origins = np.zeros((cfg.num_rows, cfg.num_cols, 3))
-    self.hfields: list[HFieldSpec] = []
+    self.geoms: list = []
+
+  @property
+  def hfields(self) -> list[HFieldSpec]:
+    return [g for g in self.geoms if isinstance(g, HFieldSpec)]
 
   def _position(self, row, col):
     c = self.cfg
     return np.array([-c.num_rows * c.size[0] * 0.5 + row * c.size[0],
                      -c.num_cols * c.size[1] * 0.5 + col * c.size[1], 0.0])
 
+  def _name(self):
+    return f"terrain_{len(self.geoms)}"
+
   def _create(self, world_position, difficulty, sub):
-    hf, origin = sub.function(difficulty, self.np_rng)
-    pos = tuple(float(v) for v in np.asarray(hf["pos"]) + world_position)
-    self.hfields.append(HFieldSpec(name=f"terrain_{len(self.hfields)}", pos=pos,
-                                   size=tuple(float(v) for v in hf["size"]), data=hf["data"]))
+    out, origin = sub.function(difficulty, self.np_rng)
+    if isinstance(out, dict):  # one heightfield
+      pos = tuple(float(v) for v in np.asarray(out["pos"]) + world_position)
+      self.geoms.append(HFieldSpec(name=self._name(), pos=pos,
+                                   size=tuple(float(v) for v in out["size"]), data=out["data"]))
+    else:  # boxes: (local position, half sizes)
+      for pos, half in out:
+        self.geoms.append(BoxSpec(name=self._name(),
+                                  pos=tuple(float(v) for v in np.asarray(pos, float) + world_position),
+                                  size=tuple(float(v) for v in half)))
     return origin + world_position
+
+  def _border(self):
+    """`terrain_generator.py:225-248`: 4 boxes around the grid, top at z = 0."""
+    c = self.cfg
+    if c.border_width <= 0:
+      return
+    inner = (c.num_rows * c.size[0], c.num_cols * c.size[1])
+    outer = (inner[0] + 2 * c.border_width, inner[1] + 2 * c.border_width)
+    for pos, half in _border_boxes(outer, inner, abs(c.border_height), (0, 0, -c.border_height / 2)):
+      self.geoms.append(BoxSpec(name=self._name(), pos=tuple(float(v) for v in pos),
+                                size=tuple(float(v) for v in half)))
 
   def generate(self):
     c = self.cfg
@@ -249,7 +373,22 @@ class TerrainGenerator:
         si = self.np_rng.choice(len(props), p=props)
         diff = self.np_rng.uniform(*c.difficulty_range)
         self.terrain_origins[row, col] = self._create(self._position(row, col), diff, subs[si])
-    return self.hfields, self.terrain_origins
+    self._border()
+    return self.geoms, self.terrain_origins
+
+
+def rough_terrains_cfg(seed: int | None = None, curriculum: bool = False) -> TerrainGeneratorCfg:
+  """ROUGH_TERRAINS_CFG (`terrains/config.py:7-57`): 8 m x 8 m patches, 10 x 20 grid, 20 m
+  border; 40% flat boxes, 30% pyramid stairs, 30% inverted pyramid stairs (its heightfield
+  entries are commented out in the reference)."""
+  stairs = dict(step_height_range=(0.0, 0.1), step_width=0.3, platform_width=3.0, border_width=1.0)
+  return TerrainGeneratorCfg(
+    seed=seed, curriculum=curriculum, size=(8.0, 8.0), border_width=20.0, num_rows=10, num_cols=20,
+    sub_terrains={
+      "flat": BoxFlatTerrainCfg(proportion=0.4),
+      "pyramid_stairs": BoxPyramidStairsTerrainCfg(proportion=0.3, **stairs),
+      "pyramid_stairs_inv": BoxInvertedPyramidStairsTerrainCfg(proportion=0.3, **stairs),
+    })
 
 
 def hf_rough_terrains_cfg(seed: int = 0) -> TerrainGeneratorCfg:

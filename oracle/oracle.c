@@ -590,6 +590,85 @@ static int col_hfield_sphere(const mjxModelDesc* m, orcData* d, int g1, int g2,
   return add_contact(d, g1, g2, best, pw, nw);
 }
 
+/* Box narrowphase (mjlab_amd engine_impl.h box_sphere / box_capsule restated in fp64).
+ * Signed distance of a box-frame point to the box of half sizes s (negative inside). */
+static double box_sd(const double* q, const double* s) {
+  double dx = fabs(q[0]) - s[0], dy = fabs(q[1]) - s[1], dz = fabs(q[2]) - s[2];
+  double ox = fmax(dx, 0), oy = fmax(dy, 0), oz = fmax(dz, 0);
+  return sqrt(ox * ox + oy * oy + oz * oz) + fmin(fmax(dx, fmax(dy, dz)), 0);
+}
+/* sphere (g1, centre loc in the frame of box g2) against the box: MuJoCo's sphere-box
+ * contact -- outside, the nearest box point; inside, the face of least penetration
+ * (ties within 1e-5 in the order +z -z +x -x +y -y); normal from the sphere to the box */
+static int col_box_sphere(orcData* d, int g1, int g2, const double* bp, const double* R,
+                          const double* s, const double* loc, double r, double margin) {
+  double cl[3], dv[3], n[3] = {0, 0, 0}, pos[3], cd;
+  for (int i = 0; i < 3; i++) cl[i] = fmin(fmax(loc[i], -s[i]), s[i]);
+  v3_sub(dv, cl, loc);
+  double dist = v3_norm(dv);
+  if (dist - r > margin) return 0;
+  if (dist > MINVAL) {
+    v3_scl(n, dv, 1.0 / dist);
+    for (int i = 0; i < 3; i++) pos[i] = 0.5 * (cl[i] + loc[i] + n[i] * r);
+    cd = dist - r;
+  } else {
+    /* faces +z -z +x -x +y -y; within 1e-5 of the least penetration: the first */
+    double f[6] = {s[2] - loc[2], loc[2] + s[2], s[0] - loc[0], loc[0] + s[0], s[1] - loc[1], loc[1] + s[1]};
+    double least = f[0];
+    for (int i = 1; i < 6; i++) least = fmin(least, f[i]);
+    int k = 0;
+    while (f[k] > least + 1e-5) k++;
+    const int ax = k < 2 ? 2 : (k < 4 ? 0 : 1);
+    n[ax] = (k & 1) ? 1.0 : -1.0;
+    for (int i = 0; i < 3; i++) pos[i] = loc[i] + n[i] * 0.5 * (r - f[k]);
+    cd = -f[k] - r;
+  }
+  double nw[3], pw[3];
+  m3_mulv(nw, R, n);
+  m3_mulv(pw, R, pos);
+  v3_add(pw, pw, bp);
+  return add_contact(d, g1, g2, cd, pw, nw);
+}
+/* capsule (g1) against box g2: sphere-box contacts at segment points -- the minimiser of
+ * the (convex) signed box distance along the segment, by golden-section search with the
+ * engine's iteration count, when it is deeper than both ends by 1e-4 (then with the deeper
+ * end), else the two ends */
+static int col_box_capsule(orcData* d, const mjxModelDesc* m, int g1, int g2, const double* bp,
+                           const double* R, const double* s, double margin) {
+  const double* cw = d->geom_xpos + 3 * g1;
+  const double* R1 = d->geom_xmat + 9 * g1;
+  double hl = m->geom_size[3 * g1 + 1], r = m->geom_size[3 * g1];
+  double t[3], aw[3] = {R1[2], R1[5], R1[8]}, c[3], a[3];
+  v3_sub(t, cw, bp);
+  m3_mulTv(c, R, t);
+  m3_mulTv(a, R, aw);
+  if (box_sd(c, s) - hl - r > margin) return 0;
+  double e0[3], e1[3], q[3];
+  for (int i = 0; i < 3; i++) { e0[i] = c[i] - a[i] * hl; e1[i] = c[i] + a[i] * hl; }
+  double sd0 = box_sd(e0, s), sd1 = box_sd(e1, s);
+  const double ig = 0.6180339887;
+  double lo = -hl, hi = hl, x1 = hi - ig * (hi - lo), x2 = lo + ig * (hi - lo);
+#define AT(x) (q[0] = c[0] + a[0] * (x), q[1] = c[1] + a[1] * (x), q[2] = c[2] + a[2] * (x), box_sd(q, s))
+  double f1 = AT(x1), f2 = AT(x2);
+  for (int it = 0; it < 28; it++) {
+    if (f1 <= f2) { hi = x2; x2 = x1; f2 = f1; x1 = hi - ig * (hi - lo); f1 = AT(x1); }
+    else { lo = x1; x1 = x2; f1 = f2; x2 = lo + ig * (hi - lo); f2 = AT(x2); }
+  }
+  double tm = 0.5 * (lo + hi), em[3];
+  double sdm = AT(tm);
+#undef AT
+  for (int i = 0; i < 3; i++) em[i] = c[i] + a[i] * tm;
+  int n = 0;
+  if (sdm < fmin(sd0, sd1) - 1e-4) {
+    n += col_box_sphere(d, g1, g2, bp, R, s, em, r, margin);
+    n += col_box_sphere(d, g1, g2, bp, R, s, sd0 <= sd1 ? e0 : e1, r, margin);
+  } else {
+    n += col_box_sphere(d, g1, g2, bp, R, s, e0, r, margin);
+    n += col_box_sphere(d, g1, g2, bp, R, s, e1, r, margin);
+  }
+  return n;
+}
+
 static void collision(const mjxModelDesc* m, orcData* d) {
   d->ncon = 0;
   for (int p = 0; p < m->npair; p++) {
@@ -643,6 +722,16 @@ static void collision(const mjxModelDesc* m, orcData* d) {
         col_hfield_sphere(m, d, g1, g2, e1, s2[0], margin);
       } else {
         d->overflow |= 4;
+      }
+    } else if (t2 == MJX_GEOM_BOX && (t1 == MJX_GEOM_SPHERE || t1 == MJX_GEOM_CAPSULE)) {
+      const double* R2 = d->geom_xmat + 9 * g2;
+      if (t1 == MJX_GEOM_SPHERE) {
+        double t[3], loc[3];
+        v3_sub(t, p1, p2);
+        m3_mulTv(loc, R2, t);
+        col_box_sphere(d, g1, g2, p2, R2, s2, loc, s1[0], margin);
+      } else {
+        col_box_capsule(d, m, g1, g2, p2, R2, s2, margin);
       }
     } else if (t1 == MJX_GEOM_SPHERE && t2 == MJX_GEOM_SPHERE) {
       col_sphere_sphere(d, g1, g2, p1, s1[0], p2, s2[0], margin);
@@ -1162,8 +1251,8 @@ static void sensors(const mjxModelDesc* m, orcData* d) {
       case MJX_SENS_CONTACT: {
         const int* ip = m->sensor_intprm + 3 * s;
         int bits = ip[0], reduce = ip[1], nslot = ip[2];
-        const uint32_t* mk1 = m->sensor_geommask1 + MJX_MASK_WORDS * s;
-        const uint32_t* mk2 = m->sensor_geommask2 + MJX_MASK_WORDS * s;
+        const uint32_t* mk1 = m->sensor_geommask1 + (size_t)m->nmaskword * s;
+        const uint32_t* mk2 = m->sensor_geommask2 + (size_t)m->nmaskword * s;
         int fdim = (bits & 1) || (bits & 8) ? 1 : 3;
         memset(out, 0, sizeof(double) * m->sensor_dim[s]);
         int found = 0;
