@@ -266,7 +266,8 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
         return fail("pair list: terrain pairs (one static terrain geom each) must follow all regular pairs");
       }
       const int sg = is_static(g1) ? g1 : g2, pg = is_static(g1) ? g2 : g1;
-      if (desc->geom_type[sg] == mjx::GEOM_HFIELD ? sg != g1 : sg != g2) {
+      if (desc->geom_type[sg] == mjx::GEOM_HFIELD ? sg != g1
+                                                  : (sg != g2 && desc->geom_type[pg] != mjx::GEOM_BOX)) {
         delete m;
         return fail("pair list: a terrain pair must keep MuJoCo's geom-type order");
       }
@@ -281,6 +282,10 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     st_adr.push_back(np);
     d.npair = nreg;
     d.npair_all = np;
+    d.nboxbox = 0;
+    for (int q = 0; q < np; q++)
+      d.nboxbox += desc->geom_type[desc->pair_geom1[q]] == mjx::GEOM_BOX &&
+                   desc->geom_type[desc->pair_geom2[q]] == mjx::GEOM_BOX;
     d.nstatic = (int)st_geom.size();
     d.nstpartner = (int)partner.size();
     // static world frames of the terrain geoms (D.geom_xpos / geom_xmat, AABBs)

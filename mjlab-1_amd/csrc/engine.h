@@ -34,6 +34,8 @@ struct Dims {
   int npair_all;  // pair list length: [0, npair) regular pairs, [npair, npair_all) terrain pairs
   int nstatic;    // static terrain geoms (heightfields, world-welded boxes) with candidate pairs
   int nstpartner; // distinct geoms paired with a terrain geom (their union AABB culls terrain)
+  int nboxbox;    // box-box candidate pairs: kernels specialised for a model without any are
+                  // compiled without the box-box narrowphase (its registers cost occupancy)
   int nconmax;  // contacts per world held in LDS
   int njmax;    // constraint rows per world held in LDS
 };

@@ -151,7 +151,7 @@ int find_spec(const Dims& d) {
            a.nhfield == b.nhfield && a.nhfielddata == b.nhfielddata && a.nlevel == b.nlevel &&
            a.nchild == b.nchild && a.nmocap == b.nmocap && a.ngeom_lds == b.ngeom_lds &&
            a.npair_all == b.npair_all && a.nstatic == b.nstatic &&
-           a.nstpartner == b.nstpartner && a.nconmax == b.nconmax && a.njmax == b.njmax;
+           a.nstpartner == b.nstpartner && a.nboxbox == b.nboxbox && a.nconmax == b.nconmax && a.njmax == b.njmax;
   };
 #define MJX_SPEC(id, scene, ...) if (eq(d, ModelSpec<id>::dims())) return id;
 #include "specs.inc"

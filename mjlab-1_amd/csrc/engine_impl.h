@@ -779,6 +779,113 @@ __device__ __forceinline__ int box_capsule(const ConOut& co, int key, int g1, in
   return n;
 }
 
+// Box against box (separating axes), in the frame of box 1 (F1, half sizes s1): box 2 has
+// centre c, axes b[0..2] (columns of R1^T R2) and half sizes s2.  Of the 15 axes (3 + 3 face
+// normals, 9 edge crosses) the one of least penetration wins -- box 1 faces, then box 2
+// faces, then edges, each later kind only when it separates more by kBoxFaceTie.  A face
+// axis clips the other box's most anti-parallel face against the reference face's side
+// planes (up to 8 points, those within the margin are contacts); an edge axis gives one
+// contact between the two supporting edges.  Normals from geom 1 to geom 2.
+__device__ __forceinline__ float vc(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+__device__ __forceinline__ V3 ev(int i) { return {i == 0 ? 1.f : 0.f, i == 1 ? 1.f : 0.f, i == 2 ? 1.f : 0.f}; }
+__device__ __forceinline__ int box_face_clip(V3 sr, int k, float sgn, V3 c, const V3 (&b)[3], V3 si,
+                                             float margin, V3 (&pt)[8], float (&dep)[8]) {
+  int j = 0;
+  float best = fabsf(vc(b[0], k));
+  for (int jj = 1; jj < 3; jj++) {
+    const float a = fabsf(vc(b[jj], k));
+    if (a > best + kBoxFaceTie) { best = a; j = jj; }
+  }
+  const float fs = sgn * vc(b[j], k) > 0.f ? -1.f : 1.f;  // incident face looks back at box R
+  const V3 fc = c + b[j] * (fs * vc(si, j));
+  const V3 u = b[(j + 1) % 3] * vc(si, (j + 1) % 3), v = b[(j + 2) % 3] * vc(si, (j + 2) % 3);
+  V3 poly[8], tmp[8];
+  poly[0] = fc + u + v; poly[1] = fc - u + v; poly[2] = fc - u - v; poly[3] = fc + u - v;
+  int np = 4;
+  for (int a = 0; a < 3; a++) {
+    if (a == k) continue;
+    for (int side = -1; side <= 1; side += 2) {
+      int nt = 0;
+      for (int i = 0; i < np; i++) {
+        const V3 P = poly[i], Q = poly[i + 1 < np ? i + 1 : 0];
+        const float dp = side * vc(P, a) - vc(sr, a), dq = side * vc(Q, a) - vc(sr, a);
+        if (dp <= 0.f) tmp[nt++] = P;
+        if ((dp <= 0.f) != (dq <= 0.f)) tmp[nt++] = P + (Q - P) * (dp / (dp - dq));
+      }
+      np = nt;
+      for (int i = 0; i < np; i++) poly[i] = tmp[i];
+    }
+  }
+  int nc = 0;
+  for (int i = 0; i < np; i++) {
+    const float d = sgn * vc(poly[i], k) - vc(sr, k);
+    if (d <= margin) { pt[nc] = poly[i]; dep[nc] = d; nc++; }
+  }
+  return nc;
+}
+__device__ __noinline__ int box_box(const ConOut& co, int key, int g1, int g2, const HFrame& F1,
+                                    V3 s1, const HFrame& F2, V3 s2, float margin) {
+  const V3 c = mulTv(F1.R, F2.p - F1.p);
+  V3 b[3];
+  for (int j = 0; j < 3; j++) b[j] = mulTv(F1.R, V3{F2.R[j], F2.R[3 + j], F2.R[6 + j]});
+  float best = -1e30f;
+  int kind = -1, ai = 0, aj = 0;
+  V3 n = {0.f, 0.f, 1.f};
+  for (int k = 0; k < 15; k++) {
+    V3 L;
+    int i = 0, j = 0;
+    if (k < 3) { i = k; L = ev(k); }
+    else if (k < 6) { j = k - 3; L = b[j]; }
+    else { i = (k - 6) / 3; j = (k - 6) % 3; L = cross(ev(i), b[j]); }
+    const float ln = norm(L);
+    if (ln < 1e-6f) continue;
+    L = L * (1.0f / ln);
+    const float r1 = s1.x * fabsf(L.x) + s1.y * fabsf(L.y) + s1.z * fabsf(L.z);
+    const float r2 = s2.x * fabsf(dot(L, b[0])) + s2.y * fabsf(dot(L, b[1])) + s2.z * fabsf(dot(L, b[2]));
+    const float d = dot(L, c);
+    const float sep = fabsf(d) - r1 - r2;
+    if (sep > margin) return 0;
+    const int kd = k < 3 ? 0 : (k < 6 ? 1 : 2);
+    if (kind < 0 || sep > best + (kd > kind ? kBoxFaceTie : 0.f)) {
+      best = sep; kind = kd; ai = i; aj = j;
+      n = d < 0.f ? L * -1.f : L;
+    }
+  }
+  V3 pt[8];
+  float dep[8];
+  int nc = 0;
+  if (kind == 0) {
+    nc = box_face_clip(s1, ai, vc(n, ai) < 0.f ? -1.f : 1.f, c, b, s2, margin, pt, dep);
+  } else if (kind == 1) {
+    // reference face on box 2: box 1 seen from box 2's frame, points mapped back
+    V3 bt[3];
+    for (int a = 0; a < 3; a++) bt[a] = {vc(b[0], a), vc(b[1], a), vc(b[2], a)};
+    const V3 c2 = {-dot(b[0], c), -dot(b[1], c), -dot(b[2], c)};
+    const float sg2 = dot(n, b[aj]) > 0.f ? -1.f : 1.f;  // box 2's face looking at box 1
+    nc = box_face_clip(s2, aj, sg2, c2, bt, s1, margin, pt, dep);
+    for (int q = 0; q < nc; q++) {
+      const V3 w = pt[q];
+      pt[q] = c + b[0] * w.x + b[1] * w.y + b[2] * w.z + n * dep[q];  // onto box 2's face side
+    }
+  } else {
+    // supporting edges: box 1's most along +n, box 2's most along -n
+    V3 p0 = {0.f, 0.f, 0.f}, q0 = c;
+    for (int a = 0; a < 3; a++) {
+      if (a != ai) p0 = p0 + ev(a) * (vc(n, a) > 0.f ? vc(s1, a) : -vc(s1, a));
+      if (a != aj) q0 = q0 + b[a] * (dot(n, b[a]) > 0.f ? -vc(s2, a) : vc(s2, a));
+    }
+    const V3 ea = ev(ai) * vc(s1, ai), eb = b[aj] * vc(s2, aj);
+    V3 pa, pb;
+    seg_seg(p0 - ea, p0 + ea, q0 - eb, q0 + eb, &pa, &pb);
+    const float d = dot(pb - pa, n);
+    if (d <= margin) { pt[0] = pb; dep[0] = d; nc = 1; }
+  }
+  // points lie on box 2; the contact sits halfway back to box 1 along the normal
+  for (int q = 0; q < nc; q++)
+    append(co, key + q, g1, g2, dep[q], F1.p + mulv(F1.R, pt[q] - n * (0.5f * dep[q])), mulv(F1.R, n));
+  return nc;
+}
+
 // --------------------------------------------------------------------------- impedance
 __device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
   float dmin = fminf(MAXIMP, fmaxf(MINIMP, si[0])), dmax = fminf(MAXIMP, fmaxf(MINIMP, si[1]));
@@ -828,6 +935,8 @@ template <int SP> struct ModelSpec {
 #include "specs.inc"
 #undef MJX_SPEC
 template <int SP> constexpr int spec_nr() { return nr_for_nv(ModelSpec<SP>::dims().nv); }
+// box-box narrowphase compiled in: generic kernels, and specialisations with such pairs
+template <int SP> constexpr bool kBoxBox = SP == 0 || ModelSpec<SP>::dims().nboxbox > 0;
 template <int SP, int K> struct SpecLds {
   static constexpr Lds get() {
     constexpr Lds v = make_lds(ModelSpec<SP>::dims(), K);
@@ -1710,6 +1819,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           V3 pa, pb;
           seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
           sphere_sphere(co, key, g1, g2, pa, s1[0], pb, s2[0], margin);
+        } else if (t1 == GEOM_BOX && t2 == GEOM_BOX) {
+          HFrame F1, F2;
+          F1.p = p1; F2.p = p2;
+          for (int i = 0; i < 9; i++) { F1.R[i] = S[L.gxmat + 9 * l1 + i]; F2.R[i] = S[L.gxmat + 9 * l2 + i]; }
+          if constexpr (kBoxBox<SP>) box_box(co, key, g1, g2, F1, v3(s1), F2, v3(s2), margin);
         } else if (t2 == GEOM_BOX && (t1 == GEOM_SPHERE || t1 == GEOM_CAPSULE)) {
           HFrame F;
           F.p = p2;
@@ -1790,11 +1904,13 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
                     atomicOr(&ints[3], 4);
                   }
                 }
-              } else {  // box welded to the world: its partner is geom 1 (lower geom type)
+              } else {  // box welded to the world: its partner is geom 1 (lower geom type),
+                        // or either side against another box (geom index order)
                 const float* bb = m.st_aabb + 6 * j;
                 const V3 bs = v3(gsize + 3 * sg);
                 for (int p = m.st_pairadr[j] + lane; p < m.st_pairadr[j + 1]; p += kWave) {
-                  const int g1 = m.pair_geom1[p];
+                  const int pa = m.pair_geom1[p], pb = m.pair_geom2[p];
+                  const int g1 = pa == sg ? pb : pa;  // the partner
                   const int t1 = m.geom_type[g1];
                   const int l1 = m.geom_lds[g1];
                   const V3 p1 = v3(S + L.gxpos + 3 * l1);
@@ -1809,6 +1925,14 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
                   } else if (t1 == GEOM_CAPSULE) {
                     const float* R1 = S + L.gxmat + 9 * l1;
                     box_capsule(co, key, g1, sg, F, bs, p1, V3{R1[2], R1[5], R1[8]}, s1[1], s1[0], margin);
+                  } else if (t1 == GEOM_BOX) {
+                    HFrame Fp;
+                    Fp.p = p1;
+                    for (int i = 0; i < 9; i++) Fp.R[i] = S[L.gxmat + 9 * l1 + i];
+                    if constexpr (kBoxBox<SP>) {
+                      if (pa == sg) box_box(co, key, pa, pb, F, bs, Fp, v3(s1), margin);
+                      else box_box(co, key, pa, pb, Fp, v3(s1), F, bs, margin);
+                    }
                   } else {
                     atomicOr(&ints[3], 4);
                   }

@@ -528,7 +528,22 @@ def _g1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
 
 def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/go1/env_cfgs.py:15-127` (flat)."""
-  cfg = make_velocity_env_cfg("go1_velocity")
+  return _go1_velocity_cfg("go1_velocity", play)
+
+
+def unitree_go1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/config/go1/env_cfgs.py:15-112` (rough): the flat Go1 task on the
+  curriculum box-stair grid with the terrain-level curriculum (as unitree_g1_rough_env_cfg)."""
+  cfg = _go1_velocity_cfg("go1_velocity_rough", play)
+  cfg.scene.max_init_terrain_level = 5
+  cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
+                                                        params={"command_name": "twist"}),
+                    **cfg.curriculum}
+  return cfg
+
+
+def _go1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
+  cfg = make_velocity_env_cfg(scene_name)
   cfg.scene.contact_sensors = {
     "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
     "nonfoot_ground_touch": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
@@ -578,6 +593,7 @@ TASKS = {
   "Mjlab-Velocity-Flat-Unitree-G1": unitree_g1_flat_env_cfg,
   "Mjlab-Velocity-Rough-Unitree-G1": unitree_g1_rough_env_cfg,
   "Mjlab-Velocity-Flat-Unitree-Go1": unitree_go1_flat_env_cfg,
+  "Mjlab-Velocity-Rough-Unitree-Go1": unitree_go1_rough_env_cfg,
   "Mjlab-Tracking-Flat-Unitree-G1": _tracking_g1,
   "Mjlab-Jump-Flat-Unitree-G1": _jump_g1,
   "Mjlab-Jump-Hfield-Unitree-G1": _jump_g1_hfield,

@@ -54,7 +54,7 @@ def build_g1_velocity(xml_path: str) -> Model:
                        **VELOCITY_SIM)
 
 
-def build_go1_velocity(xml_path: str) -> Model:
+def build_go1_velocity(xml_path: str, terrain: str = "plane", terrain_geoms=None) -> Model:
   ent = EntitySpec("robot", parse_mjcf(xml_path), collisions=(az.GO1_FULL_COLLISION,),
                    actuators=az.go1_actuators(), init_pos=az.GO1_INIT["pos"],
                    init_joint_pos=az.GO1_INIT["joint_pos"])
@@ -69,7 +69,21 @@ def build_go1_velocity(xml_path: str) -> Model:
     ContactSensorSpec("nonfoot_ground_touch", "geom", nonfoot, "body", "terrain",
                       ("found",), "none", 1),
   ]
-  return compile_scene([ent], contact_sensors=sensors, **VELOCITY_SIM)
+  return compile_scene([ent], terrain=terrain, terrain_geoms=terrain_geoms, contact_sensors=sensors,
+                       **VELOCITY_SIM)
+
+
+def build_go1_velocity_rough(xml_path: str) -> Model:
+  """`Mjlab-Velocity-Rough-Unitree-Go1` (`tasks/velocity/config/go1/env_cfgs.py:15-112`): the
+  Go1 velocity scene on the curriculum box-stair grid (as build_g1_velocity_rough); the
+  trunk box meets the terrain boxes through the box-box narrowphase."""
+  from .terrains import TerrainGenerator, rough_terrains_cfg
+  cfg = rough_terrains_cfg(seed=0, curriculum=True)
+  geoms, origins = TerrainGenerator(cfg).generate()
+  m = build_go1_velocity(xml_path, terrain="generator", terrain_geoms=geoms)
+  m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  m.arrays["terrain_size"] = np.asarray(cfg.size, np.float64)
+  return m
 
 
 def build_g1_tracking(xml_path: str) -> Model:
@@ -127,6 +141,7 @@ SCENE_BUILDERS = {
   "g1_jump_hfield": ("unitree_g1/xmls/g1.xml", build_g1_jump_hfield),
   "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
   "g1_velocity_rough": ("unitree_g1/xmls/g1.xml", build_g1_velocity_rough),
+  "go1_velocity_rough": ("unitree_go1/xmls/go1.xml", build_go1_velocity_rough),
 }
 
 

@@ -669,6 +669,137 @@ static int col_box_capsule(orcData* d, const mjxModelDesc* m, int g1, int g2, co
   return n;
 }
 
+/* box (g1) against box (g2), separating axes in box 1's frame (engine_impl.h box_box): the
+ * axis of least penetration among 3 + 3 face normals and 9 edge crosses (box 1 faces, then
+ * box 2 faces, then edges, a later kind only when it separates more by 1e-5); a face axis
+ * clips the other box's most anti-parallel face against the reference face's side planes,
+ * an edge axis gives one contact between the supporting edges */
+static int box_face_clip(const double* sr, int k, double sgn, const double* c, const double b[3][3],
+                         const double* si, double margin, double pt[8][3], double* dep) {
+  int j = 0;
+  double best = fabs(b[0][k]);
+  for (int jj = 1; jj < 3; jj++)
+    if (fabs(b[jj][k]) > best + 1e-5) { best = fabs(b[jj][k]); j = jj; }
+  double fs = sgn * b[j][k] > 0 ? -1.0 : 1.0;
+  int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+  double fc[3], u[3], v[3], poly[8][3], tmp[8][3];
+  for (int i = 0; i < 3; i++) {
+    fc[i] = c[i] + b[j][i] * fs * si[j];
+    u[i] = b[j1][i] * si[j1];
+    v[i] = b[j2][i] * si[j2];
+    poly[0][i] = fc[i] + u[i] + v[i]; poly[1][i] = fc[i] - u[i] + v[i];
+    poly[2][i] = fc[i] - u[i] - v[i]; poly[3][i] = fc[i] + u[i] - v[i];
+  }
+  int np = 4;
+  for (int a = 0; a < 3; a++) {
+    if (a == k) continue;
+    for (int side = -1; side <= 1; side += 2) {
+      int nt = 0;
+      for (int i = 0; i < np; i++) {
+        const double* P = poly[i];
+        const double* Q = poly[i + 1 < np ? i + 1 : 0];
+        double dp = side * P[a] - sr[a], dq = side * Q[a] - sr[a];
+        if (dp <= 0) { v3_copy(tmp[nt], P); nt++; }
+        if ((dp <= 0) != (dq <= 0)) {
+          double t = dp / (dp - dq);
+          for (int x = 0; x < 3; x++) tmp[nt][x] = P[x] + (Q[x] - P[x]) * t;
+          nt++;
+        }
+      }
+      np = nt;
+      for (int i = 0; i < np; i++) v3_copy(poly[i], tmp[i]);
+    }
+  }
+  int nc = 0;
+  for (int i = 0; i < np; i++) {
+    double dd = sgn * poly[i][k] - sr[k];
+    if (dd <= margin) { v3_copy(pt[nc], poly[i]); dep[nc] = dd; nc++; }
+  }
+  return nc;
+}
+
+static int col_box_box(orcData* d, const mjxModelDesc* m, int g1, int g2, double margin) {
+  const double *p1 = d->geom_xpos + 3 * g1, *R1 = d->geom_xmat + 9 * g1;
+  const double *p2 = d->geom_xpos + 3 * g2, *R2 = d->geom_xmat + 9 * g2;
+  const double *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
+  double t[3], c[3], b[3][3];
+  v3_sub(t, p2, p1);
+  m3_mulTv(c, R1, t);
+  for (int j = 0; j < 3; j++) {
+    double col[3] = {R2[j], R2[3 + j], R2[6 + j]};
+    m3_mulTv(b[j], R1, col);
+  }
+  double best = -1e30, n[3] = {0, 0, 1};
+  int kind = -1, ai = 0, aj = 0;
+  for (int k = 0; k < 15; k++) {
+    double L[3] = {0, 0, 0};
+    int i = 0, j = 0;
+    if (k < 3) { i = k; L[k] = 1; }
+    else if (k < 6) { j = k - 3; v3_copy(L, b[j]); }
+    else { i = (k - 6) / 3; j = (k - 6) % 3; double e[3] = {0, 0, 0}; e[i] = 1; v3_cross(L, e, b[j]); }
+    double ln = v3_norm(L);
+    if (ln < 1e-6) continue;
+    v3_scl(L, L, 1.0 / ln);
+    double r1 = s1[0] * fabs(L[0]) + s1[1] * fabs(L[1]) + s1[2] * fabs(L[2]);
+    double r2 = s2[0] * fabs(v3_dot(L, b[0])) + s2[1] * fabs(v3_dot(L, b[1])) + s2[2] * fabs(v3_dot(L, b[2]));
+    double dd = v3_dot(L, c);
+    double sep = fabs(dd) - r1 - r2;
+    if (sep > margin) return 0;
+    int kd = k < 3 ? 0 : (k < 6 ? 1 : 2);
+    if (kind < 0 || sep > best + (kd > kind ? 1e-5 : 0.0)) {
+      best = sep; kind = kd; ai = i; aj = j;
+      v3_scl(n, L, dd < 0 ? -1.0 : 1.0);
+    }
+  }
+  double pt[8][3], dep[8];
+  int nc = 0;
+  if (kind == 0) {
+    nc = box_face_clip(s1, ai, n[ai] < 0 ? -1.0 : 1.0, c, b, s2, margin, pt, dep);
+  } else if (kind == 1) {
+    double bt[3][3], c2[3];
+    for (int a = 0; a < 3; a++)
+      for (int x = 0; x < 3; x++) bt[a][x] = b[x][a];
+    for (int x = 0; x < 3; x++) c2[x] = -v3_dot(b[x], c);
+    double sg2 = v3_dot(n, b[aj]) > 0 ? -1.0 : 1.0;
+    nc = box_face_clip(s2, aj, sg2, c2, bt, s1, margin, pt, dep);
+    for (int q = 0; q < nc; q++) {
+      double w[3];
+      v3_copy(w, pt[q]);
+      for (int x = 0; x < 3; x++)
+        pt[q][x] = c[x] + b[0][x] * w[0] + b[1][x] * w[1] + b[2][x] * w[2] + n[x] * dep[q];
+    }
+  } else {
+    double p0[3] = {0, 0, 0}, q0[3], ea[3] = {0, 0, 0}, eb[3];
+    v3_copy(q0, c);
+    for (int a = 0; a < 3; a++) {
+      if (a != ai) p0[a] += n[a] > 0 ? s1[a] : -s1[a];
+      if (a != aj) {
+        double sgb = v3_dot(n, b[a]) > 0 ? -s2[a] : s2[a];
+        for (int x = 0; x < 3; x++) q0[x] += b[a][x] * sgb;
+      }
+    }
+    ea[ai] = s1[ai];
+    v3_scl(eb, b[aj], s2[aj]);
+    double a0[3], a1[3], b0[3], b1[3], pa[3], pb[3], df[3];
+    v3_sub(a0, p0, ea); v3_add(a1, p0, ea);
+    v3_sub(b0, q0, eb); v3_add(b1, q0, eb);
+    seg_seg(a0, a1, b0, b1, pa, pb);
+    v3_sub(df, pb, pa);
+    double dd = v3_dot(df, n);
+    if (dd <= margin) { v3_copy(pt[0], pb); dep[0] = dd; nc = 1; }
+  }
+  double nw[3];
+  m3_mulv(nw, R1, n);
+  for (int q = 0; q < nc; q++) {
+    double loc[3], pw[3];
+    for (int x = 0; x < 3; x++) loc[x] = pt[q][x] - n[x] * 0.5 * dep[q];
+    m3_mulv(pw, R1, loc);
+    v3_add(pw, pw, p1);
+    add_contact(d, g1, g2, dep[q], pw, nw);
+  }
+  return nc;
+}
+
 static void collision(const mjxModelDesc* m, orcData* d) {
   d->ncon = 0;
   for (int p = 0; p < m->npair; p++) {
@@ -723,6 +854,8 @@ static void collision(const mjxModelDesc* m, orcData* d) {
       } else {
         d->overflow |= 4;
       }
+    } else if (t1 == MJX_GEOM_BOX && t2 == MJX_GEOM_BOX) {
+      col_box_box(d, m, g1, g2, margin);
     } else if (t2 == MJX_GEOM_BOX && (t1 == MJX_GEOM_SPHERE || t1 == MJX_GEOM_CAPSULE)) {
       const double* R2 = d->geom_xmat + 9 * g2;
       if (t1 == MJX_GEOM_SPHERE) {

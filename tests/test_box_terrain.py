@@ -206,3 +206,46 @@ def test_sphere_centre_inside_a_box_leaves_through_the_nearest_face():
   assert c[2] == pytest.approx(-0.02 - 0.05)
   np.testing.assert_allclose(c[6:9], [-1.0, 0.0, 0.0], atol=1e-12)
   np.testing.assert_allclose(c[3:6], [0.98 - 0.015, 0.0, -0.3], atol=1e-12)
+
+
+def _quat_mul(a, b):
+  return np.array([a[0]*b[0]-a[1]*b[1]-a[2]*b[2]-a[3]*b[3], a[0]*b[1]+a[1]*b[0]+a[2]*b[3]-a[3]*b[2],
+                   a[0]*b[2]-a[1]*b[3]+a[2]*b[0]+a[3]*b[1], a[0]*b[3]+a[1]*b[2]-a[2]*b[1]+a[3]*b[0]])
+
+
+def test_box_resting_on_a_box_face():
+  m = _probe("box", "0.2 0.1 0.05")
+  q = np.zeros(7)
+  q[:3] = (0.3, -0.2, 0.05 - 0.004)  # 4 mm into the top face
+  q[3] = 1.0
+  f = ol.forward(m, q)
+  assert f["ncon"] == 4  # the bottom face's corners
+  c = f["contact"]
+  assert (c[:, 0] == 0).all() and (c[:, 1] == 1).all()  # static box is geom 1 (index order)
+  np.testing.assert_allclose(c[:, 2], -0.004, atol=1e-12)
+  np.testing.assert_allclose(c[:, 6:9], np.tile([0.0, 0.0, 1.0], (4, 1)), atol=1e-12)
+  np.testing.assert_allclose(np.sort(c[:, 3]), [0.1, 0.1, 0.5, 0.5], atol=1e-12)
+  np.testing.assert_allclose(c[:, 5], -0.002, atol=1e-12)  # halfway between the surfaces
+  # hanging half over the +x edge: the clip keeps the part over the face
+  q[0] = 1.0
+  f = ol.forward(m, q)
+  assert f["ncon"] == 4
+  np.testing.assert_allclose(np.sort(f["contact"][:, 3]), [0.8, 0.8, 1.0, 1.0], atol=1e-12)
+
+
+def test_box_edge_across_a_box_edge():
+  m = _probe("box", "0.2 0.05 0.05")
+  # long axis x tipped down toward +x by 0.3 rad, rolled 45 deg about it: its lowest edge
+  # (along x) passes beyond the static box's top edge at x = 1 (which runs along y)
+  qr = _quat_mul(_quat_y(0.3), np.array([np.cos(np.pi / 8), np.sin(np.pi / 8), 0.0, 0.0]))
+  q = np.zeros(7)
+  q[:3] = (1.0, 0.1, 0.05 * np.sqrt(2) - 0.01)
+  q[3:] = qr
+  f = ol.forward(m, q)
+  assert f["ncon"] == 1
+  c = f["contact"][0]
+  assert c[2] < 0.0
+  np.testing.assert_allclose(c[3:6], [1.0, 0.1, 0.0], atol=0.02)  # at the static edge
+  ex = np.array([np.cos(0.3), 0.0, -np.sin(0.3)])                 # moving edge direction
+  n = c[6:9]
+  assert abs(n[1]) < 1e-9 and abs(n @ ex) < 1e-9 and n[2] > 0.5   # normal to both edges

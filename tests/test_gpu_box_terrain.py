@@ -34,14 +34,23 @@ def _terrain_top(m, x, y):
   return float((p[inside, 2] + s[inside, 2]).max())
 
 
-def _states(m, n, seed, cols, spread, dz=(-0.03, 0.02)):
+def _states(m, n, seed, cols, spread, dz=(-0.03, 0.02), height=0.74, tilt=0.0, flip=False):
   rng = np.random.default_rng(seed)
   o = m.arrays["terrain_origins"]
   q = np.tile(m.key_qpos, (n, 1))
   for i in range(n):
     r, c = rng.integers(0, o.shape[0]), rng.choice(cols)
     q[i, :2] = o[r, c, :2] + rng.uniform(-spread, spread, 2)
-    q[i, 2] = _terrain_top(m, *q[i, :2]) + 0.74 + rng.uniform(*dz)
+    q[i, 2] = _terrain_top(m, *q[i, :2]) + height + rng.uniform(*dz)
+    if tilt > 0:  # random roll / pitch of the root
+      ax = rng.normal(size=3)
+      ax[2] = 0.0
+      ax /= np.linalg.norm(ax)
+      a = rng.uniform(-tilt, tilt)
+      qt = np.array([np.cos(a / 2), *(np.sin(a / 2) * ax)])
+      if flip:  # upside down (roll pi) before the tilt
+        qt = np.array([-qt[1], qt[0], qt[3], -qt[2]])
+      q[i, 3:7] = qt
   q[:, 7:] += rng.uniform(-0.1, 0.1, (n, m.nq - 7))
   qv = rng.normal(0, 0.3, (n, m.nv))
   qv[:, :3] *= 0.3
@@ -92,6 +101,37 @@ def test_rough_step_parity_across_stair_edges(gpu_device):
   assert sim.stats()["unsupported"] == 0
 
 
+def test_go1_trunk_on_stairs_parity(gpu_device):
+  """Go1 upside down on the stairs, trunk tilted: its trunk box meets the step boxes' faces
+  and edges (box-box narrowphase)."""
+  from mjlab_amd.scenes import load_scene
+  m = load_scene("go1_velocity_rough")
+  n = 48
+  sim = _sim(m, n, gpu_device)
+  q, qv, ctrl = _states(m, n, seed=21, cols=range(8, 20), spread=2.6, dz=(-0.02, 0.01),
+                        height=0.05, tilt=0.4, flip=True)
+  _load(sim, q, qv, ctrl)
+  sim.step()
+  torch.cuda.synchronize()
+  ref = oracle_step(m, q, qv, np.zeros_like(qv), ctrl, step=True, nconmax=64)
+  keep = [i for i, r in enumerate(ref) if r["nefc"] < 160]
+  assert len(keep) >= n - 8
+  trunk = m.names["geom"].index("robot/trunk_collision")
+  boxbox = sum(int(((r["contact"][:, 1] == trunk) | (r["contact"][:, 0] == trunk)).any()) for r in ref)
+  assert boxbox >= n // 4
+  d = sim.data
+  ncon, qacc = d.ncon.cpu().numpy(), d.qacc.cpu().numpy()
+  qpos, qvel = d.qpos.cpu().numpy(), d.qvel.cpu().numpy()
+  for i in keep:
+    r = ref[i]
+    assert ncon[i] == r["ncon"], f"world {i}: ncon {ncon[i]} vs {r['ncon']}"
+    sc = max(1.0, np.abs(r["qacc"]).max())
+    np.testing.assert_allclose(qacc[i], r["qacc"], atol=5e-3 * sc, err_msg=f"qacc world {i}")
+    np.testing.assert_allclose(qvel[i], r["qvel"], atol=5e-3 * sc * m.timestep + 1e-5)
+    np.testing.assert_allclose(qpos[i], r["qpos"], atol=5e-3 * sc * m.timestep ** 2 + 1e-5)
+  assert sim.stats()["unsupported"] == 0
+
+
 def test_flat_box_patches_match_the_plane_on_gpu(gpu_device):
   from mjlab_amd.scenes import load_scene
   mr, mp = load_scene("g1_velocity_rough"), load_scene("g1_velocity")
@@ -133,17 +173,19 @@ def test_rough_cull_far_above(gpu_device):
   np.testing.assert_allclose(gx[:, st], np.broadcast_to(m.geom_pos[st], gx[:, st].shape), atol=1e-5)
 
 
-def test_rough_task_graph_step_and_terrain_levels(gpu_device):
+@pytest.mark.parametrize("task,z0", [("Mjlab-Velocity-Rough-Unitree-G1", 0.76),
+                                     ("Mjlab-Velocity-Rough-Unitree-Go1", 0.278)])
+def test_rough_task_graph_step_and_terrain_levels(task, z0, gpu_device):
   from mjlab_amd.envs import make_env
   n = 256
-  env = make_env("Mjlab-Velocity-Rough-Unitree-G1", num_envs=n, device=gpu_device, seed=3)
+  env = make_env(task, num_envs=n, device=gpu_device, seed=3)
   env.reset()
   terrain = env.scene.terrain
   # initial levels 0..5 (max_init_terrain_level); the reset's own curriculum pass moves
   # every env one level up (the default pose sits far from its origin), as the reference
   assert terrain is not None and int(terrain.terrain_levels.max()) <= 6
   z = env.scene["robot"].data.root_link_pos_w[:, 2] - env.scene.env_origins[:, 2]
-  assert (z - 0.76).abs().max() < 0.05  # spawned on the sub-terrain origins
+  assert (z - z0).abs().max() < 0.05  # spawned on the sub-terrain origins
   env.enable_graph(capture=True)
   assert env._fused is not None, getattr(env, "_fused_unsupported", "")
   g = torch.Generator(device=gpu_device).manual_seed(0)
