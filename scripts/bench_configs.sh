@@ -13,3 +13,6 @@ run Mjlab-Velocity-Flat-Unitree-Go1 8192 200 --no-cpu-baseline
 run Mjlab-Tracking-Flat-Unitree-G1 4096 100 --no-cpu-baseline
 run Mjlab-Jump-Flat-Unitree-G1 16384 60 --no-cpu-baseline
 run Mjlab-Jump-Hfield-Unitree-G1 16384 60 --no-cpu-baseline
+# SURVEY 8f row f3 (not BASELINE configs): the rough box-stair tasks
+run Mjlab-Velocity-Rough-Unitree-G1 4096 200 --no-cpu-baseline
+run Mjlab-Velocity-Rough-Unitree-Go1 8192 200 --no-cpu-baseline
