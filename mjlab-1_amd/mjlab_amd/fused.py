@@ -578,9 +578,14 @@ class FusedVelocityStep:
     env, L, sim = self.env, self._L, self.env.sim
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
     self._ok(L.mjx_task_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
-    for _ in range(env.cfg.decimation):
-      sim.step()  # the engine updates the feet air times (mjx_sim_track_air_time)
-      if not self._engine_air:
+    if self._engine_air:
+      # the engine updates the feet air times every substep (mjx_sim_track_air_time) and
+      # nothing reads mjData between substeps: one mjx_step of `decimation` substeps, whose
+      # full mjData outputs (frames, contacts, forces) are written after the last only
+      sim.step(nsubstep=env.cfg.decimation)
+    else:
+      for _ in range(env.cfg.decimation):
+        sim.step()
         self._ok(L.mjx_task_substep(self._task, stream))
     self._ok(L.mjx_task_post(self._task, stream))
     # per-env curriculum terms (terrain levels) of the resetting envs, before the reset

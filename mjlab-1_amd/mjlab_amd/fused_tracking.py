@@ -414,8 +414,7 @@ class FusedTrackingStep:
     env, L, sim = self.env, self._L, self.env.sim
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
     self._ok(L.mjx_track_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
-    for _ in range(env.cfg.decimation):
-      sim.step()
+    sim.step(nsubstep=env.cfg.decimation)  # mjData outputs written after the last substep
     self._ok(L.mjx_track_post(self._task, stream))
     mask = ctypes.c_void_p(self.reset_buf.data_ptr())
     check(lib().mjx_reset(sim._sim, mask, stream))
