@@ -284,21 +284,22 @@ __device__ __forceinline__ void post_env(const mjxTrackDesc& t, int e, int lane,
   if (reset && lane < MJX_TRACK_NMETRIC) atomicAdd(&acc->metric[lane], t.metrics[(size_t)lane * t.nworld + e]);
 }
 
+// Accumulators: block LDS copy stored as the block's row of `part` (k_log sums the rows;
+// per-field global atomics from every block contend on a few addresses)
+constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
+static_assert(kAccN <= 128, "k_log: thread per accumulator field");
 __global__ __launch_bounds__(64 * kPostEnvs) void k_post(const mjxTrackDesc* __restrict__ T,
-                                                        Acc* __restrict__ acc) {
+                                                        float* __restrict__ part) {
   const mjxTrackDesc& t = *T;
   __shared__ Acc sh;
   float* shf = reinterpret_cast<float*>(&sh);
-  constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
   for (int i = threadIdx.x; i < kAccN; i += blockDim.x) shf[i] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
   if (e < t.nworld) post_env(t, e, lane, &sh);
   __syncthreads();
-  float* gf = reinterpret_cast<float*>(acc);
-  for (int i = threadIdx.x; i < kAccN; i += blockDim.x)
-    if (shf[i] != 0.f) atomicAdd(gf + i, shf[i]);
+  for (int i = threadIdx.x; i < kAccN; i += blockDim.x) part[(size_t)blockIdx.x * kAccN + i] = shf[i];
 }
 
 // Failure-bin statistics of one resample (commands.py:258-300), one workgroup: failed
@@ -609,16 +610,42 @@ __global__ void k_obs(const mjxTrackDesc* __restrict__ T) {
 }
 
 // episode logs of the step's resets (k_post's accumulators), then cleared
-__global__ void k_log(const mjxTrackDesc* __restrict__ T, Acc* __restrict__ acc) {
+constexpr int kLogChunks = 8;
+__global__ __launch_bounds__(128 * kLogChunks) void k_log(const mjxTrackDesc* __restrict__ T,
+                                                          const float* __restrict__ part, int nblock) {
   const mjxTrackDesc& t = *T;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (acc->count > 0.f) {
-    for (int k = 0; k < t.nreward; k++) t.log_reward[k] = acc->reward[k] / acc->count / t.episode_length_s;
-    for (int k = 0; k < t.ntermination; k++) t.log_termination[k] = acc->term[k];
-    for (int k = 0; k < MJX_TRACK_NMETRIC; k++) t.log_metric[k] = acc->metric[k] / acc->count;
+  __shared__ Acc sh;
+  __shared__ float red[kLogChunks][128];
+  // column sums of k_post's block rows: 8 row chunks x 128 field lanes, then an LDS fold
+  const int i = threadIdx.x & 127, c = threadIdx.x >> 7;
+  float sum = 0.f;
+  if (i < kAccN) {
+    const int per = (nblock + kLogChunks - 1) / kLogChunks;
+    const int b0 = c * per, b1 = min(nblock, b0 + per);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = b0;
+    for (; b + 7 < b1; b += 8)
+#pragma unroll
+      for (int u = 0; u < 8; u++) s[u] += part[(size_t)(b + u) * kAccN + i];
+    for (; b < b1; b++) s[0] += part[(size_t)b * kAccN + i];
+    sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   }
-  float* f = reinterpret_cast<float*>(acc);
-  for (int i = 0; i < (int)(sizeof(Acc) / sizeof(float)); i++) f[i] = 0.f;
+  red[c][i] = sum;
+  __syncthreads();
+  if (c == 0 && i < kAccN) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLogChunks; k++) tot += red[k][i];
+    reinterpret_cast<float*>(&sh)[i] = tot;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const Acc& acc = sh;
+  if (acc.count > 0.f) {
+    for (int k = 0; k < t.nreward; k++) t.log_reward[k] = acc.reward[k] / acc.count / t.episode_length_s;
+    for (int k = 0; k < t.ntermination; k++) t.log_termination[k] = acc.term[k];
+    for (int k = 0; k < MJX_TRACK_NMETRIC; k++) t.log_metric[k] = acc.metric[k] / acc.count;
+  }
 }
 
 }  // namespace mjtr
@@ -627,7 +654,7 @@ __global__ void k_log(const mjxTrackDesc* __restrict__ T, Acc* __restrict__ acc)
 struct mjxTrack_ {
   mjxTrackDesc host;
   mjxTrackDesc* dev = nullptr;
-  mjtr::Acc* acc = nullptr;
+  float* part = nullptr;  // [nblock][kAccN] k_post block partials
   int nworld = 0;
 };
 
@@ -660,12 +687,12 @@ int mjx_track_create(const mjxTrackDesc* d, mjxTrack** out) {
   t->host = *d;
   t->nworld = d->nworld;
   if (hipMalloc((void**)&t->dev, sizeof(mjxTrackDesc)) != hipSuccess ||
-      hipMalloc((void**)&t->acc, sizeof(mjtr::Acc)) != hipSuccess) {
+      hipMalloc((void**)&t->part, sizeof(float) * mjtr::kAccN *
+                ((t->nworld + mjtr::kPostEnvs - 1) / mjtr::kPostEnvs + 1)) != hipSuccess) {
     delete t;
     return track_fail("hipMalloc failed");
   }
-  if (hipMemcpy(t->dev, d, sizeof(mjxTrackDesc), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(t->acc, 0, sizeof(mjtr::Acc)) != hipSuccess) {
+  if (hipMemcpy(t->dev, d, sizeof(mjxTrackDesc), hipMemcpyHostToDevice) != hipSuccess) {
     delete t;
     return track_fail("upload failed");
   }
@@ -676,7 +703,7 @@ int mjx_track_create(const mjxTrackDesc* d, mjxTrack** out) {
 int mjx_track_destroy(mjxTrack* t) {
   if (!t) return 0;
   if (t->dev) (void)hipFree(t->dev);
-  if (t->acc) (void)hipFree(t->acc);
+  if (t->part) (void)hipFree(t->part);
   delete t;
   return 0;
 }
@@ -692,8 +719,9 @@ int mjx_track_action(mjxTrack* t, const float* action, void* stream) {
 int mjx_track_post(mjxTrack* t, void* stream) {
   if (!t) return track_fail("null task");
   hipLaunchKernelGGL(mjtr::k_post, dim3((t->nworld + mjtr::kPostEnvs - 1) / mjtr::kPostEnvs),
-                     dim3(64 * mjtr::kPostEnvs), 0, (hipStream_t)stream, t->dev, t->acc);
-  hipLaunchKernelGGL(mjtr::k_log, dim3(1), dim3(64), 0, (hipStream_t)stream, t->dev, t->acc);
+                     dim3(64 * mjtr::kPostEnvs), 0, (hipStream_t)stream, t->dev, t->part);
+  hipLaunchKernelGGL(mjtr::k_log, dim3(1), dim3(128 * mjtr::kLogChunks), 0, (hipStream_t)stream, t->dev, t->part,
+                     (t->nworld + mjtr::kPostEnvs - 1) / mjtr::kPostEnvs);
   return track_launched("k_post");
 }
 

@@ -226,15 +226,60 @@ __device__ __forceinline__ JointSums joint_sums(const mjxTaskDesc& t, int e, int
   return r;
 }
 
+// Per-foot values of one env, staged lane-parallel (lane s = foot s) before the term switch:
+// the terms' lanes diverge, so every global load inside a case runs in that case's own
+// serial turn -- loaded up front they overlap, and the cases read LDS.
+struct FootVals { float found, z, vx, vy, air, cc, peak, fx, fy, fz; };
+struct EnvVals {
+  FootVals f[MJX_TASK_MAX_FEET];
+  float og_x, og_y, ocv0, ocv1;  // orient body: projected gravity xy, angular velocity xy
+  int illegal;                   // any illegal-contact slot found
+};
+__device__ __forceinline__ void stage_env(const mjxTaskDesc& t, const int e, const Root& r,
+                                          const float* sd, const int lane, EnvVals* ev) {
+  if (lane < t.nfeet) {
+    const int s = lane;
+    const size_t i = (size_t)e * t.nfeet + s;
+    FootVals f;
+    f.found = sd[t.feet_found_adr[s]];
+    const float* fv = sd + t.feet_force_adr[s];
+    f.fx = fv[0]; f.fy = fv[1]; f.fz = fv[2];
+    f.z = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
+    const V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
+    f.vx = v.x; f.vy = v.y;
+    f.air = t.cur_air[i]; f.cc = t.cur_contact[i]; f.peak = t.peak_heights[i];
+    ev->f[s] = f;
+  }
+  const bool ill = lane < t.nillegal && sd[t.illegal_found_adr[lane]] > 0.f;
+  const unsigned long long ib = __ballot(ill);
+  if (lane == 0) {
+    ev->illegal = ib != 0ull;
+    V3 g = r.grav_b;
+    float c0 = 0.f, c1 = 0.f;
+    if (t.orient_body >= 0) {
+      g = qapply_inv(t.xquat + ((size_t)e * t.nbody + t.orient_body) * 4, V3{0.f, 0.f, -1.f});
+      const float* cv = t.cvel + ((size_t)e * t.nbody + t.orient_body) * 6;
+      c0 = cv[0]; c1 = cv[1];
+    }
+    ev->og_x = g.x; ev->og_y = g.y; ev->ocv0 = c0; ev->ocv1 = c1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Called by every lane of the env's wave: lane k evaluates termination k and reward term k
 // (terms are independent; their loads overlap instead of queueing behind each other's
 // stores), the wave reduces the flags and the reward total.
 __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, const JointSums& js,
-                                         const int lane, Acc* __restrict__ acc) {
+                                         const int lane, Acc* __restrict__ acc,
+                                         EnvVals* __restrict__ ev) {
   const int64_t len = t.episode_length[e] + 1;
   const Root r = root_state(t, e);
   const float* sd = t.sensordata + (size_t)e * t.nsensordata;
   if (lane == 0) t.episode_length[e] = len;
+  stage_env(t, e, r, sd, lane, ev);
+  const FootVals* F = ev->f;
   // ---- terminations (termination_manager.py:87-97)
   bool tm_v = false;
   {
@@ -243,18 +288,14 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
     switch (k < t.ntermination ? t.termination_kind[k] : -1) {
       case MJX_TM_TIME_OUT: v = len >= t.max_episode_length; break;
       case MJX_TM_BAD_ORIENT: v = fabsf(acosf(-r.grav_b.z)) > t.termination_p0[k]; break;  // NaN -> false, as torch
-      case MJX_TM_ILLEGAL_CONTACT:
-        for (int s = 0; s < t.nillegal; s++) v |= sd[t.illegal_found_adr[s]] > 0.f;
-        break;
+      case MJX_TM_ILLEGAL_CONTACT: v = ev->illegal; break;
       case MJX_TM_ROOT_HEIGHT:  // envs/mdp/terminations.py root_height_below_minimum
         v = t.xpos[((size_t)e * t.nbody + t.root_body) * 3 + 2] < t.termination_p0[k];
         break;
       case MJX_TM_EXCESSIVE_FORCE: {  // tasks/jump/mdp/terminations.py:15-45
         float fmax = 0.f;
-        for (int s = 0; s < t.nfeet; s++) {
-          const float* fv = sd + t.feet_force_adr[s];
-          fmax = fmaxf(fmax, sqrtf(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]));
-        }
+        for (int s = 0; s < t.nfeet; s++)
+          fmax = fmaxf(fmax, sqrtf(F[s].fx * F[s].fx + F[s].fy * F[s].fy + F[s].fz * F[s].fz));
         v = fmax > t.termination_p0[k];
       } break;
     }
@@ -296,21 +337,17 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         float dz = cmd[2] - r.ang_b.z;
         f = expf(-(dz * dz + r.ang_b.x * r.ang_b.x + r.ang_b.y * r.ang_b.y) / (p0 * p0));
       } break;
-      case MJX_RW_FLAT_ORIENT: {  // rewards.py:63-85
-        V3 g = r.grav_b;
-        if (t.orient_body >= 0)
-          g = qapply_inv(t.xquat + ((size_t)e * t.nbody + t.orient_body) * 4, V3{0.f, 0.f, -1.f});
-        f = expf(-(g.x * g.x + g.y * g.y) / (p0 * p0));
-      } break;
+      case MJX_RW_FLAT_ORIENT:  // rewards.py:63-85
+        f = expf(-(ev->og_x * ev->og_x + ev->og_y * ev->og_y) / (p0 * p0));
+        break;
       case MJX_RW_POSE: {  // rewards.py:291-359 (p0 walking, p1 running threshold)
         const float speed = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) + fabsf(cmd[2]);
         const float s = js.pose[speed < p0 ? 0 : (speed < p1 ? 1 : 2)];
         f = expf(-s / (float)nj);
       } break;
-      case MJX_RW_BODY_ANG_VEL: {  // rewards.py:98-107
-        const float* cv = t.cvel + ((size_t)e * t.nbody + t.orient_body) * 6;
-        f = cv[0] * cv[0] + cv[1] * cv[1];
-      } break;
+      case MJX_RW_BODY_ANG_VEL:  // rewards.py:98-107
+        f = ev->ocv0 * ev->ocv0 + ev->ocv1 * ev->ocv1;
+        break;
       case MJX_RW_ANGMOM: {  // rewards.py:110-120
         const float* h = sd + t.angmom_adr;
         f = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
@@ -322,7 +359,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       case MJX_RW_FEET_AIR_TIME: {  // rewards.py:123-152 (p0 min, p1 max, p2 cmd thr)
         float in_air_t = 0.f, in_air_n = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
-          float at = t.cur_air[(size_t)e * t.nfeet + s];
+          const float at = F[s].air;
           f += (at > p0 && at < p1) ? 1.f : 0.f;
           if (at > 0.f) { in_air_t += at; in_air_n += 1.f; }
         }
@@ -331,21 +368,17 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         f *= command_gate(t, cmd, p2, 0.f);
       } break;
       case MJX_RW_FEET_CLEARANCE: {  // rewards.py:155-177 (p0 target, p1 cmd thr)
-        for (int s = 0; s < t.nfeet; s++) {
-          float z = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
-          V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
-          f += fabsf(z - p0) * sqrtf(v.x * v.x + v.y * v.y);
-        }
+        for (int s = 0; s < t.nfeet; s++)
+          f += fabsf(F[s].z - p0) * sqrtf(F[s].vx * F[s].vx + F[s].vy * F[s].vy);
         f *= command_gate(t, cmd, p1, 0.f);
       } break;
       case MJX_RW_FEET_SWING: {  // rewards.py:180-229 (p0 target, p1 cmd thr)
         float land_n = 0.f, land_h = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
           const size_t i = (size_t)e * t.nfeet + s;
-          float z = t.site_xpos[((size_t)e * t.nsite + t.foot_site[s]) * 3 + 2];
-          float peak = t.peak_heights[i];
-          if (sd[t.feet_found_adr[s]] == 0.f) peak = fmaxf(peak, z);
-          const float cc = t.cur_contact[i];
+          float peak = F[s].peak;
+          if (F[s].found == 0.f) peak = fmaxf(peak, F[s].z);
+          const float cc = F[s].cc;
           const bool first = cc > 0.f && cc < dt + 1e-8f;
           if (first) {
             float err = peak / p0 - 1.f;
@@ -363,9 +396,8 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       case MJX_RW_FEET_SLIP: {  // rewards.py:232-259 (p0 cmd thr)
         float vs = 0.f, n = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
-          if (!(sd[t.feet_found_adr[s]] > 0.f)) continue;
-          V3 v = site_lin_vel(t, e, t.foot_site[s], t.foot_site_body[s]);
-          float v2 = v.x * v.x + v.y * v.y;
+          if (!(F[s].found > 0.f)) continue;
+          const float v2 = F[s].vx * F[s].vx + F[s].vy * F[s].vy;
           f += v2;
           vs += sqrtf(v2);
           n += 1.f;
@@ -377,10 +409,9 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       case MJX_RW_SOFT_LANDING: {  // rewards.py:262-288 (p0 cmd thr)
         float n = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
-          const float cc = t.cur_contact[(size_t)e * t.nfeet + s];
+          const float cc = F[s].cc;
           if (!(cc > 0.f && cc < dt + 1e-8f)) continue;
-          const float* fv = sd + t.feet_force_adr[s];
-          f += sqrtf(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]);
+          f += sqrtf(F[s].fx * F[s].fx + F[s].fy * F[s].fy + F[s].fz * F[s].fz);
           n += 1.f;
         }
         atomicAdd(&acc->metric_sum[MJX_MT_LANDING], f);
@@ -405,18 +436,18 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       } break;
       case MJX_RW_EXPLOSIVE_TAKEOFF: {  // :73-108, p0 power threshold
         bool in_contact = false;
-        for (int s = 0; s < t.nfeet; s++) in_contact |= sd[t.feet_found_adr[s]] > 0.f;
+        for (int s = 0; s < t.nfeet; s++) in_contact |= F[s].found > 0.f;
         f = in_contact ? fmaxf(js.power - p0, 0.f) / 1000.f : 0.f;
       } break;
       case MJX_RW_SYNC_EXTENSION: f = js.jv_var; break;  // :111-139
       case MJX_RW_VERTICAL_IMPULSE:  // :142-167
-        for (int s = 0; s < t.nfeet; s++) f += fmaxf(sd[t.feet_force_adr[s] + 2], 0.f);
+        for (int s = 0; s < t.nfeet; s++) f += fmaxf(F[s].fz, 0.f);
         f /= 500.f;
         break;
       case MJX_RW_AIR_TIME_BONUS: {  // :170-204, p0 min air time
         float amin = 1e30f, in_air_t = 0.f, in_air_n = 0.f;
         for (int s = 0; s < t.nfeet; s++) {
-          const float at = t.cur_air[(size_t)e * t.nfeet + s];
+          const float at = F[s].air;
           amin = fminf(amin, at);
           if (at > 0.f) { in_air_t += at; in_air_n += 1.f; }
         }
@@ -426,7 +457,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       } break;
       case MJX_RW_LANDING_BALANCE: {  // :207-270, p0 stability time; stateful, never reset
         bool in_contact = false;
-        for (int s = 0; s < t.nfeet; s++) in_contact |= sd[t.feet_found_adr[s]] > 0.f;
+        for (int s = 0; s < t.nfeet; s++) in_contact |= F[s].found > 0.f;
         const bool just_landed = t.was_in_air[e] && in_contact;
         t.was_in_air[e] = !in_contact;
         const bool upright = fabsf(r.grav_b.z + 1.f) < 0.2f;
@@ -442,7 +473,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       case MJX_RW_SYMMETRIC_LANDING: {  // :273-316: both feet in first contact
         bool both = t.nfeet >= 2;
         for (int s = 0; s < 2 && s < t.nfeet; s++) {
-          const float cc = t.cur_contact[(size_t)e * t.nfeet + s];
+          const float cc = F[s].cc;
           both = both && cc > 0.f && cc < dt + 1e-8f;
         }
         f = both ? 1.f : 0.f;
@@ -493,27 +524,56 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
 }
 
 // Wave per env (kPostEnvs envs per block): the joint sums run lane-parallel, the rest of
-// the env's terms on lane 0.  Accumulators: block LDS copy, one global atomic per field
-// and block.
+// the env's terms on lane 0.  Accumulators: block LDS copy, stored as the block's row of
+// `part` (plain stores; k_accum sums the rows).  A global atomic per field and block put
+// hundreds of blocks on the same few addresses: ~13 us of the kernel's 42 (G1, 4096 envs).
 constexpr int kPostEnvs = 16;
+constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
+static_assert(kAccN <= 128, "k_accum: thread per accumulator field");
 __global__ __launch_bounds__(64 * kPostEnvs) void k_post(const mjxTaskDesc* __restrict__ T,
-                                                        Acc* __restrict__ acc) {
+                                                        float* __restrict__ part) {
   const mjxTaskDesc& t = *T;
   __shared__ Acc sh;
   float* shf = reinterpret_cast<float*>(&sh);
-  constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
   for (int i = threadIdx.x; i < kAccN; i += blockDim.x) shf[i] = 0.f;
   __syncthreads();
+  __shared__ EnvVals ev[kPostEnvs];
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
   if (e < t.nworld) {
     const JointSums js = joint_sums(t, e, lane);
-    post_env(t, e, js, lane, &sh);
+    post_env(t, e, js, lane, &sh, &ev[threadIdx.x >> 6]);
   }
   __syncthreads();
-  float* gf = reinterpret_cast<float*>(acc);
-  for (int i = threadIdx.x; i < kAccN; i += blockDim.x)
-    if (shf[i] != 0.f) atomicAdd(gf + i, shf[i]);
+  for (int i = threadIdx.x; i < kAccN; i += blockDim.x) part[(size_t)blockIdx.x * kAccN + i] = shf[i];
+}
+// acc += the column sums of k_post's block rows: 8 row chunks x 128 field lanes, each
+// summing its chunk with 8 independent loads in flight, then an LDS fold of the chunks
+constexpr int kAccChunks = 8;
+__global__ __launch_bounds__(128 * kAccChunks) void k_accum(const float* __restrict__ part, int nblock,
+                                                            Acc* __restrict__ acc) {
+  __shared__ float red[kAccChunks][128];
+  const int i = threadIdx.x & 127, c = threadIdx.x >> 7;
+  float sum = 0.f;
+  if (i < kAccN) {
+    const int per = (nblock + kAccChunks - 1) / kAccChunks;
+    const int b0 = c * per, b1 = min(nblock, b0 + per);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = b0;
+    for (; b + 7 < b1; b += 8)
+#pragma unroll
+      for (int u = 0; u < 8; u++) s[u] += part[(size_t)(b + u) * kAccN + i];
+    for (; b < b1; b++) s[0] += part[(size_t)b * kAccN + i];
+    sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  }
+  red[c][i] = sum;
+  __syncthreads();
+  if (c == 0 && i < kAccN) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kAccChunks; k++) tot += red[k][i];
+    reinterpret_cast<float*>(acc)[i] += tot;
+  }
 }
 
 __device__ __forceinline__ void resample_command(const mjxTaskDesc& t, int e, uint64_t step,
@@ -790,6 +850,7 @@ struct mjxTask_ {
   mjxTaskDesc host;
   mjxTaskDesc* dev = nullptr;
   mjxt::Acc* acc = nullptr;
+  float* part = nullptr;  // [nblock][kAccN] k_post block partials
   int nworld = 0;
 };
 
@@ -812,8 +873,10 @@ int mjx_task_create(const mjxTaskDesc* desc, mjxTask** out) {
   auto* t = new mjxTask_();
   t->host = *desc;
   t->nworld = desc->nworld;
+  const size_t nblock = ((size_t)t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs;
   if (hipMalloc((void**)&t->dev, sizeof(mjxTaskDesc)) != hipSuccess ||
-      hipMalloc((void**)&t->acc, sizeof(mjxt::Acc)) != hipSuccess) {
+      hipMalloc((void**)&t->acc, sizeof(mjxt::Acc)) != hipSuccess ||
+      hipMalloc((void**)&t->part, sizeof(float) * mjxt::kAccN * (nblock > 0 ? nblock : 1)) != hipSuccess) {
     delete t;
     return task_fail("hipMalloc failed");
   }
@@ -830,6 +893,7 @@ int mjx_task_destroy(mjxTask* t) {
   if (!t) return 0;
   if (t->dev) (void)hipFree(t->dev);
   if (t->acc) (void)hipFree(t->acc);
+  if (t->part) (void)hipFree(t->part);
   delete t;
   return 0;
 }
@@ -855,8 +919,11 @@ int mjx_task_action(mjxTask* t, const float* action, void* stream) {
 int mjx_task_substep(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_substep, t->dev); }
 int mjx_task_post(mjxTask* t, void* stream) {
   if (!t) return task_fail("null task");
-  hipLaunchKernelGGL(mjxt::k_post, dim3((t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs),
-                     dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream, t->dev, t->acc);
+  const int nblock = (t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs;
+  hipLaunchKernelGGL(mjxt::k_post, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
+                     t->dev, t->part);
+  hipLaunchKernelGGL(mjxt::k_accum, dim3(1), dim3(128 * mjxt::kAccChunks), 0, (hipStream_t)stream,
+                     t->part, nblock, t->acc);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : task_fail(std::string("k_post: ") + hipGetErrorString(e));
 }
