@@ -236,6 +236,11 @@ class ManagerBasedRlEnv:
   def enable_graph(self, capture: bool = True, fused: bool = True) -> None:
     """Switch to the sync-free step; with capture=True record it into a HIP graph
     (replayed per step; re-recorded when a curriculum changes command ranges)."""
+    if self.sim.nan_guard.enabled:
+      import warnings
+      warnings.warn("NanGuard is enabled: the env step stays eager (the guard reads a NaN "
+                    "flag back to the host after every physics step)")
+      return
     self.sync_free = True
     self._use_graph = capture
     self._fused = None

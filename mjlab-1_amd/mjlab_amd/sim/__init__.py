@@ -1,5 +1,6 @@
-from .sim import MujocoCfg, NanGuardCfg, Simulation, SimulationCfg, world_capacity
+from .sim import (MujocoCfg, NanGuard, NanGuardCfg, Simulation, SimulationCfg, load_nan_dump,
+                  world_capacity)
 from .sim_data import DeviceBridge, WarpBridge
 
-__all__ = ["MujocoCfg", "NanGuardCfg", "Simulation", "SimulationCfg", "DeviceBridge",
+__all__ = ["MujocoCfg", "NanGuard", "NanGuardCfg", "load_nan_dump", "Simulation", "SimulationCfg", "DeviceBridge",
            "WarpBridge", "world_capacity"]

@@ -61,7 +61,7 @@ class MujocoCfg:
 
 @dataclass
 class NanGuardCfg:
-  """`utils/nan_guard.py` config; the dump tool is out of scope, `watch()` is a no-op."""
+  """`utils/nan_guard.py:16-23`."""
   enabled: bool = False
   buffer_size: int = 100
   output_dir: str = "/tmp/mjlab/nan_dumps"
@@ -69,12 +69,102 @@ class NanGuardCfg:
 
 
 class NanGuard:
+  """`utils/nan_guard.py:26-181`: when enabled, a rolling buffer of the last `buffer_size`
+  pre-step (qpos, qvel) states; after a step with NaN/Inf in qpos, qvel, qacc or
+  qacc_warmstart of any world, the buffered states of the first `max_envs_to_dump` such worlds
+  are written once to `nan_dump_<time>.npz` (keys `states_step_<n>`: [envs, nq + nv] rows,
+  MuJoCo's mjSTATE_PHYSICS layout for a model without actuator activations or history) with
+  the compiled model beside it and `*_latest` symlinks.  Differences, stated: the model is
+  saved as this build's compiled-scene npz (`model_<time>.npz`, `scenes.load_model`), not a
+  MuJoCo .mjb; `_metadata` is a JSON string (loadable without pickle), same fields.  A
+  no-op when disabled; enabled, every step reads a flag back to the host (as the reference)."""
+
   def __init__(self, cfg: NanGuardCfg, num_envs: int, model) -> None:
     self.cfg = cfg
+    self.enabled = cfg.enabled
+    self.num_envs = num_envs
+    if not self.enabled:
+      return
+    from collections import deque
+    self.buffer: deque = deque(maxlen=cfg.buffer_size)
+    self.output_dir = cfg.output_dir
+    self.max_envs_to_dump = cfg.max_envs_to_dump
+    self.step_counter = 0
+    self._dumped = False
+    self.model = model
+    self.state_size = int(model.nq + model.nv)
+    self.last_dump: str | None = None
+
+  def capture(self, data) -> None:
+    if not self.enabled:
+      return
+    self.buffer.append({"step": self.step_counter, "qpos": data.qpos.clone(), "qvel": data.qvel.clone()})
+    self.step_counter += 1
 
   @contextlib.contextmanager
   def watch(self, data):
+    self.capture(data)
     yield
+    self.check_and_dump(data)
+
+  @staticmethod
+  def detect_nans(data) -> torch.Tensor:
+    mask = torch.zeros(data.qpos.shape[0], dtype=torch.bool, device=data.qpos.device)
+    for t in (data.qpos, data.qvel, data.qacc, data.qacc_warmstart):
+      mask |= torch.isnan(t).any(dim=-1) | torch.isinf(t).any(dim=-1)
+    return mask
+
+  def check_and_dump(self, data) -> bool:
+    if not self.enabled or self._dumped:
+      return False
+    mask = self.detect_nans(data)
+    if bool(mask.any()):
+      self._dump_buffer(torch.where(mask)[0].cpu().numpy().tolist())
+      self._dumped = True
+      return True
+    return False
+
+  def _dump_buffer(self, nan_env_ids: list[int]) -> None:
+    import datetime
+    import json
+    import os
+    from ..scenes import save_model
+    os.makedirs(self.output_dir, exist_ok=True)
+    stamp = datetime.datetime.now().strftime("%Y%m%d_%H%M%S")
+    dump = os.path.join(self.output_dir, f"nan_dump_{stamp}.npz")
+    model_file = os.path.join(self.output_dir, f"model_{stamp}.npz")
+    envs = nan_env_ids[: self.max_envs_to_dump]
+    out = {}
+    for item in self.buffer:
+      q, v = item["qpos"][envs].double().cpu().numpy(), item["qvel"][envs].double().cpu().numpy()
+      out[f"states_step_{item['step']:06d}"] = np.concatenate([q, v], axis=1)
+    meta = {"num_envs_total": self.num_envs, "num_envs_dumped": len(envs), "nan_env_ids": nan_env_ids,
+            "dumped_env_ids": list(envs), "state_size": self.state_size, "buffer_size": len(self.buffer),
+            "detection_step": self.step_counter, "timestamp": stamp,
+            "model_file": os.path.basename(model_file),
+            "note": "Rows are [qpos, qvel] (mjSTATE_PHYSICS without act / history). Model saved "
+                    "as the compiled-scene npz (mjlab_amd.scenes.load_model)."}
+    out["_metadata"] = np.array(json.dumps(meta))
+    np.savez_compressed(dump, **out)
+    save_model(self.model, model_file)
+    for name, target in (("nan_dump_latest.npz", dump), ("model_latest.npz", model_file)):
+      link = os.path.join(self.output_dir, name)
+      if os.path.lexists(link):
+        os.remove(link)
+      os.symlink(os.path.basename(target), link)
+    self.last_dump = dump
+    print(f"[NanGuard] Detected NaN/Inf at step {self.step_counter}")
+    print(f"[NanGuard] NaN/Inf found in envs: {nan_env_ids[:10]}...")
+    print(f"[NanGuard] Dumped {len(self.buffer)} states of envs {envs} to: {dump}")
+
+
+def load_nan_dump(path: str) -> tuple[dict, dict]:
+  """Read a NanGuard dump without unpickling: ({key: states}, metadata)."""
+  import json
+  with np.load(path, allow_pickle=False) as z:
+    states = {k: z[k] for k in z.files if k != "_metadata"}
+    meta = json.loads(str(z["_metadata"]))
+  return states, meta
 
 
 @dataclass(kw_only=True)
