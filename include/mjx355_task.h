@@ -161,6 +161,19 @@ int mjx_task_observe(mjxTask* task, void* stream);
 size_t mjx_task_desc_size(void);  /* sizeof(mjxTaskDesc): ABI check for FFI bindings */
 const char* mjx_task_last_error(void);
 
+/* Terrain-level curriculum of the rough velocity tasks over a reset mask, replacing
+ * tasks/velocity/mdp/curriculums.py:30-64 (terrain_levels_vel) + terrains/terrain_importer.py:
+ * 186-201 (update_env_origins) for the resetting envs: root xy (xpos[world, root_body]) vs
+ * env origin, commanded xy speed x episode length; levels [nworld] int64 updated, env_origins
+ * [nworld, 3] set from terrain_origins [nrows, ncols, 3] at (level, type); a level past the
+ * top draws uniformly (counter-based hash of seed, env, *counter -- not torch's generator);
+ * mean_level = mean of levels; *counter advances by one.  Two launches on `stream`. */
+int mjx_terrain_levels(int nworld, const uint8_t* mask, const float* xpos, int nbody, int root_body,
+                       const float* command, float half_patch, float episode_length_s,
+                       const int64_t* types, int64_t* levels, const float* terrain_origins,
+                       int nrows, int ncols, float* env_origins, uint64_t seed, uint64_t* counter,
+                       float* mean_level, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Motion tracking (Mjlab-Tracking-Flat-Unitree-G1): the same fused pattern for the
  * tracking MDP (tasks/tracking/tracking_env_cfg.py:42-317, tasks/tracking/mdp/{commands,rewards,terminations,observations}.py):

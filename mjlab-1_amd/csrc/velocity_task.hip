@@ -81,7 +81,7 @@ __device__ __forceinline__ float uniform(float lo, float hi, float u) { return l
 
 // draw ids (per env, per env-step), kept disjoint between kernels
 enum : uint32_t { D_RESET = 0x1000, D_CMD_RESET = 0x2000, D_CMD = 0x3000, D_PUSH = 0x4000,
-                  D_NOISE = 0x5000 };
+                  D_NOISE = 0x5000, D_TERRAIN = 0x6000 };
 
 // EntityData derived reads (entity/data.py:20-31, 219-229, 320-327)
 struct Root {
@@ -843,6 +843,55 @@ __global__ void k_obs(const mjxTaskDesc* __restrict__ T) {
   co[i] = v;
 }
 
+// Terrain-level curriculum over the reset mask (tasks/velocity/mdp/curriculums.py:30-64,
+// terrains/terrain_importer.py:186-201), thread per env: a resetting env moves one level up
+// when it walked more than half a patch from its origin, down when less than half its
+// commanded distance over an episode; past the top level it draws a level (counter hash of
+// seed, env, counter); its origin becomes the sub-terrain origin [level, type].
+__global__ void k_terrain(int nworld, const uint8_t* __restrict__ mask, const float* __restrict__ xpos,
+                          int nbody, int root, const float* __restrict__ cmd, float half_patch,
+                          float ep_len_s, const int64_t* __restrict__ types, int64_t* __restrict__ levels,
+                          const float* __restrict__ torig, int nrows, int ncols,
+                          float* __restrict__ origins, uint64_t seed, const uint64_t* __restrict__ counter) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nworld || !mask[e]) return;
+  const float* p = xpos + ((size_t)e * nbody + root) * 3;
+  float* o = origins + (size_t)e * 3;
+  const float dx = p[0] - o[0], dy = p[1] - o[1];
+  const float dist = sqrtf(dx * dx + dy * dy);
+  const float* c = cmd + (size_t)e * 3;
+  const bool up = dist > half_patch;
+  const bool down = !up && dist < sqrtf(c[0] * c[0] + c[1] * c[1]) * ep_len_s * 0.5f;
+  int64_t lv = levels[e] + (up ? 1 : 0) - (down ? 1 : 0);
+  if (lv >= nrows) {
+    lv = (int64_t)(urand(seed, (uint32_t)e, *counter, D_TERRAIN) * (float)nrows);
+    if (lv >= nrows) lv = nrows - 1;
+  } else if (lv < 0) {
+    lv = 0;
+  }
+  levels[e] = lv;
+  const int64_t ty = types[e];
+  const float* src = torig + ((size_t)lv * ncols + (size_t)ty) * 3;
+  o[0] = src[0]; o[1] = src[1]; o[2] = src[2];
+}
+// mean level (the curriculum's logged state) and the draw counter's advance: one block
+__global__ __launch_bounds__(256) void k_terrain_mean(int nworld, const int64_t* __restrict__ levels,
+                                                      float* __restrict__ mean, uint64_t* __restrict__ counter) {
+  __shared__ float red[256];
+  float sum = 0.f;
+  for (int e = threadIdx.x; e < nworld; e += 256) sum += (float)levels[e];
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *mean = red[0] / (float)(nworld > 0 ? nworld : 1);
+    *counter += 1;
+  }
+}
+
 }  // namespace mjxt
 
 // ----------------------------------------------------------------------------- C ABI
@@ -951,5 +1000,23 @@ int mjx_task_observe(mjxTask* t, void* stream) {
 }
 
 const char* mjx_task_last_error(void) { return g_task_err.c_str(); }
+
+int mjx_terrain_levels(int nworld, const uint8_t* mask, const float* xpos, int nbody, int root_body,
+                       const float* command, float half_patch, float episode_length_s,
+                       const int64_t* types, int64_t* levels, const float* terrain_origins,
+                       int nrows, int ncols, float* env_origins, uint64_t seed, uint64_t* counter,
+                       float* mean_level, void* stream) {
+  if (nworld <= 0 || !mask || !xpos || !command || !types || !levels || !terrain_origins ||
+      !env_origins || !counter || !mean_level || nrows <= 0 || ncols <= 0 || root_body < 0 ||
+      root_body >= nbody)
+    return task_fail("mjx_terrain_levels: bad arguments");
+  hipLaunchKernelGGL(mjxt::k_terrain, dim3((nworld + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     nworld, mask, xpos, nbody, root_body, command, half_patch, episode_length_s,
+                     types, levels, terrain_origins, nrows, ncols, env_origins, seed, counter);
+  hipLaunchKernelGGL(mjxt::k_terrain_mean, dim3(1), dim3(256), 0, (hipStream_t)stream, nworld,
+                     levels, mean_level, counter);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : task_fail(std::string("k_terrain: ") + hipGetErrorString(e));
+}
 
 }  // extern "C"

@@ -23,7 +23,7 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
-           "mjx_task_last_error", "mjx_quat_mul",
+           "mjx_task_last_error", "mjx_quat_mul", "mjx_terrain_levels",
            # fused tracking-task managers (bound in fused_tracking.py)
            "mjx_track_create", "mjx_track_destroy", "mjx_track_action", "mjx_track_post",
            "mjx_track_reset", "mjx_track_observe", "mjx_track_desc_size", "mjx_track_last_error")
@@ -65,6 +65,10 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_spec.argtypes = [vp]
   L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
+  if hasattr(L, "mjx_terrain_levels"):
+    f32, u64 = ctypes.c_float, ctypes.c_uint64
+    L.mjx_terrain_levels.argtypes = [ci, vp, vp, ci, ci, vp, f32, f32, vp, vp, vp, ci, ci, vp, u64,
+                                     vp, vp, vp]
   if hasattr(L, "mjx_sim_track_air_time"):
     L.mjx_sim_track_air_time.argtypes = [vp, ci, ctypes.POINTER(ctypes.c_int32)] + [vp] * 6
   missing = [n for n in EXPORTS if not hasattr(L, n)]

@@ -679,9 +679,17 @@ def terrain_levels_vel(env, env_ids, command_name: str, asset_cfg=None):
 
 
 def _terrain_levels_vel_masked(env, mask, command_name: str, asset_cfg=None):
-  """The same over a reset mask (sync-free / graph-captured step)."""
+  """The same over a reset mask (sync-free / graph-captured step): one HIP kernel on the
+  GPU (`Terrain.update_env_origins_native`), the torch form elsewhere."""
   terrain = env.scene.terrain
-  up, down = _terrain_moves(env, slice(None), command_name, asset_cfg.name if asset_cfg else "robot")
+  name = asset_cfg.name if asset_cfg else "robot"
+  cmd = env.command_manager.get_command(command_name)
+  if terrain.env_origins.is_cuda and cmd.is_contiguous() and cmd.dtype == torch.float32:
+    root = int(env.scene[name].indexing.root_body_id)
+    terrain.update_env_origins_native(mask.contiguous(), env.sim.data.xpos, root, cmd,
+                                      env.max_episode_length_s)
+    return terrain.mean_level
+  up, down = _terrain_moves(env, slice(None), command_name, name)
   terrain.update_env_origins_masked(mask, up, down)
   return terrain.mean_level
 

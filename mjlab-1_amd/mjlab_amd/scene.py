@@ -592,6 +592,34 @@ class Terrain:
                                        self.env_origins))
     self.mean_level.copy_(self.terrain_levels.float().mean())
 
+  def update_env_origins_native(self, mask, xpos, root_body: int, command, episode_length_s: float):
+    """The terrain-level curriculum of the resetting envs as one HIP kernel
+    (`mjx_terrain_levels`: the rule of `terrain_levels_vel` + `update_env_origins`, and the
+    mean level), in place of ~13 torch launches.  Its wrap-around draw is a counter hash,
+    not torch's generator."""
+    import ctypes
+    from ._lib import lib
+    L = lib()
+    if not hasattr(self, "_counter"):
+      self._counter = torch.zeros(1, dtype=torch.int64, device=self.env_origins.device)
+      self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    for t in (mask, xpos, command, self.terrain_levels, self.terrain_types, self.terrain_origins,
+              self.env_origins):
+      assert t.is_contiguous()
+    vp = ctypes.c_void_p
+    stream = vp(torch.cuda.current_stream(self.env_origins.device).cuda_stream)
+    n, nb = int(xpos.shape[0]), int(xpos.shape[1])
+    rc = L.mjx_terrain_levels(n, vp(mask.data_ptr()), vp(xpos.data_ptr()), nb, int(root_body),
+                              vp(command.data_ptr()), float(self.size[0] / 2), float(episode_length_s),
+                              vp(self.terrain_types.data_ptr()), vp(self.terrain_levels.data_ptr()),
+                              vp(self.terrain_origins.data_ptr()), int(self.terrain_origins.shape[0]),
+                              int(self.terrain_origins.shape[1]), vp(self.env_origins.data_ptr()),
+                              ctypes.c_uint64(self._seed), vp(self._counter.data_ptr()),
+                              vp(self.mean_level.data_ptr()), stream)
+    if rc != 0:
+      from ._lib import MjxError
+      raise MjxError(L.mjx_task_last_error().decode())
+
   def randomize_env_origins(self, env_ids) -> None:
     """`terrain_importer.py:203-222` (play mode)."""
     rows, cols = self.terrain_origins.shape[:2]
