@@ -16,7 +16,6 @@
 
 namespace mjtr {
 
-constexpr int kBlock = 128;
 constexpr int kPostEnvs = 16;
 
 struct Acc {  // cross-env accumulators of one step's resets (block LDS copy, then global)
@@ -377,20 +376,21 @@ __global__ __launch_bounds__(kBinThreads) void k_bins(const mjxTrackDesc* __rest
 // U(joint_position_range) clipped to the soft limits; targets cleared.  `full_reset` adds
 // the rest of _reset_idx for the env (action, command-counter, push timer, episode length,
 // ctrl).  Every env writes the sampling metrics (CommandTerm fills them for all envs).
-__global__ void k_rsi(const mjxTrackDesc* __restrict__ T, const uint8_t* __restrict__ mask,
-                      int full_reset, uint32_t draw) {
+// wave per env: lane 0 the sampling, root and counters, lane j joint j
+__global__ __launch_bounds__(64 * kPostEnvs) void k_rsi(const mjxTrackDesc* __restrict__ T,
+                                                       const uint8_t* __restrict__ mask,
+                                                       int full_reset, uint32_t draw) {
   const mjxTrackDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= t.nworld) return;
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
+  if (e >= t.nworld) return;  // wave-uniform
   const int nbin = t.bin_count;
   const float* cdf = t.sampling;
-  t.metrics[(size_t)10 * t.nworld + e] = cdf[nbin + 0];
-  t.metrics[(size_t)11 * t.nworld + e] = cdf[nbin + 1];
-  t.metrics[(size_t)12 * t.nworld + e] = cdf[nbin + 2];
+  if (lane < 3) t.metrics[(size_t)(10 + lane) * t.nworld + e] = cdf[nbin + lane];
   if (!mask[e]) return;
   const uint64_t step = *t.step_counter, seed = t.seed;
   const int nj = t.njoint;
-  // start frame
+  // start frame (every lane draws the same values)
   int64_t ts = 0;
   if (t.sampling_mode == 1) {
     ts = (int64_t)(urand(seed, e, step, draw) * (float)t.nframe);
@@ -401,12 +401,23 @@ __global__ void k_rsi(const mjxTrackDesc* __restrict__ T, const uint8_t* __restr
     while (b < nbin - 1 && cdf[b] <= u) b++;
     ts = (int64_t)(((float)b + urand(seed, e, step, draw + 1)) / (float)nbin * (float)(t.nframe - 1));
   }
-  t.time_steps[e] = ts;
-  if (full_reset) {
-    for (int j = 0; j < nj; j++) {
+  for (int j = lane; j < nj; j += 64) {
+    if (full_reset) {
       const size_t i = (size_t)e * nj + j;
       t.action[i] = t.prev_action[i] = t.prev_prev_action[i] = 0.f;
     }
+    float jp = t.m_joint_pos[(size_t)ts * nj + j] +
+               uniform(t.joint_position_range[0], t.joint_position_range[1], urand(seed, e, step, D_RSI + 12 + j));
+    jp = fminf(fmaxf(jp, t.soft_lo[j]), t.soft_hi[j]);
+    t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] = jp;
+    t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]] = t.m_joint_vel[(size_t)ts * nj + j];
+    t.joint_pos_target[(size_t)e * nj + j] = 0.f;
+    if (full_reset)  // Scene.write_data_to_sim after the reset: ctrl <- cleared targets
+      t.ctrl[(size_t)e * t.nu + t.ctrl_of_action[j]] = 0.f;
+  }
+  if (lane != 0) return;
+  t.time_steps[e] = ts;
+  if (full_reset) {
     t.command_counter[e] = 0;
     if (t.has_push)
       t.push_time_left[e] = uniform(t.push_interval[0], t.push_interval[1], urand(seed, e, step, D_PUSH + 15));
@@ -431,35 +442,23 @@ __global__ void k_rsi(const mjxTrackDesc* __restrict__ T, const uint8_t* __restr
   float* qv = t.qvel + (size_t)e * t.nv + t.free_v_adr;
   qv[0] = m.lin.x + v[0]; qv[1] = m.lin.y + v[1]; qv[2] = m.lin.z + v[2];
   qv[3] = ang_b.x; qv[4] = ang_b.y; qv[5] = ang_b.z;
-  for (int j = 0; j < nj; j++) {
-    float jp = t.m_joint_pos[(size_t)ts * nj + j] +
-               uniform(t.joint_position_range[0], t.joint_position_range[1], urand(seed, e, step, D_RSI + 12 + j));
-    jp = fminf(fmaxf(jp, t.soft_lo[j]), t.soft_hi[j]);
-    t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]] = jp;
-    t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]] = t.m_joint_vel[(size_t)ts * nj + j];
-    t.joint_pos_target[(size_t)e * nj + j] = 0.f;
-  }
-  if (full_reset)  // Scene.write_data_to_sim after the reset: ctrl <- cleared targets
-    for (int k = 0; k < nj; k++) t.ctrl[(size_t)e * t.nu + t.ctrl_of_action[k]] = 0.f;
 }
 
 // CommandTerm.compute, first half: _update_metrics (commands.py:223-257), timer, time step
 // advance, envs at the motion end into resample_mask (thread per env)
-__global__ void k_cmd(const mjxTrackDesc* __restrict__ T) {
+// Wave per env (kPostEnvs envs per block): lane k takes body k and joint k (a thread-per-env
+// loop pays a dependent index-then-state global load per body and joint), wave sums.
+__global__ __launch_bounds__(64 * kPostEnvs) void k_cmd(const mjxTrackDesc* __restrict__ T) {
   const mjxTrackDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= t.nworld) return;
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
+  if (e >= t.nworld) return;  // wave-uniform
   const int64_t ts = frame_of(t, e);
   const int nmb = t.nmb, nj = t.njoint;
   float* M = t.metrics;
   const size_t N = (size_t)t.nworld;
-  const Link ra = robot_link(t, e, t.anchor_body), ma = motion_link(t, e, ts, t.anchor_motion);
-  M[0 * N + e] = norm3(ma.p - ra.p);
-  M[1 * N + e] = qerr(ma.q, ra.q);
-  M[2 * N + e] = norm3(ma.lin - ra.lin);
-  M[3 * N + e] = norm3(ma.ang - ra.ang);
   float bp = 0.f, bo = 0.f, bl = 0.f, ba = 0.f;
-  for (int k = 0; k < nmb; k++) {
+  for (int k = lane; k < nmb; k += 64) {
     const Link r = robot_link(t, e, t.robot_body[k]), m = motion_link(t, e, ts, k);
     const size_t i = (size_t)e * nmb + k;
     bp += norm3(v3(t.body_pos_rel + 3 * i) - r.p);
@@ -467,17 +466,25 @@ __global__ void k_cmd(const mjxTrackDesc* __restrict__ T) {
     bl += norm3(m.lin - r.lin);
     ba += norm3(m.ang - r.ang);
   }
-  M[4 * N + e] = bp / (float)nmb;
-  M[5 * N + e] = bo / (float)nmb;
-  M[6 * N + e] = bl / (float)nmb;
-  M[7 * N + e] = ba / (float)nmb;
   float jp = 0.f, jv = 0.f;
-  for (int j = 0; j < nj; j++) {
+  for (int j = lane; j < nj; j += 64) {
     const float dp = t.m_joint_pos[(size_t)ts * nj + j] - t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
     const float dv = t.m_joint_vel[(size_t)ts * nj + j] - t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]];
     jp += dp * dp;
     jv += dv * dv;
   }
+  bp = wave_add(bp); bo = wave_add(bo); bl = wave_add(bl); ba = wave_add(ba);
+  jp = wave_add(jp); jv = wave_add(jv);
+  if (lane != 0) return;
+  const Link ra = robot_link(t, e, t.anchor_body), ma = motion_link(t, e, ts, t.anchor_motion);
+  M[0 * N + e] = norm3(ma.p - ra.p);
+  M[1 * N + e] = qerr(ma.q, ra.q);
+  M[2 * N + e] = norm3(ma.lin - ra.lin);
+  M[3 * N + e] = norm3(ma.ang - ra.ang);
+  M[4 * N + e] = bp / (float)nmb;
+  M[5 * N + e] = bo / (float)nmb;
+  M[6 * N + e] = bl / (float)nmb;
+  M[7 * N + e] = ba / (float)nmb;
   M[8 * N + e] = sqrtf(jp);
   M[9 * N + e] = sqrtf(jv);
   t.time_left[e] -= t.step_dt;
@@ -488,16 +495,19 @@ __global__ void k_cmd(const mjxTrackDesc* __restrict__ T) {
 
 // _relative_targets (commands.py:384-404) after the resample, then the interval push
 // (event_manager.py:124-146, events.py:209-223); thread per env
-__global__ void k_targets(const mjxTrackDesc* __restrict__ T) {
+__global__ __launch_bounds__(64 * kPostEnvs) void k_targets(const mjxTrackDesc* __restrict__ T) {
+  // wave per env, lane per body (the stores of a thread-per-env loop may alias the next
+  // body's loads, which then serialise)
   const mjxTrackDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= t.nworld) return;
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
+  if (e >= t.nworld) return;  // wave-uniform
   const int64_t ts = frame_of(t, e);
   const int nmb = t.nmb;
   const Link ra = robot_link(t, e, t.anchor_body), ma = motion_link(t, e, ts, t.anchor_motion);
   const V3 dpos = {ra.p.x, ra.p.y, ma.p.z};
   const Q4 dori = yaw_only(qmul(ra.q, qinv(ma.q)));
-  for (int k = 0; k < nmb; k++) {
+  for (int k = lane; k < nmb; k += 64) {
     const Link m = motion_link(t, e, ts, k);
     const size_t i = (size_t)e * nmb + k;
     const Q4 q = qmul(dori, m.q);
@@ -507,7 +517,7 @@ __global__ void k_targets(const mjxTrackDesc* __restrict__ T) {
     op[0] = p.x; op[1] = p.y; op[2] = p.z;
     oq[0] = q.w; oq[1] = q.x; oq[2] = q.y; oq[3] = q.z;
   }
-  if (t.has_push) {
+  if (lane == 0 && t.has_push) {
     float pt = t.push_time_left[e] - t.step_dt;
     if (pt < 1e-6f) {
       const uint64_t step = *t.step_counter, seed = t.seed;
@@ -727,24 +737,24 @@ int mjx_track_post(mjxTrack* t, void* stream) {
 
 int mjx_track_reset(mjxTrack* t, void* stream) {
   if (!t) return track_fail("null task");
-  const int nb = (t->nworld + mjtr::kBlock - 1) / mjtr::kBlock;
+  const int nwave = (t->nworld + mjtr::kPostEnvs - 1) / mjtr::kPostEnvs;  // blocks of kPostEnvs waves
   hipLaunchKernelGGL(mjtr::k_bins, dim3(1), dim3(mjtr::kBinThreads), 0, (hipStream_t)stream,
                      t->dev, (const uint8_t*)t->host.reset_buf, 0);
-  hipLaunchKernelGGL(mjtr::k_rsi, dim3(nb), dim3(mjtr::kBlock), 0, (hipStream_t)stream, t->dev,
-                     (const uint8_t*)t->host.reset_buf, 1, (uint32_t)mjtr::D_RESET_SAMPLE);
+  hipLaunchKernelGGL(mjtr::k_rsi, dim3(nwave), dim3(64 * mjtr::kPostEnvs), 0, (hipStream_t)stream,
+                     t->dev, (const uint8_t*)t->host.reset_buf, 1, (uint32_t)mjtr::D_RESET_SAMPLE);
   return track_launched("k_rsi");
 }
 
 int mjx_track_observe(mjxTrack* t, void* stream) {
   if (!t) return track_fail("null task");
-  const int nb = (t->nworld + mjtr::kBlock - 1) / mjtr::kBlock;
+  const int nwave = (t->nworld + mjtr::kPostEnvs - 1) / mjtr::kPostEnvs;  // blocks of kPostEnvs waves
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(mjtr::k_cmd, dim3(nb), dim3(mjtr::kBlock), 0, s, t->dev);
+  hipLaunchKernelGGL(mjtr::k_cmd, dim3(nwave), dim3(64 * mjtr::kPostEnvs), 0, s, t->dev);
   hipLaunchKernelGGL(mjtr::k_bins, dim3(1), dim3(mjtr::kBinThreads), 0, s, t->dev,
                      (const uint8_t*)t->host.resample_mask, 1);
-  hipLaunchKernelGGL(mjtr::k_rsi, dim3(nb), dim3(mjtr::kBlock), 0, s, t->dev,
+  hipLaunchKernelGGL(mjtr::k_rsi, dim3(nwave), dim3(64 * mjtr::kPostEnvs), 0, s, t->dev,
                      (const uint8_t*)t->host.resample_mask, 0, (uint32_t)mjtr::D_CMD_SAMPLE);
-  hipLaunchKernelGGL(mjtr::k_targets, dim3(nb), dim3(mjtr::kBlock), 0, s, t->dev);
+  hipLaunchKernelGGL(mjtr::k_targets, dim3(nwave), dim3(64 * mjtr::kPostEnvs), 0, s, t->dev);
   const long n = (long)t->nworld * t->host.ncritic;
   hipLaunchKernelGGL(mjtr::k_obs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, t->dev);
   return track_launched("k_obs");
