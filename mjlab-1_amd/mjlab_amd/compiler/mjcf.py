@@ -171,6 +171,7 @@ class XModel:
   sensors: list
   angle_deg: bool
   eulerseq: str
+  inertiafromgeom: str = "auto"  # <compiler inertiafromgeom>: "auto" | "true" | "false"
 
 
 class _Defaults:
@@ -219,9 +220,11 @@ def parse_mjcf_string(text: str) -> XModel:
   comp = root.find("compiler")
   angle_deg = True
   eulerseq = "xyz"
+  inertiafromgeom = "auto"
   if comp is not None:
     angle_deg = comp.attrib.get("angle", "degree") != "radian"
     eulerseq = comp.attrib.get("eulerseq", "xyz")
+    inertiafromgeom = comp.attrib.get("inertiafromgeom", "auto")
   defaults = _Defaults()
   dflt = root.find("default")
   if dflt is not None:
@@ -281,7 +284,8 @@ def parse_mjcf_string(text: str) -> XModel:
   if sens is not None:
     for s in sens:
       sensors.append((s.tag, dict(s.attrib)))
-  return XModel(root.attrib.get("model", ""), world, excludes, sensors, angle_deg, eulerseq)
+  return XModel(root.attrib.get("model", ""), world, excludes, sensors, angle_deg, eulerseq,
+                inertiafromgeom)
 
 
 def geom_frame(attrs: dict, angle_deg: bool, eulerseq: str):

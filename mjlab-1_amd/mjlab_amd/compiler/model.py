@@ -194,7 +194,64 @@ class _Builder:
     return len(self.bodies) - 1
 
 
-def _inertial(b: XBody):
+def _geom_inertia(attrs: dict, xml: XModel):
+  """Mass, frame and principal inertia of one geom at its density (or explicit mass), as
+  MuJoCo's geom inertia for sphere / capsule / cylinder / box / ellipsoid; None for the
+  massless types (plane, hfield) and meshes (volume unavailable without the mesh)."""
+  t = attrs["type"]
+  if t not in ("sphere", "capsule", "cylinder", "box", "ellipsoid"):
+    return None
+  pos, quat, size = geom_frame(attrs, xml.angle_deg, xml.eulerseq)
+  r = float(size[0])
+  if t == "sphere":
+    vol, unit = 4.0 / 3.0 * np.pi * r ** 3, np.full(3, 0.4 * r * r)
+  elif t == "capsule":
+    h = 2.0 * float(size[1])  # cylinder length; two hemispheres of radius r at its ends
+    vs, vc = 4.0 / 3.0 * np.pi * r ** 3, np.pi * r * r * h
+    vol = vs + vc
+    ixy = (vc * (3 * r * r + h * h) / 12 + vs * (0.4 * r * r + h * h / 4 + 3 * r * h / 8)) / vol
+    unit = np.array([ixy, ixy, (vc * r * r / 2 + vs * 0.4 * r * r) / vol])
+  elif t == "cylinder":
+    h = 2.0 * float(size[1])
+    vol = np.pi * r * r * h
+    unit = np.array([(3 * r * r + h * h) / 12, (3 * r * r + h * h) / 12, r * r / 2])
+  elif t == "box":
+    a, b, c = (2.0 * float(x) for x in size[:3])
+    vol = a * b * c
+    unit = np.array([b * b + c * c, a * a + c * c, a * a + b * b]) / 12
+  else:  # ellipsoid
+    a, b, c = (float(x) for x in size[:3])
+    vol = 4.0 / 3.0 * np.pi * a * b * c
+    unit = np.array([b * b + c * c, a * a + c * c, a * a + b * b]) / 5
+  mass = float(attrs["mass"]) if "mass" in attrs else float(attrs.get("density", 1000.0)) * vol
+  return mass, np.asarray(pos, float), quat_to_mat(quat), mass * unit
+
+
+def _inertial_from_geoms(b: XBody, xml: XModel):
+  """MuJoCo's inertiafromgeom: the body's mass, centre of mass and principal inertia from
+  its geoms (parallel-axis sum about the com, eigen-decomposed into ipos / iquat / diag)."""
+  parts = [g for g in (_geom_inertia(x.attrs, xml) for x in b.geoms) if g is not None and g[0] > 0]
+  if not parts:
+    return None
+  mass = sum(p[0] for p in parts)
+  com = sum(p[0] * p[1] for p in parts) / mass
+  I = np.zeros((3, 3))
+  for m, pos, R, diag in parts:
+    d = pos - com
+    I += R @ np.diag(diag) @ R.T + m * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+  w, V = np.linalg.eigh(I)
+  if np.linalg.det(V) < 0:
+    V[:, 0] = -V[:, 0]
+  from .mjcf import mat_to_quat
+  return dict(mass=mass, ipos=com, iquat=quat_normalize(mat_to_quat(V)), inertia=w)
+
+
+def _inertial(b: XBody, xml: XModel | None = None):
+  mode = xml.inertiafromgeom if xml is not None else "false"
+  if mode == "true" or (mode == "auto" and b.inertial is None):
+    fg = _inertial_from_geoms(b, xml)
+    if fg is not None:
+      return fg
   if b.inertial is None:
     return dict(mass=0.0, ipos=np.zeros(3), iquat=np.array([1.0, 0, 0, 0]), inertia=np.zeros(3))
   inr = b.inertial
@@ -313,7 +370,7 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     joint_name_order = []
 
     def walk(xb: XBody, parent: int):
-      bid = B.add_body(prefix + xb.name, parent, xb.pos, xb.quat, _inertial(xb), xb.mocap)
+      bid = B.add_body(prefix + xb.name, parent, xb.pos, xb.quat, _inertial(xb, xml), xb.mocap)
       for j in xb.joints:
         joints.append(dict(body=bid, name=prefix + j.name, attrs=j.attrs))
         if j.attrs["type"] != "free":
@@ -825,6 +882,9 @@ def _set_const(m: Model):
   A["body_subtreemass"] = k["stm"]
   M = k["M"]
   if m.nv:
+    if np.min(np.diag(M)) < MINVAL or np.linalg.cond(M) > 1e14:
+      # MuJoCo's compiler error for the same model (mj_setConst)
+      raise ValueError("mass and inertia of moving bodies must be larger than mjMINVAL")
     Minv = np.linalg.inv(M)
     m.meaninertia = float(np.trace(M) / m.nv)
   else:
