@@ -94,10 +94,15 @@ struct mjxSim_ {
       if (side.join[k]) (void)hipEventDestroy(side.join[k]);
       if (side.stream[k]) (void)hipStreamDestroy(side.stream[k]);
     }
+    for (int p = 0; p < mjx::kMaxSplit; p++) {
+      if (side.split[p]) (void)hipStreamDestroy(side.split[p]);
+      if (side.split_join[p]) (void)hipEventDestroy(side.split_join[p]);
+    }
+    if (side.split_fork) (void)hipEventDestroy(side.split_fork);
   }
   int gC = 0, gF = 0, gstride = 0;
   float* gscr = nullptr;
-  int* wl = nullptr;  // Newton work lists: [nworld] world ids + [2 * (kRowClasses + 1)] segments
+  int* wl = nullptr;  // Newton work lists: [nworld] world ids + [kMaxSplit][2 * (kRowClasses + 1)] segments
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
   std::vector<void*> expanded_allocs;
@@ -445,13 +450,28 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
     ds.njmax = k < s->nrowclass ? s->row_cap[k] : s->d.njmax;
     s->lds_ph[3 + k] = mjx::make_lds(ds, 1);
   }
-  if (s->nrowclass > 0) {
-    hipError_t e = hipEventCreateWithFlags(&s->side.fork, hipEventDisableTiming);
+  // batch splits (launch_step): large batches of models without row classes run as
+  // concurrent halves.  MJX355_SPLIT=<n> overrides (diagnostic; 1 = one launch set per phase).
+  s->side.nsplit = nworld >= mjx::kSplitMinWorlds && s->nrowclass == 0 ? 2 : 1;
+  if (const char* ev = getenv("MJX355_SPLIT")) s->side.nsplit = std::max(1, std::min(atoi(ev), mjx::kMaxSplit));
+  if (s->nrowclass > 0) s->side.nsplit = 1;
+  {
+    hipError_t e = hipSuccess;
+    if (s->side.nsplit > 1) {
+      e = hipEventCreateWithFlags(&s->side.split_fork, hipEventDisableTiming);
+      for (int p = 1; p < s->side.nsplit && e == hipSuccess; p++) {
+        e = hipStreamCreateWithFlags(&s->side.split[p], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.split_join[p], hipEventDisableTiming);
+      }
+    }
     // default priority: measured, high-priority side streams let the few heavy worlds hold
     // LDS that the bulk of small-class worlds needs (Newton span 214 -> 281 us, G1 4096)
-    for (int k = 0; k < s->nrowclass && e == hipSuccess; k++) {
-      e = hipStreamCreateWithFlags(&s->side.stream[k], hipStreamNonBlocking);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[k], hipEventDisableTiming);
+    if (s->nrowclass > 0 && e == hipSuccess) {
+      e = hipEventCreateWithFlags(&s->side.fork, hipEventDisableTiming);
+      for (int k = 0; k < s->nrowclass && e == hipSuccess; k++) {
+        e = hipStreamCreateWithFlags(&s->side.stream[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[k], hipEventDisableTiming);
+      }
     }
     if (e != hipSuccess) { delete s; return fail(std::string("side streams: ") + hipGetErrorString(e)); }
   }
@@ -484,9 +504,9 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc scratch: ") + hipGetErrorString(e)); }
   e = hipMemset(s->gscr, 0, sizeof(float) * (size_t)nworld * s->gstride);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
-  e = hipMalloc((void**)&s->wl, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1)));
+  e = hipMalloc((void**)&s->wl, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1) * mjx::kMaxSplit));
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc work lists: ") + hipGetErrorString(e)); }
-  e = hipMemset(s->wl, 0, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1)));
+  e = hipMemset(s->wl, 0, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1) * mjx::kMaxSplit));
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
   e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }

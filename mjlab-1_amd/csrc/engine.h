@@ -15,6 +15,8 @@ constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
 constexpr int kRowClasses = 2;   // Newton row classes below the full capacity
+constexpr int kMaxSplit = 4;     // concurrent batch splits (launch_step; default 2)
+constexpr int kSplitMinWorlds = 2048;  // batches at least this large run split
 constexpr int kMaxAirSlots = 8;  // contact-sensor slots with air-time tracking
 constexpr int kStaticChunk = 64; // terrain geoms per broadphase chunk
 
@@ -146,7 +148,7 @@ struct Params {
   // wl_seg[2k] + wl_seg[2k+1]) -- each class launch takes its worlds densely and largest
   // first instead of filtering all nworld workgroups.
   int* wl_list;
-  int* wl_seg;   // [2 * (kRowClasses + 1)]
+  int* wl_seg;   // [kMaxSplit][2 * (kRowClasses + 1)]: one segment table per batch split
   float* gscr;   // per-world hand-off scratch: [B pack | C pack | F], gstride floats per world
   int gC;        // offset of the C pack inside a world's scratch
   int gF;        // offset of F: the implicit-integration factor (nvp x nvp rows), read by
@@ -165,9 +167,15 @@ struct Params {
 hipError_t prepare_step(const Params& host);  // one-time kernel attributes (not capturable)
 // Side streams for the Newton row classes beyond the first: forked from and joined back
 // into the launch stream every substep (graph-capturable fork/join).
+// With the batch split (nsplit > 1; models without row classes), split k > 0 runs on
+// split[k], forked from the launch stream before the first substep and joined back after
+// the last.
 struct SideStream {
   hipStream_t stream[kRowClasses];
   hipEvent_t fork, join[kRowClasses];
+  int nsplit;                        // batch splits in use (1 = one launch set per phase)
+  hipStream_t split[kMaxSplit];      // [0] unused: split 0 runs on the launch stream
+  hipEvent_t split_fork, split_join[kMaxSplit];
 };
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,

@@ -1170,9 +1170,11 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
   }
 }
 
+// Worlds [w0, w1) -- one split of the batch (launch_step); `split` selects that split's
+// Newton work-list segments.
 template <int NR, int PH, int SP>
-__global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int nworld,
-                                                    int last, int integrate,
+__global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int w0, int w1,
+                                                    int split, int last, int integrate,
                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
   const auto& d = dims_of<SP>(P);
@@ -1183,17 +1185,18 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate] : lds_of<SP, PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
-  int w = blockIdx.x;
+  int w = w0 + (int)blockIdx.x;
   if constexpr (PH == 1) {
     // Newton by row class: workgroup i takes the i-th world of its class's list
     // (classify_kernel: rows descending, masked worlds only)
     if (P->nrowclass > 0 && integrate >= 0) {  // integrate < 0: every world, full carve
-      const int* seg = P->wl_seg + 2 * integrate;
-      if (w >= seg[1]) return;
-      w = P->wl_list[seg[0] + w];
+      const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + integrate);
+      if ((int)blockIdx.x >= seg[1]) return;
+      w = P->wl_list[seg[0] + blockIdx.x];
     }
   }
-  if (w >= nworld) return;
+  (void)split;
+  if (w >= w1) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
   float* gc = gw + P->gC;
@@ -2914,6 +2917,6 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
 #endif
 }
 
-using StepFn = void (*)(const Params*, int, int, int, const uint8_t*);
+using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 
 }  // namespace mjx
