@@ -131,6 +131,11 @@ static mjx::Params host_params(const mjxSim_* s) {
   for (int i = 0; i < mjx::kMaxAirSlots; i++) p.air_found[i] = s->air_found[i];
   p.air_cur = s->air_buf[0]; p.air_last = s->air_buf[1]; p.air_cc = s->air_buf[2];
   p.air_lc = s->air_buf[3]; p.air_time = s->air_buf[4];
+  static const int minrows = [] {
+    const char* e = getenv("MJX355_STAMP_MINROWS");
+    return e ? atoi(e) : 0;
+  }();
+  p.stamp_minrows = minrows;
   return p;
 }
 

@@ -160,6 +160,7 @@ struct Params {
   int nair;
   int air_found[kMaxAirSlots];
   float *air_cur, *air_last, *air_cc, *air_lc, *air_time;
+  int stamp_minrows;  // diagnostic stamps build: count worlds with at least this many rows
 };
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of

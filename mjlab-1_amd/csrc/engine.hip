@@ -217,14 +217,25 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     }
     if (e != hipSuccess) return e;
   }
+  // Row-class pipelines (nc > 0, one split): each class's Newton launch is followed on the
+  // same stream by its phase C and then by the next substep's phase A for the same worlds,
+  // so the bulk class's C and next A overlap the heavy class's Newton tail; the streams
+  // join before the next classify.  MJX355_CLASS_PIPE=0: phase C / A over every world
+  // after the join (diagnostic).
+  static const bool pipe = [] {
+    const char* e = getenv("MJX355_CLASS_PIPE");
+    return !e || atoi(e) != 0;
+  }();
   for (int sub = 0; sub < nsubstep; sub++) {
     const int last = sub == nsubstep - 1;
     for (int k = 0; k < nsplit; k++) {
       const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
       if (n <= 0) continue;
       hipStream_t st = sst[k];
-      hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), st, dev, w0, w1, k,
-                         last, integrate, mask);
+      const bool piped = nc > 0 && !mask && pipe;
+      if (!piped || sub == 0)
+        hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), st, dev, w0, w1, k,
+                           last, integrate, mask);
       if (nc > 0 && mask) {
         // masked forward (a few reset worlds): one Newton launch at full capacity over the
         // masked worlds -- no classify launch, no fork/join latency on this short critical path
@@ -235,25 +246,35 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                            k, mask);
         // Newton by row class, concurrently: the full-capacity class (few worlds, long
         // per-world latency) first on a side stream so its blocks dispatch first, the middle
-        // classes on further side streams, the smallest (most worlds) on the split's stream.
+        // classes on further side streams, the smallest (most worlds) on the launch stream.
         // Measured: forking the side classes after the smallest makes the full class the tail
         // (B span 240 -> 255 us, G1).
         e = hipEventRecord(side->fork, st);
         if (e != hipSuccess) return e;
+        // class c's stream: B, then (piped) C and the next substep's A of the same worlds
+        auto class_chain = [&](hipStream_t cs, int cls) {
+          hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1), cs, dev,
+                             w0, w1, k, last, cls, mask);
+          if (!piped) return;
+          hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
+                             k | (cls + 1) << 8, last, integrate, mask);
+          if (!last)
+            hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
+                               k | (cls + 1) << 8, sub + 1 == nsubstep - 1, integrate, mask);
+        };
         for (int c = 0; c < nc; c++) {
           const int cls = c == 0 ? 0 : nc + 1 - c;  // 0, then nc, nc-1, ..., 2
           e = hipStreamWaitEvent(side->stream[c], side->fork, 0);
           if (e != hipSuccess) return e;
-          hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
-                             side->stream[c], dev, w0, w1, k, last, cls, mask);
+          class_chain(side->stream[c], cls);
         }
-        hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 3), st, dev, w0, w1, k, last,
-                           1, mask);
+        class_chain(st, 1);
         for (int c = 0; c < nc; c++) {
           e = hipEventRecord(side->join[c], side->stream[c]);
           if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[c], 0);
           if (e != hipSuccess) return e;
         }
+        if (piped) continue;
       } else {
         hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
                            0, mask);

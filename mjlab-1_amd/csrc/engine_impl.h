@@ -198,11 +198,15 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
     stamp_acc[16 + (k)] += t_ - sub_prev;                                        \
     sub_prev = t_;                                                               \
   } while (0)
+// Only worlds with at least P->stamp_minrows constraint rows this substep are counted
+// (MJX355_STAMP_MINROWS: the breakdown of the heavy worlds); slot 47 counts flushes.
 #define STAMP_FLUSH()                                                            \
   do {                                                                           \
-    if (lane == 0)                                                               \
+    if (lane == 0 && D.nefc[w] >= P->stamp_minrows) {                            \
+      stamp_acc[47] = 1;                                                         \
       for (int k_ = 0; k_ < 48; k_++)                                            \
         if (stamp_acc[k_]) atomicAdd((unsigned long long*)&D.prof[k_], stamp_acc[k_]); \
+    }                                                                            \
   } while (0)
 #else
 #define STAMP(k) do {} while (0)
@@ -1170,11 +1174,12 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
   }
 }
 
-// Worlds [w0, w1) -- one split of the batch (launch_step); `split` selects that split's
-// Newton work-list segments.
+// Worlds [w0, w1) -- one split of the batch (launch_step).  `sel` & 0xff selects that
+// split's Newton work-list segments; in phases A and C, sel >> 8 = row class + 1 restricts
+// the launch to that class's worlds (0: every world).
 template <int NR, int PH, int SP>
 __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int w0, int w1,
-                                                    int split, int last, int integrate,
+                                                    int sel, int last, int integrate,
                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
   const auto& d = dims_of<SP>(P);
@@ -1186,6 +1191,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
   int w = w0 + (int)blockIdx.x;
+  const int split = sel & 0xff;
   if constexpr (PH == 1) {
     // Newton by row class: workgroup i takes the i-th world of its class's list
     // (classify_kernel: rows descending, masked worlds only)
@@ -1195,7 +1201,15 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
       w = P->wl_list[seg[0] + blockIdx.x];
     }
   }
-  (void)split;
+  if constexpr (PH == 0 || PH == 2) {
+    // phase C of one row class right behind that class's Newton launch, and phase A of the
+    // next substep for the same worlds (the class lists stay valid until the next classify)
+    if (sel >> 8) {
+      const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + (sel >> 8) - 1);
+      if ((int)blockIdx.x >= seg[1]) return;
+      w = P->wl_list[seg[0] + blockIdx.x];
+    }
+  }
   if (w >= w1) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]

@@ -20,7 +20,10 @@ for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
   p1 = env.sim.profile()
   d = [b - a for a, b in zip(p0, p1)]
   tot = sum(d[:16])
-  nsub = 20 * env.cfg.decimation * N
+  # world-substeps counted (MJX355_STAMP_MINROWS filters to the heavy worlds): 3 flushes
+  # (phases A, B, C) per counted world-substep
+  nsub = max(d[47] // 3, 1)
+  print(f"   counted world-substeps {nsub} of {20 * env.cfg.decimation * N}")
   print(f"== {task}: {tot / nsub:.0f} cycles per world-substep (s_memtime ticks)")
   for i, n in enumerate(NAMES):
     print(f"  {n:22s} {d[i] / nsub:10.0f}  {100 * d[i] / max(tot, 1):5.1f}%")
