@@ -1128,49 +1128,61 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     }
     fg = mulTv(S + L.con_frame + 9 * c, fc);
   }
-  for (int k = 0; k < m.ncsens; k++) {
-    const int s = m.cs_sensor[k];
-    const int32_t* ip = m.sensor_intprm + 3 * s;
-    const int bits = ip[0], reduce = ip[1];
-    float* out = sd + m.sensor_adr[s];
+  // the sensors' descriptors, lane k = k-th single-slot contact sensor (ncsens <= 64): the
+  // loop below reads them with v_readlane instead of a dependent scalar-load chain per sensor
+  const int ncs = m.ncsens;
+  int dbits = 0, dred = 0, dadr = 0, ddim = 0;
+  if (lane < ncs) {
+    const int s = m.cs_sensor[lane];
+    dbits = m.sensor_intprm[3 * s];
+    dred = m.sensor_intprm[3 * s + 1];
+    dadr = m.sensor_adr[s];
+    ddim = m.sensor_dim[s];
+  }
+  for (int k = 0; k < ncs; k++) {
+    const int bits = __builtin_amdgcn_readlane(dbits, k), reduce = __builtin_amdgcn_readlane(dred, k);
+    const int adr = __builtin_amdgcn_readlane(dadr, k), dim = __builtin_amdgcn_readlane(ddim, k);
+    float* out = sd + adr;
     const bool a1 = (m1 >> k) & 1ull, a2 = (m2 >> k) & 1ull;
     const bool match = a1 || a2;
     const unsigned long long bal = __ballot(match);
     const float found = (float)__popcll(bal);
-    const int dim = m.sensor_dim[s];
+    // every output element of the sensor in one store (lanes < dim <= 3): the zeros of
+    // mjSENS_CONTACT's empty slot and the selected values at once
+    float v = 0.f;
     if (reduce == REDUCE_NETFORCE) {
       const float sg = match ? (a1 ? 1.f : -1.f) : 0.f;
       const float nx = wave_sum(sg * fg.x), ny = wave_sum(sg * fg.y), nz = wave_sum(sg * fg.z);
-      if (lane == 0) {
-        for (int i = 0; i < dim; i++) out[i] = 0.f;
-        if (bits & 1) out[0] = found;
-        else if (bits & 2) { out[0] = nx; out[1] = ny; out[2] = nz; }
-      }
-      continue;
-    }
-    // one slot: the matching contact with the smallest key (ties -> lowest contact index)
-    int sel = -1;
-    if (reduce == REDUCE_NONE) {
-      sel = bal ? __ffsll((long long)bal) - 1 : -1;  // key = contact index
+      if (bits & 1) v = lane == 0 ? found : 0.f;
+      else if (bits & 2) v = lane == 0 ? nx : lane == 1 ? ny : lane == 2 ? nz : 0.f;
     } else {
-      float key = reduce == REDUCE_MINDIST ? dist : -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z);
-      if (!match) key = FLT_MAX;
-      float kmin = key;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) kmin = fminf(kmin, __shfl_xor(kmin, o));
-      const unsigned long long win = __ballot(match && key == kmin);
-      sel = win ? __ffsll((long long)win) - 1 : -1;
+      // one slot: the matching contact with the smallest key (ties -> lowest contact index)
+      int sel = -1;
+      if (reduce == REDUCE_NONE) {
+        sel = bal ? __ffsll((long long)bal) - 1 : -1;  // key = contact index
+      } else {
+        float key = reduce == REDUCE_MINDIST ? dist : -sqrtf(fc.x * fc.x + fc.y * fc.y + fc.z * fc.z);
+        if (!match) key = FLT_MAX;
+        const float kmin = wave_min(key);
+        const unsigned long long win = __ballot(match && key == kmin);
+        sel = win ? __ffsll((long long)win) - 1 : -1;
+      }
+      if (sel >= 0) {
+        const int cs = sel;
+        const float sg = rl(a1 ? 1.f : -1.f, cs);
+        const int t = lane < 3 ? lane : 0;
+        if (bits & 1) v = lane == 0 ? found : 0.f;
+        else if (bits & 8) v = lane == 0 ? rl(dist, cs) : 0.f;
+        else if (bits & 16) v = lane < 3 ? S[L.con_pos + 3 * cs + t] : 0.f;
+        else if (bits & 32) v = lane < 3 ? sg * S[L.con_frame + 9 * cs + t] : 0.f;
+        else if (bits & 64) v = lane < 3 ? sg * S[L.con_frame + 9 * cs + 3 + t] : 0.f;
+        else if (bits & 2) {
+          const float fx = rl(fc.x, cs), fy = rl(fc.y, cs), fz = rl(fc.z, cs);
+          v = lane == 0 ? fx : lane == 1 ? fy : lane == 2 ? fz : 0.f;
+        }
+      }
     }
-    if (lane == 0) for (int i = 0; i < dim; i++) out[i] = 0.f;
-    if (sel >= 0 && lane == sel) {
-      const float sg = a1 ? 1.f : -1.f;
-      if (bits & 1) out[0] = found;
-      else if (bits & 8) out[0] = dist;
-      else if (bits & 16) { for (int t = 0; t < 3; t++) out[t] = S[L.con_pos + 3 * c + t]; }
-      else if (bits & 32) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + t]; }
-      else if (bits & 64) { for (int t = 0; t < 3; t++) out[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
-      else if (bits & 2) { out[0] = fc.x; out[1] = fc.y; out[2] = fc.z; }
-    }
+    if (lane < dim) out[lane] = v;
   }
 }
 
