@@ -1139,7 +1139,21 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     dadr = m.sensor_adr[s];
     ddim = m.sensor_dim[s];
   }
-  for (int k = 0; k < ncs; k++) {
+  // found-only sensors (data = found, one slot: Go1's 26 non-foot touch sensors): the count
+  // of matching contacts is the output whatever the reduce, so each costs one ballot and
+  // popcount kept in its own lane, and all of them go out in one store at the end
+  const bool fonly = lane < ncs && dbits == 1 && ddim == 1;
+  const uint64_t mm = m1 | m2;
+  float fcount = 0.f;
+  uint64_t rest = __ballot(lane < ncs && !fonly);
+  for (uint64_t fo = __ballot(fonly); fo; fo &= fo - 1) {
+    const int k = __ffsll((long long)fo) - 1;
+    const float f = (float)__popcll(__ballot((mm >> k) & 1ull));
+    fcount = lane == k ? f : fcount;
+  }
+  if (fonly) sd[dadr] = fcount;
+  for (; rest; rest &= rest - 1) {
+    const int k = __ffsll((long long)rest) - 1;
     const int bits = __builtin_amdgcn_readlane(dbits, k), reduce = __builtin_amdgcn_readlane(dred, k);
     const int adr = __builtin_amdgcn_readlane(dadr, k), dim = __builtin_amdgcn_readlane(ddim, k);
     float* out = sd + adr;
