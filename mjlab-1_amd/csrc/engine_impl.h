@@ -2135,21 +2135,25 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
           Si[L.efc_cid + r0 + k] = efc_code(cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, lane);
       }
       sync();
-      // Jacobian rows: lane per dof
-      for (int i = lane; i < nvp; i += kWave) {
+      // Jacobian rows: lane per dof; when nvp <= 32 the wave holds kWave / nvp groups of nvp
+      // lanes that take every ngrp-th row / contact (Go1, nvp 20: 3 contacts at once instead
+      // of 20 active lanes of 64)
+      const int ngrp = nvp <= kWave / 2 ? kWave / nvp : 1;
+      const int grp = lane / nvp;
+      for (int i = lane - grp * nvp; grp < ngrp && i < nvp; i += kWave) {
         // limits
-        for (int r = 0; r < lim_total && r < nefc; r++) {
+        for (int r = grp; r < lim_total && r < nefc; r += ngrp) {
           const int jd = Si[L.efc_cid + r] >> 2;
           Jg[r * nvp + i] = (jd >> 8) == i ? S[L.efc_D + r] : 0.f;
         }
         if (i >= nv) {  // zero padding columns of the contact rows
-          for (int r = lim_total; r < nefc; r++) Jg[r * nvp + i] = 0.f;
+          for (int r = lim_total + grp; r < nefc; r += ngrp) Jg[r * nvp + i] = 0.f;
           continue;
         }
         uint64_t bm = m.dof_bodymask[i];
         const float* cd = S + L.cdof + 6 * i;
         V3 cang = v3(cd), clin = v3(cd + 3);
-        for (int c = 0; c < ncon; c++) {
+        for (int c = grp; c < ncon; c += ngrp) {
           const int cb = Si[L.con_key + c];
           const int b1 = cb_b1(cb), b2 = cb_b2(cb);
           V3 pos = v3(S + L.con_pos + 3 * c);
