@@ -723,9 +723,16 @@ int mjx_expand_field(mjxSim* s, const char* cname, void* stream) {
   int ws = 0;
   const float* cur = (const float*)model_field_ptr(s, name, &ws);
   if (ws > 0) return fail("field '" + name + "' already expanded");
-  for (int w = 0; w < s->nworld; w++)
-    HIPCHK(hipMemcpyAsync(buf + (size_t)w * per, cur, sizeof(float) * per, hipMemcpyDeviceToDevice,
+  // world 0 from the model, then doubling copies of the filled prefix: ceil(log2 N) + 1
+  // copies instead of one per world (8,192 copy dispatches for Go1 at sim creation)
+  if (s->nworld > 0)
+    HIPCHK(hipMemcpyAsync(buf, cur, sizeof(float) * per, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  for (size_t done = 1; done < (size_t)s->nworld;) {
+    const size_t n = std::min(done, (size_t)s->nworld - done);
+    HIPCHK(hipMemcpyAsync(buf + done * per, buf, sizeof(float) * per * n, hipMemcpyDeviceToDevice,
                           (hipStream_t)stream));
+    done += n;
+  }
 #define X_FLT(n, cnt, w) if (name == #n) { s->dm.n = buf; s->dm.n##_ws = (int)per; }
   MJX_MODEL_FLOAT_FIELDS(X_FLT)
 #undef X_FLT
