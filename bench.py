@@ -11,16 +11,21 @@ Workload semantics follow the reference's scripts/benchmarks/measure_throughput.
     `--mode physics` times decimation x Simulation.step only (measure_physics_sps).
 Actions are uniform[-1,1) from a torch Generator seeded 0 (scripts/play.py:173-176).
 
-roofline: dominant kernel = one Simulation.step launch group (step_phase<NR,0|1|2>, the
-three phases of one substep); algorithmic bytes per env-step
-B_env = 4*[dec*(2nq+5nv+2nu+ns+1) + 16*nbody + 72], per launch
-B_env/dec per world; achieved = bytes/launch / mean launch time (HIP events on the
-launch stream); peak 8 TB/s (MI355X_MICROARCH.md).  `traffic` = HBM bytes per launch from
-the committed PMC measurements profiles/*_hbm_traffic.json (FETCH_SIZE x2 + WRITE_SIZE,
-separate rocprofv3 passes, scripts/profile_round.sh) when one was taken on this task /
-num_envs / nv (latest round first), else null.
-cpu_baseline: the fp64 CPU oracle (oracle/liboracle.so, "port"), OpenMP over worlds on
-the box's host cores, bounded sample.
+roofline: the dominant "kernel" is one env step exactly as the timed region runs it (the
+HIP graph of decimation x physics phases A/B/C + the fused manager kernels); algorithmic
+bytes per env-step B_env = 4*[dec*(2nq+5nv+2nu+ns+1) + 16*nbody + 72] (SURVEY.md section
+8d) x num_envs per launch; achieved = bytes / mean launch time (HIP event pairs around
+`--launch-reps` further steps, on the stream the graph is replayed on); peak 8 TB/s
+(MI355X_MICROARCH.md).  `traffic` = HBM bytes per env step of the same captured step from
+the committed PMC measurement profiles/*_hbm_traffic.json (FETCH_SIZE x2 + WRITE_SIZE,
+separate rocprofv3 passes over bench.py itself, scripts/profile_round.sh) when one was
+taken on this task / num_envs / nv, else null.  `bound` is the larger of the HBM and MFMA
+fractions.
+overflow: contact/row overflow events counted by the engine over the timed steps (dropped
+contact work); non-zero makes the run exit 3 after printing the line (--allow-overflow).
+cpu_baseline: the fp64 CPU oracle (oracle/liboracle.so, "port") on the allotted host cores
+over the bench's own worlds with random actions, plus config 1 (num_envs=1, zero action,
+one thread).
 """
 
 from __future__ import annotations
@@ -46,7 +51,104 @@ def b_env(m, dec):
   return 4 * (dec * (2 * m.nq + 5 * m.nv + 2 * m.nu + m.nsensordata + 1) + 16 * m.nbody + 72)
 
 
-def measured_traffic(task, num_envs, nv):
+def cpu_threads():
+  """Host threads for the CPU leg: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
+  share), else every core of the affinity mask."""
+  aff = len(os.sched_getaffinity(0))
+  t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+  return (t if t > 0 else aff), aff
+
+
+def cgroup_cpus():
+  try:
+    with open("/sys/fs/cgroup/cpu.max") as fh:
+      q, p = fh.read().split()[:2]
+    return None if q == "max" else float(q) / float(p)
+  except (OSError, ValueError):
+    return None
+
+
+def ctrl_affine(env):
+  """ctrl = A @ action + b for world 0, probed through the env's own action path
+  (JointPositionAction: a * scale + offset - encoder_bias, then the actuator order of
+  write_ctrl; managers/action_manager.py:113-130, entity/data.py:168-180)."""
+  nact = env.action_manager.total_action_dim
+  n = env.num_envs
+
+  def ctrl_of(a):
+    env.action_manager.process_action(a)
+    env.action_manager.apply_action()
+    env.scene.write_data_to_sim()
+    torch.cuda.synchronize()
+    return env.sim.data.ctrl[0].double().cpu().numpy().copy()
+
+  z = torch.zeros(n, nact, device=env.device)
+  b = ctrl_of(z)
+  A = np.zeros((b.size, nact))
+  for k in range(nact):
+    e = z.clone()
+    e[:, k] = 1.0
+    A[:, k] = ctrl_of(e) - b
+  return A, b
+
+
+def cpu_baseline(env, dec, budget_s=12.0, config1_s=4.0):
+  """The fp64 CPU oracle ("port") on the box's host cores, physics only (decimation x
+  mj_step per env step; the managers are not included):
+    - the bench's own worlds: the first <= 4096 worlds' states as the timed region left
+      them, a new uniform[-1, 1) action per env step mapped through the action scale and
+      offset (ctrl_affine), OpenMP over worlds on every allotted core;
+    - config 1 (BASELINE.json): num_envs = 1, zero actions (`--agent zero`), one thread,
+      from the init keyframe."""
+  import oracle_lib as ol
+  m = env.sim.mj_model
+  threads, aff = cpu_threads()
+  A, b = ctrl_affine(env)
+  nact = A.shape[1]
+  nw = min(4096, env.num_envs)
+  d = env.sim.data
+  f64 = lambda t: np.ascontiguousarray(t[:nw].double().cpu().numpy())
+  q, qv, qws, tm = f64(d.qpos), f64(d.qvel), f64(d.qacc_warmstart), f64(d.time).reshape(nw)
+  rng = np.random.default_rng(0)
+
+  def env_step():
+    a = rng.uniform(-1.0, 1.0, (nw, nact))
+    ctrl = np.ascontiguousarray(a @ A.T + b)
+    ol.rollout(m, q, qv, qws, ctrl, tm, dec, nthreads=threads, outputs=False)
+
+  t0 = time.perf_counter()
+  env_step()
+  one = max(time.perf_counter() - t0, 1e-4)
+  nsteps = int(max(3, min(200, budget_s / one)))
+  t0 = time.perf_counter()
+  for _ in range(nsteps):
+    env_step()
+  el = time.perf_counter() - t0
+  # config 1: one world, zero action, single thread
+  q1 = np.ascontiguousarray(m.key_qpos.reshape(1, -1), dtype=np.float64)
+  v1, w1, t1 = np.zeros((1, m.nv)), np.zeros((1, m.nv)), np.zeros(1)
+  c1 = np.ascontiguousarray(b.reshape(1, -1))
+  t0 = time.perf_counter()
+  ol.rollout(m, q1, v1, w1, c1, t1, 50 * dec, nthreads=1, outputs=False)
+  one1 = max((time.perf_counter() - t0) / 50, 1e-6)
+  n1 = int(max(50, min(200000, config1_s / one1)))
+  t0 = time.perf_counter()
+  ol.rollout(m, q1, v1, w1, c1, t1, n1 * dec, nthreads=1, outputs=False)
+  el1 = time.perf_counter() - t0
+  return {"value": nw * nsteps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+          "sample": f"{nw} of the bench's worlds (states as the timed region left them) x "
+                    f"{nsteps} env-steps ({dec} substeps each), new uniform[-1,1) actions per "
+                    "env step through the action scale/offset, fp64 oracle, physics only",
+          "host_cores_visible": aff, "cgroup_cpus": cgroup_cpus(),
+          "config1": {"value": n1 / el1, "unit": "env-steps/s", "cores": 1, "num_envs": 1,
+                      "sample": f"1 world x {n1} env-steps from the init keyframe, zero action "
+                                "(--agent zero), single thread, fp64 oracle, physics only"}}
+
+
+def traffic_profile(task, num_envs, nv):
+  """Measured HBM traffic per captured env step (profiles/*_hbm_traffic.json taken by
+  scripts/profile_round.sh on this task / num_envs / nv with the env-step graph path),
+  latest round first."""
   import glob
   for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")), reverse=True):
     try:
@@ -54,37 +156,12 @@ def measured_traffic(task, num_envs, nv):
         t = json.load(fh)
     except (OSError, ValueError):
       continue
-    if (t.get("task"), t.get("num_envs"), t.get("nv")) == (task, num_envs, nv):
-      return float(t["traffic_bytes_per_launch"])
-  return None
+    if (t.get("task"), t.get("num_envs"), t.get("nv"), t.get("path")) == (task, num_envs, nv, "env_step_graph"):
+      return t, os.path.relpath(path, ROOT)
+  return None, None
 
 
-def cpu_baseline(model, dec, budget_s=12.0):
-  """Time the fp64 CPU oracle on a bounded sample of the same workload."""
-  import oracle_lib as ol
-  threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-  if threads <= 0:
-    threads = len(os.sched_getaffinity(0))
-  threads = max(1, min(threads, 16))
-  nw = 8 * threads
-  rng = np.random.default_rng(0)
-  q = np.tile(model.key_qpos, (nw, 1)).astype(np.float64)
-  qv = np.zeros((nw, model.nv))
-  qws = np.zeros((nw, model.nv))
-  jq = np.array([model.jnt_qposadr[j] for j in model.actuator_trnid])
-  ctrl = q[:, jq] + 0.1 * rng.uniform(-1, 1, (nw, model.nu))
-  tm = np.zeros(nw)
-  # calibrate with one env step, then run for ~budget_s
-  t0 = time.perf_counter()
-  ol.rollout(model, q, qv, qws, ctrl, tm, dec, nthreads=threads, outputs=False)
-  one = max(time.perf_counter() - t0, 1e-4)
-  nsteps = int(max(1, min(200, budget_s / one)))
-  t0 = time.perf_counter()
-  ol.rollout(model, q, qv, qws, ctrl, tm, nsteps * dec, nthreads=threads, outputs=False)
-  el = time.perf_counter() - t0
-  return {"value": nw * nsteps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-          "sample": f"{nw} worlds x {nsteps} env-steps ({dec} substeps each), G1 velocity "
-                    f"scene, PD hold of the init keyframe + U(-0.1,0.1) ctrl noise, fp64 oracle"}
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md: Peak FP32 (matrix))
 
 
 def main():
@@ -97,6 +174,10 @@ def main():
   ap.add_argument("--mode", choices=["env", "physics"], default="env")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--eager", action="store_true", help="reference-style eager env.step (host syncs)")
+  ap.add_argument("--launch-reps", type=int, default=20,
+                  help="env steps timed one by one with HIP events after the timed region")
+  ap.add_argument("--allow-overflow", action="store_true",
+                  help="exit 0 even if contacts were dropped in the timed steps")
   args = ap.parse_args()
 
   from mjlab_amd import distributed as mjdist
@@ -110,7 +191,8 @@ def main():
 
   from mjlab_amd.envs import make_env
   env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
-  m = env.sim.mj_model
+  sim = env.sim
+  m = sim.mj_model
   dec = env.cfg.decimation
   gen = torch.Generator(device=device)
   gen.manual_seed(0 + rank)
@@ -119,8 +201,10 @@ def main():
   if args.mode == "env" and not args.eager:
     env.enable_graph(capture=True)
 
-  def one_step():
-    a = 2.0 * torch.rand((args.num_envs, nact), device=device, generator=gen) - 1.0
+  def draw():
+    return 2.0 * torch.rand((args.num_envs, nact), device=device, generator=gen) - 1.0
+
+  def one_step(a):
     if args.mode == "env":
       env.step(a)
     else:
@@ -128,27 +212,43 @@ def main():
       for _ in range(dec):
         env.action_manager.apply_action()
         env.scene.write_data_to_sim()
-        env.sim.step()
+        sim.step()
 
   for _ in range(args.warmup):
-    one_step()
+    one_step(draw())
+  ev_before = sim.overflow_events().clone()
+  sim.marker(1)  # kernel-trace bracket (outside the timing: it completes before t0)
+  torch.cuda.synchronize()
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for _ in range(args.steps):
-    one_step()
+    one_step(draw())
   torch.cuda.synchronize()
   if dist is not None:
     dist.barrier()
   el = time.perf_counter() - t0
-  # Step-kernel launch duration for the roofline: HIP events around individual
-  # Simulation.step launches (the timed env steps run inside a HIP graph).
-  env.sim.timing_begin()
-  for _ in range(10):
-    env.scene.write_data_to_sim()
-    env.sim.step()
-  launch_ms = env.sim.timing_end()
+  sim.marker(2)
+  # contacts dropped in the timed steps (a world whose contacts or rows overflow its LDS
+  # capacity drops whole contacts; the engine counts the events every substep)
+  dropped = (sim.overflow_events() - ev_before).cpu().tolist()
+  # the dominant "kernel" is one env step as the timed region ran it (the captured HIP
+  # graph of physics + fused managers): HIP events around each of `launch_reps` further
+  # steps on the stream they are launched on (torch's current stream; graph replays and
+  # the engine's launches both go there)
+  stream = torch.cuda.current_stream()
+  acts = [draw() for _ in range(args.launch_reps)]
+  pairs = []
+  for a in acts:
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    one_step(a)
+    e1.record(stream)
+    pairs.append((e0, e1))
+  torch.cuda.synchronize()
+  launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in pairs]))
+  st = sim.stats()
   if dist is not None:
     el = mjdist.max_over_ranks(el, device)
     # episode statistics: one packed all-gather over RCCL
@@ -157,36 +257,55 @@ def main():
   total = args.steps * args.num_envs * world
   value = total / el
   if rank == 0:
-    bytes_launch = b_env(m, dec) / dec * args.num_envs
-    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic = measured_traffic(args.task, args.num_envs, m.nv)
+    ms_step = el / args.steps * 1e3
+    bytes_launch = b_env(m, dec) * args.num_envs
+    launch_s = launch_ms * 1e-3
+    achieved = bytes_launch / launch_s / 1e9
+    graph_path = args.mode == "env" and not args.eager
+    prof, prof_path = traffic_profile(args.task, args.num_envs, m.nv) if graph_path else (None, None)
+    traffic = float(prof["traffic_bytes_per_env_step"]) if prof else None
+    traffic_gbps = traffic / launch_s / 1e9 if traffic else None
+    mfma_flops = float(prof.get("mfma_flops_per_env_step", 0.0)) if prof else 0.0
+    frac_hbm = max(achieved, traffic_gbps or 0.0) / HBM_PEAK_GBS
+    frac_mfma = mfma_flops / launch_s / 1e12 / MFMA_F32_PEAK_TFLOPS
+    bound = "hbm" if frac_hbm >= frac_mfma else "mfma"
+    step_path = ("eager" if not graph_path else "sync-free, HIP-graph captured" +
+                 (", fused HIP managers" if getattr(env, "_fused", None) is not None else ""))
     out = {
       "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
-      "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+      "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
       "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
       "data": "synthetic (random-init state from the compiled G1 MJCF; uniform random actions)",
       "config": {"workload": f"{args.task} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
                  "task": args.task, "num_envs_per_gpu": args.num_envs, "decimation": dec,
-                 "parallelism": f"dp{world}", "mode": args.mode,
-                 "step_path": ("eager" if (args.eager or args.mode != "env") else
-                               "sync-free, HIP-graph captured" +
-                               (", fused HIP managers" if getattr(env, "_fused", None) is not None else ""))},
-      "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": achieved / HBM_PEAK_GBS,
-                   "traffic": traffic,
-                   "kernel": "mjx::step_phase<NR,0|1|2> (one Simulation.step)", "launch_ms": launch_ms,
+                 "parallelism": f"dp{world}", "mode": args.mode, "step_path": step_path,
+                 "capacity": {"contacts_per_world": sim.nconmax, "rows_per_world": sim.njmax,
+                              "asked": {"nconmax": env.cfg.sim.nconmax, "njmax": env.cfg.sim.njmax}}},
+      "overflow": {"timed_steps": args.steps, "contact_overflow_events": int(dropped[0]),
+                   "row_overflow_events": int(dropped[1]), "unsupported_pair_events": int(dropped[2]),
+                   "max_contacts_seen": st["max_ncon"], "max_rows_seen": st["max_nefc"]},
+      "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                   "kernel": f"one env step ({step_path}; {dec} substeps x phases A/B/C"
+                             + (" + the fused manager kernels" if graph_path else "") + ")",
+                   "launch_ms": launch_ms, "launch_reps": args.launch_reps,
                    "bytes_per_launch": bytes_launch,
-                   # the HBM roofline is the north star's pricing; what actually bounds the
-                   # kernel is per-world dependency latency and VALU issue,
-                   # as the measured traffic rate next to the peak shows
-                   "limiter": "latency/VALU issue (not HBM)",
-                   "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9
-                                    if traffic is not None and launch_ms > 0 else None)},
+                   "bytes_per_env": b_env(m, dec),
+                   "traffic_gbps": traffic_gbps, "traffic_profile": prof_path,
+                   "frac_hbm_measured_traffic": (traffic_gbps / HBM_PEAK_GBS) if traffic_gbps else None,
+                   "frac_mfma": frac_mfma, "mfma_flops_per_launch": mfma_flops,
+                   # what actually bounds the step: per-world dependency latency and issue
+                   # (SQ counters in the profile), DESIGN.md section 3
+                   "limiter": (prof or {}).get("limiter", "latency/VALU issue (not HBM)")},
       "cpu_baseline": None,
     }
     if not args.no_cpu_baseline and world == 1:
-      out["cpu_baseline"] = cpu_baseline(m, dec)
+      out["cpu_baseline"] = cpu_baseline(env, dec)
     print(json.dumps(out))
+    if any(dropped) and not args.allow_overflow:
+      print(f"bench.py: contacts were dropped in the timed steps (overflow events {dropped}); "
+            "the line above reports them", file=sys.stderr)
+      sys.exit(3)
   if dist is not None:
     dist.destroy_process_group()
 

@@ -164,6 +164,11 @@ int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
  * kernels; -1 for a null sim.  No reference counterpart (mujoco_warp specialises by
  * tracing Python at graph-capture time, sim/sim.py:164-191). */
 int mjx_sim_spec(const mjxSim* sim);
+/* Diagnostics: enqueue one empty kernel (`mjx::marker_kernel`, one wave, argument `tag`) on
+ * `stream`.  bench.py brackets its timed region with tags 1 and 2 outside the timing, so a
+ * rocprofv3 kernel trace or --pmc pass of the same command can attribute exactly the
+ * timed steps' dispatches.  No reference counterpart. */
+int mjx_marker(int tag, void* stream);
 
 #ifdef __cplusplus
 }

@@ -89,10 +89,12 @@ struct mjxSim_ {
   int spec = 0;  // model specialisation in use (mjx::find_spec), 0 = generic kernels
   mjx::SideStream side{};  // streams of the Newton row classes (when classes are used)
   ~mjxSim_() {
-    if (side.fork) (void)hipEventDestroy(side.fork);
-    for (int k = 0; k < mjx::kRowClasses; k++) {
-      if (side.join[k]) (void)hipEventDestroy(side.join[k]);
-      if (side.stream[k]) (void)hipStreamDestroy(side.stream[k]);
+    for (int p = 0; p < mjx::kMaxSplit; p++) {
+      if (side.fork[p]) (void)hipEventDestroy(side.fork[p]);
+      for (int k = 0; k < mjx::kRowClasses; k++) {
+        if (side.join[p][k]) (void)hipEventDestroy(side.join[p][k]);
+        if (side.stream[p][k]) (void)hipStreamDestroy(side.stream[p][k]);
+      }
     }
     for (int p = 0; p < mjx::kMaxSplit; p++) {
       if (side.split[p]) (void)hipStreamDestroy(side.split[p]);
@@ -456,10 +458,10 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
     s->lds_ph[3 + k] = mjx::make_lds(ds, 1);
   }
   // batch splits (launch_step): large batches of models without row classes run as
-  // concurrent halves.  MJX355_SPLIT=<n> overrides (diagnostic; 1 = one launch set per phase).
+  // concurrent halves.  MJX355_SPLIT=<n> overrides (diagnostic; 1 = one launch set per phase),
+  // also for models with row classes (each split then forks its own class streams).
   s->side.nsplit = nworld >= mjx::kSplitMinWorlds && s->nrowclass == 0 ? 2 : 1;
   if (const char* ev = getenv("MJX355_SPLIT")) s->side.nsplit = std::max(1, std::min(atoi(ev), mjx::kMaxSplit));
-  if (s->nrowclass > 0) s->side.nsplit = 1;
   {
     hipError_t e = hipSuccess;
     if (s->side.nsplit > 1) {
@@ -471,11 +473,11 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
     }
     // default priority: measured, high-priority side streams let the few heavy worlds hold
     // LDS that the bulk of small-class worlds needs (Newton span 214 -> 281 us, G1 4096)
-    if (s->nrowclass > 0 && e == hipSuccess) {
-      e = hipEventCreateWithFlags(&s->side.fork, hipEventDisableTiming);
+    for (int p = 0; p < s->side.nsplit && s->nrowclass > 0 && e == hipSuccess; p++) {
+      e = hipEventCreateWithFlags(&s->side.fork[p], hipEventDisableTiming);
       for (int k = 0; k < s->nrowclass && e == hipSuccess; k++) {
-        e = hipStreamCreateWithFlags(&s->side.stream[k], hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[k], hipEventDisableTiming);
+        e = hipStreamCreateWithFlags(&s->side.stream[p][k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[p][k], hipEventDisableTiming);
       }
     }
     if (e != hipSuccess) { delete s; return fail(std::string("side streams: ") + hipGetErrorString(e)); }
@@ -747,6 +749,12 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
 }
 
 int mjx_sim_spec(const mjxSim* s) { return s ? s->spec : -1; }
+
+int mjx_marker(int tag, void* stream) {
+  hipError_t e = mjx::launch_marker(tag, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(std::string("marker launch: ") + hipGetErrorString(e));
+  return 0;
+}
 
 int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {
   if (!s || !out) return fail("null argument");

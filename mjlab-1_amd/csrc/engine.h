@@ -167,13 +167,15 @@ struct Params {
 // `host`; `host` is used only for the launch geometry.
 hipError_t prepare_step(const Params& host);  // one-time kernel attributes (not capturable)
 // Side streams for the Newton row classes beyond the first: forked from and joined back
-// into the launch stream every substep (graph-capturable fork/join).
-// With the batch split (nsplit > 1; models without row classes), split k > 0 runs on
-// split[k], forked from the launch stream before the first substep and joined back after
-// the last.
+// into the split's stream every substep (graph-capturable fork/join).
+// With the batch split (nsplit > 1), split k > 0 runs on split[k], forked from the launch
+// stream before the first substep and joined back after the last.  Every split owns its
+// class streams and fork / join events, so the captured dependency graph is a tree of
+// per-split fork/join diamonds (class streams shared by two splits made a capture whose
+// side streams joined two origin streams, and hipStreamEndCapture crashed on it).
 struct SideStream {
-  hipStream_t stream[kRowClasses];
-  hipEvent_t fork, join[kRowClasses];
+  hipStream_t stream[kMaxSplit][kRowClasses];
+  hipEvent_t fork[kMaxSplit], join[kMaxSplit][kRowClasses];
   int nsplit;                        // batch splits in use (1 = one launch set per phase)
   hipStream_t split[kMaxSplit];      // [0] unused: split 0 runs on the launch stream
   hipEvent_t split_fork, split_join[kMaxSplit];
@@ -185,5 +187,6 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
 int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
                         int nworld, hipStream_t stream);
+hipError_t launch_marker(int tag, hipStream_t stream);  // empty kernel (profiling brackets)
 
 }  // namespace mjx

@@ -196,14 +196,13 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   const StepFn fA = step_fn(host, 0), fB = step_fn(host, 1), fC = step_fn(host, 2);
   const int nc = host.nrowclass;
   if (nc > 0 && !side) return hipErrorInvalidValue;
-  // Batch split (models without Newton row classes): the worlds in nsplit contiguous ranges,
-  // each range's A -> B -> C chain on its own stream.  The ranges are independent, so one
-  // range's launches fill the tail of the other's (the last, partly filled round of
-  // workgroups per CU) and the launch gaps.  Measured: Go1 8192 worlds 4.91 -> 5.61 M
-  // env-steps/s at 2 splits (3: 5.47, 4: 5.38).  With row classes the split buys ~1 % (G1,
-  // eager) and its nested class fork/join crashes HIP graph capture, so it is not used there;
-  // masked forwards (reset worlds) stay one launch set.
-  const int nsplit = (!mask && side && nc == 0) ? std::max(1, std::min(side->nsplit, kMaxSplit)) : 1;
+  // Batch split: the worlds in nsplit contiguous ranges, each range's A -> B -> C chain on
+  // its own stream.  The ranges are independent, so one range's launches fill the tail of
+  // the other's (the last, partly filled round of workgroups per CU) and the launch gaps.
+  // Measured: Go1 8192 worlds 4.91 -> 5.61 M env-steps/s at 2 splits (3: 5.47, 4: 5.38).
+  // With row classes each split forks its own class streams (SideStream); the default for
+  // those models is one split (capi.cpp).  Masked forwards (reset worlds) stay one launch set.
+  const int nsplit = (!mask && side) ? std::max(1, std::min(side->nsplit, kMaxSplit)) : 1;
   hipStream_t sst[kMaxSplit];
   int wb[kMaxSplit + 1];
   for (int k = 0; k <= nsplit; k++) wb[k] = (int)(((long long)nworld * k) / nsplit);
@@ -249,7 +248,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         // classes on further side streams, the smallest (most worlds) on the launch stream.
         // Measured: forking the side classes after the smallest makes the full class the tail
         // (B span 240 -> 255 us, G1).
-        e = hipEventRecord(side->fork, st);
+        e = hipEventRecord(side->fork[k], st);
         if (e != hipSuccess) return e;
         // class c's stream: B, then (piped) C and the next substep's A of the same worlds
         auto class_chain = [&](hipStream_t cs, int cls) {
@@ -264,14 +263,14 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         };
         for (int c = 0; c < nc; c++) {
           const int cls = c == 0 ? 0 : nc + 1 - c;  // 0, then nc, nc-1, ..., 2
-          e = hipStreamWaitEvent(side->stream[c], side->fork, 0);
+          e = hipStreamWaitEvent(side->stream[k][c], side->fork[k], 0);
           if (e != hipSuccess) return e;
-          class_chain(side->stream[c], cls);
+          class_chain(side->stream[k][c], cls);
         }
         class_chain(st, 1);
         for (int c = 0; c < nc; c++) {
-          e = hipEventRecord(side->join[c], side->stream[c]);
-          if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[c], 0);
+          e = hipEventRecord(side->join[k][c], side->stream[k][c]);
+          if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[k][c], 0);
           if (e != hipSuccess) return e;
         }
         if (piped) continue;
@@ -334,6 +333,17 @@ int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
     if (r > 0 && (n == 0 || r > caps[n - 1]) && n < kRowClasses) caps[n++] = r;
   }
   return n;
+}
+
+// Profiling marker: an empty one-wave kernel whose dispatches bracket a region of interest
+// in a kernel trace (mjx_marker; the argument is the tag, visible in the trace only by order).
+__global__ void marker_kernel(int tag) {
+  (void)tag;
+}
+
+hipError_t launch_marker(int tag, hipStream_t stream) {
+  hipLaunchKernelGGL(marker_kernel, dim3(1), dim3(kWave), 0, stream, tag);
+  return hipGetLastError();
 }
 
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,

@@ -2872,14 +2872,16 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         D.contact_force[(wc + c) * 3 + 1] = f.y;
         D.contact_force[(wc + c) * 3 + 2] = f.z;
       }
-      if (lane < 6) {  // per-world counters: [0,1,5] running max, [2..4] event counts
-        int* ws = D.wstats + 8 * (size_t)w;
-        const int v = lane == 0 ? ints[0] : lane == 1 ? nefc : lane == 5 ? niter_last
-                    : (ints[3] >> (lane - 2)) & 1;
-        const int old = ws[lane];
-        ws[lane] = (lane >= 2 && lane <= 4) ? old + v : max(old, v);
-        if (lane >= 2 && lane <= 4 && v) atomicAdd(D.evtotal + lane - 2, v);
-      }
+    }
+    // per-world counters, every substep (a fused multi-substep step must not lose the
+    // overflow events of its earlier substeps): [0,1,5] running max, [2..4] event counts
+    if (lane < 6) {
+      int* ws = D.wstats + 8 * (size_t)w;
+      const int v = lane == 0 ? ints[0] : lane == 1 ? nefc : lane == 5 ? niter_last
+                  : (ints[3] >> (lane - 2)) & 1;
+      const int old = ws[lane];
+      ws[lane] = (lane >= 2 && lane <= 4) ? old + v : max(old, v);
+      if (lane >= 2 && lane <= 4 && v) atomicAdd(D.evtotal + lane - 2, v);
     }
     STAMP(12);
 #ifdef MJX_STAMPS

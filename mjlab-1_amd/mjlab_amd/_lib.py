@@ -19,7 +19,7 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
            "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile", "mjx_sim_spec",
-           "mjx_forward_masked", "mjx_sim_track_air_time",
+           "mjx_forward_masked", "mjx_sim_track_air_time", "mjx_marker",
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
@@ -65,6 +65,8 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_spec.argtypes = [vp]
   L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
+  if hasattr(L, "mjx_marker"):
+    L.mjx_marker.argtypes = [ci, vp]
   if hasattr(L, "mjx_terrain_levels"):
     f32, u64 = ctypes.c_float, ctypes.c_uint64
     L.mjx_terrain_levels.argtypes = [ci, vp, vp, ci, ci, vp, f32, f32, vp, vp, vp, ci, ci, vp, u64,

@@ -230,6 +230,14 @@ def _geom_inertia(attrs: dict, xml: XModel):
 def _inertial_from_geoms(b: XBody, xml: XModel):
   """MuJoCo's inertiafromgeom: the body's mass, centre of mass and principal inertia from
   its geoms (parallel-axis sum about the com, eigen-decomposed into ipos / iquat / diag)."""
+  for x in b.geoms:
+    # MuJoCo includes a mesh's volume; without the mesh this compiler cannot, and dropping
+    # the geom would give silently wrong dynamics
+    if x.attrs.get("type") == "mesh" and (float(x.attrs.get("mass", 0.0)) > 0.0 or
+                                          float(x.attrs.get("density", 1000.0)) > 0.0):
+      raise NotImplementedError(
+        f"body '{b.name}': inertia from geoms needs the volume of mesh geom "
+        f"'{x.attrs.get('name', '?')}' (nonzero density or mass); give the body an <inertial>")
   parts = [g for g in (_geom_inertia(x.attrs, xml) for x in b.geoms) if g is not None and g[0] > 0]
   if not parts:
     return None

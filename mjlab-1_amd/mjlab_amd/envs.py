@@ -243,6 +243,8 @@ class ManagerBasedRlEnv:
       return
     self.sync_free = True
     self._use_graph = capture
+    if self._fused is not None and hasattr(self._fused, "release"):
+      self._fused.release()  # the engine stops owning the contact air-time buffers
     self._fused = None
     if fused and os.environ.get("MJX355_FUSED", "1") != "0":
       from .fused import FusedJumpStep, FusedVelocityStep

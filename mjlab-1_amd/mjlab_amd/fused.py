@@ -545,7 +545,22 @@ class FusedVelocityStep:
       _need(air[k].is_contiguous() and air[k].dtype == torch.float32, "air-time buffers")
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
     check(tl.mjx_sim_track_air_time(sim._sim, d.nfeet, adr, *ptrs, stream))
+    self._feet_sensor.engine_owned = True
     return True
+
+  def release(self) -> None:
+    """Hand the air-time buffers back to the torch ContactSensor.update path: the engine
+    stops updating them (n = 0).  Called when the env drops or replaces this fused step
+    (enable_graph); without it a later torch-manager step would advance air time twice per
+    substep."""
+    if not getattr(self, "_engine_air", False):
+      return
+    sim = self.env.sim
+    if getattr(sim, "_sim", None) is not None and sim._sim.value:
+      stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
+      check(lib().mjx_sim_track_air_time(sim._sim, 0, None, None, None, None, None, None, stream))
+    self._feet_sensor.engine_owned = False
+    self._engine_air = False
 
   # ------------------------------------------------------------------ device handle
   def upload(self):
@@ -563,6 +578,10 @@ class FusedVelocityStep:
     self._task = h
 
   def __del__(self):
+    try:
+      self.release()
+    except Exception:
+      pass
     try:
       if self._task is not None:
         self._L.mjx_task_destroy(self._task)

@@ -684,7 +684,9 @@ def _terrain_levels_vel_masked(env, mask, command_name: str, asset_cfg=None):
   terrain = env.scene.terrain
   name = asset_cfg.name if asset_cfg else "robot"
   cmd = env.command_manager.get_command(command_name)
-  if terrain.env_origins.is_cuda and cmd.is_contiguous() and cmd.dtype == torch.float32:
+  # the kernel reads the command rows with a stride of 3 (lin_x, lin_y, ang_z)
+  if (terrain.env_origins.is_cuda and cmd.is_contiguous() and cmd.dtype == torch.float32
+      and cmd.dim() == 2 and cmd.shape[1] == 3):
     root = int(env.scene[name].indexing.root_body_id)
     terrain.update_env_origins_native(mask.contiguous(), env.sim.data.xpos, root, cmd,
                                       env.max_episode_length_s)

@@ -184,8 +184,10 @@ class RolloutStorage:
     actions, values, returns = flat(self.actions), flat(self.values), flat(self.returns)
     logp, adv = flat(self.actions_log_prob), flat(self.advantages)
     mu, sigma = flat(self.mu), flat(self.sigma)
+    # rsl_rl 3.1.0 RolloutStorage.mini_batch_generator: one permutation drawn before the
+    # epoch loop, reused by every epoch
+    idx = torch.randperm(num_mini_batches * mb, device=self.device)
     for _ in range(num_epochs):
-      idx = torch.randperm(num_mini_batches * mb, device=self.device)
       for i in range(num_mini_batches):
         b = idx[i * mb:(i + 1) * mb]
         yield ({k: v[b] for k, v in obs.items()}, actions[b], values[b], adv[b], returns[b],

@@ -473,6 +473,10 @@ _FIELD_DIM = {"found": 1, "force": 3, "torque": 3, "dist": 1, "pos": 3, "normal"
 class ContactSensor:
   """mjSENS_CONTACT group expanded per primary x field (sensor/contact_sensor.py)."""
 
+  # set while a fused env step has handed the air-time buffers to the engine
+  # (mjx_sim_track_air_time): phase C then updates them every substep
+  engine_owned = False
+
   def __init__(self, name: str, slots: list[tuple[str, str, int, int]], fields, num_slots: int,
                track_air_time: bool):
     self.name = name
@@ -534,6 +538,9 @@ class ContactSensor:
   def update(self, dt):
     if self._air is None or "found" not in self._fields:
       return
+    if self.engine_owned:
+      raise RuntimeError(f"ContactSensor '{self.name}': the engine updates the air times of this "
+                         "sensor (a fused env step owns them); release the fused step first")
     s = self._air
     found = self._extract().found
     now = self._data.time

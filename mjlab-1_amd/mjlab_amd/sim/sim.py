@@ -392,5 +392,10 @@ class Simulation:
     check(lib().mjx_sim_profile(self._sim, out, _stream_handle(self._torch_device)))
     return list(out)
 
+  def marker(self, tag: int) -> None:
+    """Enqueue the engine's empty marker kernel on the current stream (profiling brackets:
+    bench.py marks its timed region so a kernel trace can attribute those dispatches)."""
+    check(lib().mjx_marker(int(tag), _stream_handle(self._torch_device)))
+
   def field(self, name: str) -> torch.Tensor:
     return field_tensor(self._sim, name)

@@ -39,3 +39,29 @@ def oracle_step(model, q, qv, qws, ctrl, step=True, nconmax=64, njmax=160):
     outs.append(ol.forward(model, q[i], qv[i], qws[i], ctrl[i], 0.0, step=step,
                            nconmax=nconmax, njmax=njmax))
   return outs
+
+
+def expanded_fields(sim) -> list[str]:
+  """Model fields the sim holds one copy of per world (Simulation.expand_model_fields)."""
+  out = []
+  for name in sim.mj_model.arrays:
+    try:
+      t = getattr(sim.model, name)
+    except AttributeError:
+      continue
+    if t.dim() > 0 and t.shape[0] == sim.num_envs and sim.num_envs > 1 and t.stride(0) != 0:
+      out.append(name)
+  return out
+
+
+def world_model(sim, w: int, fields=None):
+  """The compiled model with world `w`'s copies of the expanded (domain-randomised) model
+  fields, for the oracle: the engine reads `base + w * stride` (sim/sim.py:226-240)."""
+  import dataclasses
+  base = sim.mj_model
+  fields = expanded_fields(sim) if fields is None else fields
+  arrays = dict(base.arrays)
+  for f in fields:
+    shape = np.asarray(base.arrays[f]).shape
+    arrays[f] = getattr(sim.model, f)[w].double().cpu().numpy().reshape(shape)
+  return dataclasses.replace(base, arrays=arrays)

@@ -99,6 +99,34 @@ def test_fused_reset_path_matches_torch(task, gpu_device):
       _close(torch.as_tensor(v, device=gpu_device).reshape(()), log_f[k].reshape(()), rtol=1e-4, atol=1e-6)
 
 
+def test_fused_release_hands_air_time_back(gpu_device):
+  """A fused step hands the feet air-time buffers to the engine (mjx_sim_track_air_time);
+  switching the env back to the torch managers must turn that off, or air time would
+  advance twice per substep (engine phase C + ContactSensor.update).  After the switch the
+  env must track air time exactly as an env that never built the fused step."""
+  task = "Mjlab-Velocity-Flat-Unitree-G1"
+  n = 64
+  et = _env(task, n, gpu_device, fused=False)
+  ef = _env(task, n, gpu_device, fused=True)
+  sensor = ef.scene["feet_ground_contact"]
+  assert sensor.engine_owned
+  with pytest.raises(RuntimeError):
+    sensor.update(0.005)
+  ef.enable_graph(capture=False, fused=False)
+  assert ef._fused is None and not sensor.engine_owned
+  g = torch.Generator(device=gpu_device).manual_seed(1)
+  nact = et.action_manager.total_action_dim
+  for _ in range(8):
+    a = 0.3 * (2 * torch.rand(n, nact, device=gpu_device, generator=g) - 1)
+    et.step(a)
+    ef.step(a)
+  torch.cuda.synchronize()
+  fs_t = et.scene["feet_ground_contact"]
+  for k in ("current_air_time", "current_contact_time", "last_air_time", "last_contact_time"):
+    _close(fs_t._air[k], sensor._air[k], atol=1e-6, rtol=0)
+  assert float(sensor._air["current_air_time"].max() + sensor._air["current_contact_time"].max()) > 0
+
+
 def test_fused_random_draws_in_range(gpu_device):
   """Command resampling and reset events from the counter-based RNG follow the configured
   ranges (velocity_env_cfg.py:120-136 command ranges; reset pose range)."""

@@ -74,6 +74,33 @@ def test_masked_forward_only_touches_masked_worlds(gpu_device):
   assert moved.tolist() == mask.tolist()
 
 
+def test_overflow_counted_on_every_fused_substep(gpu_device):
+  """The engine's per-world overflow counters (engine_counters[:, 2:5]) and the event
+  totals must count the events of every substep of a fused multi-substep step, not only
+  the last: with 8 constraint rows per world the standing G1's foot contacts overflow the
+  rows on every substep, so one step(nsubstep=4) must count what four step() calls count."""
+  from mjlab_amd.scenes import load_scene
+  from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+  m = load_scene("g1_velocity")
+  counts = []
+  for fused in (True, False):
+    sim = Simulation(16, SimulationCfg(nconmax=48, njmax=8, mujoco=MujocoCfg(
+      timestep=m.timestep, iterations=10, ls_iterations=20)), m, gpu_device)
+    _keyframe(sim, m, gpu_device, jitter=0.05)
+    ev0 = sim.overflow_events().clone()
+    if fused:
+      sim.step(nsubstep=4)
+    else:
+      for _ in range(4):
+        sim.step()
+    torch.cuda.synchronize()
+    counts.append((sim.engine_counters[:, 2:5].cpu().clone(), (sim.overflow_events() - ev0).cpu()))
+  (wf, tf), (ws, ts) = counts
+  assert int(ws[:, 1].max()) == 4, "expected a row overflow on each of the 4 substeps"
+  assert torch.equal(wf, ws)
+  assert torch.equal(tf, ts)
+
+
 def test_step_is_deterministic(gpu_device):
   outs = []
   for _ in range(2):

@@ -85,23 +85,41 @@ def test_split_bit_identical(gpu_device):
         np.testing.assert_array_equal(a[k], b[k], err_msg=f"split={split} graph={graph} field {k}")
 
 
-def test_split_ignored_with_row_classes(gpu_device):
-  """With row classes the split is not used (HIP capture of the nested class fork crashes):
-  forcing MJX355_SPLIT must still capture and replay, bit-identical to the default."""
-  from mjlab_amd.scenes import load_scene
-  n = 64
-  q, qv, ctrl = g1_states(load_scene("g1_velocity"), n, seed=22)
-  outs = []
-  for env in ({"MJX355_ROW_CLASSES": "24"}, {"MJX355_ROW_CLASSES": "24", "MJX355_SPLIT": "2"}):
-    sim = _make(env, n, gpu_device)
-    _load(sim, q, qv, ctrl)
+def _run_env(env, q, qv, ctrl, device, graph, nsub=3, reps=2):
+  sim = _make(env, q.shape[0], device)
+  _load(sim, q, qv, ctrl)
+  out = []
+  if graph:
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-      sim.step(nsubstep=2)
+      sim.step(nsubstep=nsub)
     _load(sim, q, qv, ctrl)
-    g.replay()
-    outs.append(_snap(sim))
-  for k in outs[0]:
-    np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+  for _ in range(reps):
+    if graph:
+      g.replay()
+    else:
+      sim.step(nsubstep=nsub)
+    out.append(_snap(sim))
+  return out
+
+
+@pytest.mark.parametrize("classes", ["24", "24,60"])
+def test_split_with_row_classes(classes, gpu_device):
+  """Batch split x Newton row classes (each split forks its own class streams and joins
+  them back, SideStream in engine.h): eager and HIP-graph-captured multi-substep steps,
+  split 2 and 3, bit-identical to one split.  Worlds with rows above every class capacity
+  must be present so the full-capacity class runs too."""
+  from mjlab_amd.scenes import load_scene
+  n = 131  # ragged ranges
+  q, qv, ctrl = g1_states(load_scene("g1_velocity"), n, seed=22)
+  base = _run_env({"MJX355_ROW_CLASSES": classes, "MJX355_SPLIT": "1"}, q, qv, ctrl, gpu_device, False)
+  cap = max(int(c) for c in classes.split(","))
+  assert (base[0]["nefc"] > cap).any() and (base[0]["nefc"] <= 24).any()
+  for split, graph in ((2, False), (2, True), (3, True), (1, True)):
+    got = _run_env({"MJX355_ROW_CLASSES": classes, "MJX355_SPLIT": str(split)}, q, qv, ctrl,
+                   gpu_device, graph)
+    for a, b in zip(base, got):
+      for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"split={split} graph={graph} field {k}")
