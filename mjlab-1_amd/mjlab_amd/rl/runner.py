@@ -6,6 +6,13 @@ envs (seed + rank), rank 0's parameters broadcast at start, gradients all-reduce
 
 Episode statistics stay on the device during the rollout (sums and counts of finished
 episodes); the iteration's log reads them once, together with the env's extras["log"].
+With several ranks, the rollout's statistics (finished-episode reward / length sums and
+counts, and the numeric extras["log"] entries) are packed into one fixed-size vector and
+all-gathered asynchronously on a side stream (distributed.StatsGather) while the PPO update
+runs; rank 0's record then carries the world-wide values under "world/..." (episode means
+over every rank's finished episodes, extras["log"] averaged over ranks).  rsl_rl logs rank
+0's local statistics only (docs/api/distributed_training.md:68-100); those stay in the
+record as before.
 """
 
 from __future__ import annotations
@@ -17,6 +24,7 @@ from dataclasses import asdict
 import torch
 import torch.distributed as dist
 
+from ..distributed import StatsGather
 from .config import RslRlOnPolicyRunnerCfg
 from .ppo import PPO, ActorCritic
 
@@ -51,6 +59,46 @@ class OnPolicyRunner:
     self.tot_timesteps = 0
     self.tot_time = 0.0
     self.history: list[dict] = []
+    self._gather = None
+    self._log_keys: list[str] | None = None
+
+  @staticmethod
+  def _numeric_log(log: dict) -> dict:
+    out = {}
+    for k, v in log.items():
+      if isinstance(v, torch.Tensor) and v.numel() == 1:
+        out[k] = v.reshape(())
+      elif isinstance(v, (int, float)) and not isinstance(v, bool):
+        out[k] = v
+    return out
+
+  def _start_gather(self, done_rew, done_len, done_cnt, log: dict) -> None:
+    """Pack [reward sum, length sum, episode count, extras["log"] values in a fixed key
+    order] and start the all-gather (no host sync).  The key order is fixed at the first
+    iteration (every rank runs the same task config, so the keys agree)."""
+    num = self._numeric_log(log)
+    if self._log_keys is None:
+      self._log_keys = sorted(num)
+      self._gather = StatsGather(3 + len(self._log_keys), torch.device(self.device))
+    dev = done_rew.device
+    vals = [done_rew, done_len, done_cnt]
+    for k in self._log_keys:
+      v = num.get(k, 0.0)
+      vals.append(v.to(dev, torch.float32) if isinstance(v, torch.Tensor)
+                  else torch.tensor(float(v), device=dev))
+    self._gather.start(torch.stack([v.reshape(()).float() for v in vals]))
+
+  def _finish_gather(self, rec: dict) -> None:
+    g = self._gather.wait()  # [world, 3 + nkeys]
+    if self.rank != 0:
+      return
+    g = g.double().cpu()
+    cnt = float(g[:, 2].sum())
+    rec["world/episodes"] = cnt
+    rec["world/mean_reward"] = float(g[:, 0].sum()) / cnt if cnt > 0 else None
+    rec["world/mean_episode_length"] = float(g[:, 1].sum()) / cnt if cnt > 0 else None
+    for i, k in enumerate(self._log_keys):
+      rec[f"world/{k}"] = float(g[:, 3 + i].mean())
 
   def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False) -> list[dict]:
     env, alg = self.env, self.alg
@@ -81,6 +129,9 @@ class OnPolicyRunner:
           cur_rew *= 1.0 - d
           cur_len *= 1.0 - d
         alg.compute_returns(obs)
+      log = getattr(env.unwrapped, "extras", {}).get("log", {})
+      if self.distributed:
+        self._start_gather(done_rew, done_len, done_cnt, log)  # overlaps the update
       if dev.type == "cuda":
         torch.cuda.synchronize(dev)
       t1 = time.perf_counter()
@@ -96,12 +147,13 @@ class OnPolicyRunner:
              "mean_action_noise_std": float(alg.policy.std.detach().mean()) if hasattr(alg.policy, "std") else None,
              "episodes": n, "mean_reward": float(done_rew) / n if n > 0 else None,
              "mean_episode_length": float(done_len) / n if n > 0 else None, **losses}
-      log = getattr(env.unwrapped, "extras", {}).get("log", {})
       for k, v in log.items():
         try:
           rec[k] = float(v)
         except (TypeError, ValueError):
           pass
+      if self.distributed:
+        self._finish_gather(rec)
       self.history.append(rec)
       if self.log_dir and self.rank == 0 and self.save_interval and (it + 1) % self.save_interval == 0:
         self.save(os.path.join(self.log_dir, f"model_{it + 1}.pt"))

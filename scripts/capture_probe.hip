@@ -1,0 +1,139 @@
+// capture_probe.hip -- standalone reproduction of launch_step's stream fork/join topology
+// (engine.hip) under HIP stream capture, with a trivial kernel in place of the step phases.
+//
+//   hipcc -O2 --offload-arch=gfx950 -o scripts/capture_probe scripts/capture_probe.hip
+//   ./scripts/capture_probe <nsplit> <nclass> <nsub> <piped> [shared_class_streams]
+//
+// Topology per substep (as launch_step): origin --split_fork--> split streams; on split
+// stream k: [A] -> classify -> record fork[k] -> class streams wait -> class chains
+// (B [, C, next A]) -> join[k][c] -> split stream waits; after the last substep the split
+// streams join the origin.  Every kernel adds 1 to its own counter slot so the replay can
+// be checked.  Exit 0 = captured, instantiated, replayed and checked.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                         \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return 2;                                                                       \
+    }                                                                                 \
+  } while (0)
+
+__global__ void work(int* slot) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(slot, 1);
+}
+
+int main(int argc, char** argv) {
+  const int nsplit = argc > 1 ? atoi(argv[1]) : 2;
+  const int nc = argc > 2 ? atoi(argv[2]) : 1;
+  const int nsub = argc > 3 ? atoi(argv[3]) : 3;
+  const int piped = argc > 4 ? atoi(argv[4]) : 1;
+  const int shared = argc > 5 ? atoi(argv[5]) : 0;
+  printf("probe: nsplit=%d nclass=%d nsub=%d piped=%d shared_class_streams=%d\n", nsplit, nc,
+         nsub, piped, shared);
+  fflush(stdout);
+  hipStream_t origin;
+  CK(hipStreamCreateWithFlags(&origin, hipStreamNonBlocking));
+  std::vector<hipStream_t> split(nsplit);
+  std::vector<hipEvent_t> split_join(nsplit);
+  hipEvent_t split_fork;
+  CK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
+  for (int k = 1; k < nsplit; k++) {
+    CK(hipStreamCreateWithFlags(&split[k], hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&split_join[k], hipEventDisableTiming));
+  }
+  std::vector<std::vector<hipStream_t>> cls(nsplit, std::vector<hipStream_t>(nc));
+  std::vector<std::vector<hipEvent_t>> join(nsplit, std::vector<hipEvent_t>(nc));
+  std::vector<hipEvent_t> fork(nsplit);
+  for (int k = 0; k < nsplit; k++) {
+    CK(hipEventCreateWithFlags(&fork[k], hipEventDisableTiming));
+    for (int c = 0; c < nc; c++) {
+      if (shared && k > 0) cls[k][c] = cls[0][c];
+      else CK(hipStreamCreateWithFlags(&cls[k][c], hipStreamNonBlocking));
+      CK(hipEventCreateWithFlags(&join[k][c], hipEventDisableTiming));
+    }
+  }
+  const int nslot = 64;
+  int* slots;
+  CK(hipMalloc(&slots, nslot * sizeof(int)));
+  CK(hipMemset(slots, 0, nslot * sizeof(int)));
+  CK(hipDeviceSynchronize());
+  int expect[nslot] = {};
+  auto launch = [&](hipStream_t s, int slot) {
+    hipLaunchKernelGGL(work, dim3(4), dim3(64), 0, s, slots + slot);
+    expect[slot]++;
+  };
+  for (int k = 0; k < nslot; k++) expect[k] = 0;
+  CK(hipStreamBeginCapture(origin, hipStreamCaptureModeGlobal));
+  split[0] = origin;
+  if (nsplit > 1) {
+    CK(hipEventRecord(split_fork, origin));
+    for (int k = 1; k < nsplit; k++) CK(hipStreamWaitEvent(split[k], split_fork, 0));
+  }
+  for (int sub = 0; sub < nsub; sub++) {
+    const int last = sub == nsub - 1;
+    for (int k = 0; k < nsplit; k++) {
+      hipStream_t st = split[k];
+      const int base = 8 * k;
+      if (!(nc > 0 && piped) || sub == 0) launch(st, base + 0);  // A
+      if (nc > 0) {
+        launch(st, base + 1);  // classify
+        CK(hipEventRecord(fork[k], st));
+        for (int c = 0; c < nc; c++) {
+          CK(hipStreamWaitEvent(cls[k][c], fork[k], 0));
+          launch(cls[k][c], base + 2 + c);  // B of class c
+          if (piped) {
+            launch(cls[k][c], base + 4);  // C
+            if (!last) launch(cls[k][c], base + 5);  // next A
+          }
+        }
+        launch(st, base + 6);  // B of the smallest class
+        if (piped) {
+          launch(st, base + 4);
+          if (!last) launch(st, base + 5);
+        }
+        for (int c = 0; c < nc; c++) {
+          CK(hipEventRecord(join[k][c], cls[k][c]));
+          CK(hipStreamWaitEvent(st, join[k][c], 0));
+        }
+        if (piped) continue;
+      } else {
+        launch(st, base + 6);
+      }
+      launch(st, base + 7);  // C
+    }
+  }
+  for (int k = 1; k < nsplit; k++) {
+    CK(hipEventRecord(split_join[k], split[k]));
+    CK(hipStreamWaitEvent(origin, split_join[k], 0));
+  }
+  hipGraph_t graph;
+  printf("end capture\n");
+  fflush(stdout);
+  CK(hipStreamEndCapture(origin, &graph));
+  size_t nn = 0;
+  CK(hipGraphGetNodes(graph, nullptr, &nn));
+  printf("captured %zu nodes; instantiate\n", nn);
+  fflush(stdout);
+  hipGraphExec_t exec;
+  CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+  printf("launch\n");
+  fflush(stdout);
+  CK(hipGraphLaunch(exec, origin));
+  CK(hipGraphLaunch(exec, origin));
+  CK(hipStreamSynchronize(origin));
+  int got[nslot];
+  CK(hipMemcpy(got, slots, sizeof(got), hipMemcpyDeviceToHost));
+  for (int k = 0; k < nslot; k++)
+    if (got[k] != 2 * expect[k]) {
+      printf("slot %d: %d != %d\n", k, got[k], 2 * expect[k]);
+      return 1;
+    }
+  printf("ok\n");
+  return 0;
+}

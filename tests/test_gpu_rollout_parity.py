@@ -56,7 +56,8 @@ K = 4
 HEAVY_ROWS = 60
 
 QACC_ABS, QACC_REL = 5e-2, 2e-3
-QPOS_ABS = 2e-6
+QPOS_ABS = 1e-6
+QPOS_ULPS = 2.0 ** -21  # 4 fp32 ulps of the coordinate
 SENS_ABS, SENS_REL = 2e-2, 2e-3
 TIE = 2e-5
 FUSED_MUL = 10.0
@@ -117,7 +118,17 @@ def _near_tie(ref, gpu_dist, ncon_gpu):
   return bool(d) and min(d) < TIE
 
 
-def _check_step(m, ref, st1, out, i, stats, where):
+def _converged_ref(m, st0, i, sim):
+  """The oracle's answer with the Newton iteration cap raised to 100 (MuJoCo stops at
+  `iterations`; a world that hits the cap holds a truncated iterate)."""
+  import dataclasses
+  m100 = dataclasses.replace(m, iterations=100)
+  return ol.forward(m100, st0["qpos"][i], st0["qvel"][i], st0["qacc_warmstart"][i],
+                    st0["ctrl"][i], float(st0["time"][i].reshape(-1)[0]), step=True,
+                    nconmax=sim.nconmax, njmax=sim.njmax)
+
+
+def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
   h = m.timestep
   ncon = int(out["ncon"][i].reshape(-1)[0])
   nefc = int(out["nefc"][i].reshape(-1)[0])
@@ -126,32 +137,56 @@ def _check_step(m, ref, st1, out, i, stats, where):
             f"{where}: ncon {ncon} vs {ref['ncon']}, nefc {nefc} vs {ref['nefc']}", stats)
     stats["ties"] += 1
     return
+  niter_g = int(out["solver_niter"][i].reshape(-1)[0])
+  capped = ref["niter"] >= m.iterations
+  # truncation gap of a capped world: how far MuJoCo's own iterate is from the converged
+  # answer; the GPU iterate may differ from the oracle's by that much in addition
+  gap_a = gap_v = 0.0
+  if capped:
+    conv = _converged_ref(m, st0, i, sim)
+    gap_a = np.abs(conv["qacc"] - ref["qacc"])
+    gap_v = np.abs(conv["qvel"] - ref["qvel"])
+    stats["capped"] += 1
+    stats["capped_gap_max"] = max(stats["capped_gap_max"], float(gap_a.max()))
   qa, qa_ref = out["qacc"][i], ref["qacc"]
-  bound = QACC_ABS + QACC_REL * np.abs(qa_ref)
+  bound = QACC_ABS + QACC_REL * np.abs(qa_ref) + 2.0 * gap_a
   e = np.abs(qa - qa_ref)
-  stats["qacc_ratio"] = max(stats["qacc_ratio"], float((e / bound).max()))
+  key = "capped_" if capped else ""
+  stats[key + "qacc_ratio"] = max(stats[key + "qacc_ratio"], float((e / bound).max()))
   stats["qacc_abs"] = max(stats["qacc_abs"], float(e.max()))
   stats["qacc_rel_world"] = max(stats["qacc_rel_world"], float(e.max() / max(1.0, np.abs(qa_ref).max())))
   k = int(np.argmax(e))
   stats["qacc_worst"] = sorted(stats["qacc_worst"] + [(float(e[k]), float(qa_ref[k]),
-                                float(np.abs(qa_ref).max()), nefc, where)], reverse=True)[:6]
-  _expect((e <= bound).all(), f"{where}: qacc dof {int(np.argmax(e / bound))} err {e.max():.3e}", stats)
+                                float(np.abs(qa_ref).max()), nefc, ref["niter"], niter_g, where)],
+                               reverse=True)[:6]
+  _expect((e <= bound).all(), f"{where}: qacc dof {int(np.argmax(e / bound))} err {e.max():.3e}"
+          f" (niter {niter_g} vs {ref['niter']}, capped {capped})", stats)
   ev = np.abs(st1["qvel"][i] - ref["qvel"])
-  vb = h * bound + 1e-6
-  stats["qvel_ratio"] = max(stats["qvel_ratio"], float((ev / vb).max()))
+  vb = h * (QACC_ABS + QACC_REL * np.abs(qa_ref)) + 2.0 * gap_v + 1e-6
+  stats[key + "qvel_ratio"] = max(stats[key + "qvel_ratio"], float((ev / vb).max()))
+  if not (ev <= vb).all():
+    j = int(np.argmax(ev / vb))
+    stats.setdefault("qvel_detail", []).append(dict(
+      where=where, dof=j, err=float(ev[j]), h_qacc_err=float(h * e[j]), qvel_in=float(st0["qvel"][i][j]),
+      qvel_ref=float(ref["qvel"][j]), qacc_ref=float(qa_ref[j]), niter=(niter_g, ref["niter"]), nefc=nefc))
   _expect((ev <= vb).all(), f"{where}: qvel err {ev.max():.3e}", stats)
   ep = np.abs(st1["qpos"][i] - ref["qpos"])
+  # position: a few fp32 ulps of the coordinate (root x/y reach tens of metres on the
+  # terrain grids) plus the velocity error integrated over the step
+  pb = QPOS_ABS + QPOS_ULPS * np.abs(ref["qpos"]) + h * (vb - 1e-6).max()
   stats["qpos_abs"] = max(stats["qpos_abs"], float(ep.max()))
-  _expect(ep.max() <= QPOS_ABS, f"{where}: qpos err {ep.max():.3e}", stats)
+  stats["qpos_ratio"] = max(stats["qpos_ratio"], float((ep / pb).max()))
+  _expect((ep <= pb).all(), f"{where}: qpos err {ep.max():.3e}", stats)
   s, s_ref = out["sensordata"][i], ref["sensordata"]
   es = np.abs(s - s_ref)
-  sb = SENS_ABS + SENS_REL * np.abs(s_ref)
+  sb = SENS_ABS + SENS_REL * np.abs(s_ref) + (SENS_REL * np.abs(s_ref).max() if capped else 0.0)
   stats["sens_ratio"] = max(stats["sens_ratio"], float((es / sb).max()) if es.size else 0.0)
-  _expect((es <= sb).all(), f"{where}: sensordata {int(np.argmax(es / sb))} err {es.max():.3e}", stats)
-  dn = abs(int(out["solver_niter"][i].reshape(-1)[0]) - ref["niter"])
+  _expect((es <= sb).all(), f"{where}: sensordata {int(np.argmax(es / sb))} err {es.max():.3e} "
+          f"(value {float(s_ref[int(np.argmax(es / sb))]):.3e})", stats)
+  dn = abs(niter_g - ref["niter"])
   stats["niter_maxdiff"] = max(stats["niter_maxdiff"], dn)
   stats["niter_equal"] += int(dn == 0)
-  _expect(dn <= 1, f"{where}: Newton iterations {out['solver_niter'][i]} vs {ref['niter']}", stats)
+  _expect(dn <= 1 or capped, f"{where}: Newton iterations {niter_g} vs {ref['niter']}", stats)
   stats["checked"] += 1
   stats["max_nefc"] = max(stats["max_nefc"], nefc)
   stats["heavy_checked"] += int(nefc > HEAVY_ROWS)
@@ -182,7 +217,8 @@ def test_rollout_shadow_parity(task, num_envs, gpu_device):
   stats = dict(task=task, num_envs=num_envs, worlds=len(sel), checked=0, ties=0,
                heavy_checked=0, max_nefc=0, reset_worlds=int(just_reset[sel].sum()),
                qacc_ratio=0.0, qacc_abs=0.0, qacc_rel_world=0.0, qvel_ratio=0.0, qpos_abs=0.0,
-               sens_ratio=0.0, qacc_worst=[], niter_maxdiff=0, niter_equal=0, overflow_skipped=0,
+               sens_ratio=0.0, qacc_worst=[], niter_maxdiff=0, capped=0, capped_gap_max=0.0,
+               capped_qacc_ratio=0.0, capped_qvel_ratio=0.0, qpos_ratio=0.0, niter_equal=0, overflow_skipped=0,
                fields=fields, rows_over_60=int((nefc_all > HEAVY_ROWS).sum()))
   for t in range(K):
     st0, st1, out = states[t], states[t + 1], outs[t]
@@ -194,7 +230,7 @@ def test_rollout_shadow_parity(task, num_envs, gpu_device):
       if ref["overflow"]:
         stats["overflow_skipped"] += 1
         continue
-      _check_step(m, ref, st1, out, i, stats, f"{task} world {w} substep {t}")
+      _check_step(m, ref, st0, st1, out, i, stats, f"{task} world {w} substep {t}", sim)
   # one fused decimation-substep step (mjData outputs after the last substep only)
   dec = env.cfg.decimation
   st0 = states[-1]
@@ -208,7 +244,7 @@ def test_rollout_shadow_parity(task, num_envs, gpu_device):
     tm = np.ascontiguousarray(st0["time"][i].reshape(1))
     ref = ol.rollout(m, q, v, ws, c, tm, dec, nconmax=sim.nconmax, njmax=sim.njmax)
     ev = np.abs(st1["qvel"][i] - v[0])
-    ep = np.abs(st1["qpos"][i] - q[0])
+    ep = np.abs(st1["qpos"][i] - q[0]) / (1.0 + QPOS_ULPS / QPOS_ABS * np.abs(q[0]))
     # bound: FUSED_MUL x the one-step qvel bound summed over the substeps, at the larger of
     # the last substep's qacc and the mean acceleration over the step
     acc = np.maximum(np.abs(ref["qacc"][0]), np.abs(v[0] - st0["qvel"][i]) / (dec * m.timestep))
