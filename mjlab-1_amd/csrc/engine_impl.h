@@ -286,6 +286,47 @@ __device__ __forceinline__ void tiles_add_jtdj(float (&A)[2][16], const Tiles& T
     }
   }
 }
+// The same sum on the matrix cores (built with -DMJX_JTDJ_MFMA=1; A/B against the VALU
+// tiles above): v_mfma_f32_16x16x4_f32 (exact fp32, 32 cycles issue per SIMD) over 16x16
+// blocks (I, J), I >= J, of the padded Hessian, 4 active rows per instruction.  Lane l
+// supplies A[i = l & 15][k = l >> 4] = J[act[k0 + k], 16 I + i] and B[k][j = l & 15] =
+// D * J[act[k0 + k], 16 J + j]; the accumulator holds block row (l >> 4) * 4 + reg, column
+// l & 15 (cdna_hip_programming.md section 3).  Lm (row stride nvp) must already hold M; the
+// blocks are added into it (lower triangle and the diagonal blocks).  Ends synced.
+#ifndef MJX_JTDJ_MFMA
+#define MJX_JTDJ_MFMA 0
+#endif
+typedef float mfma_f4 __attribute__((ext_vector_type(4)));
+template <int NR>
+__device__ __forceinline__ void mfma_add_jtdj(float* Lm, const float* J, const float* Dv,
+                                              const int* act, int nact, int nvp, int lane) {
+  // one block at a time (one 4-register accumulator live: the Newton kernel sits at the
+  // 3-waves-per-SIMD register bound)
+  constexpr int NB = (NR + 15) / 16;
+  const int i16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int I = 0; I < NB; I++) {
+#pragma unroll
+    for (int Jb = 0; Jb <= I; Jb++) {
+      mfma_f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int ca = 16 * I + i16, cb = 16 * Jb + i16;
+      for (int k0 = 0; k0 < nact; k0 += 4) {
+        const int k = k0 + kq;
+        const bool in = k < nact;
+        const int r = in ? act[k] : 0;
+        const float a = (in && ca < nvp) ? J[r * nvp + ca] : 0.f;
+        const float bv = (in && cb < nvp) ? J[r * nvp + cb] * Dv[r] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int row = 16 * I + 4 * kq + q;
+        if (row < nvp && cb < nvp) Lm[row * nvp + cb] += acc[q];
+      }
+    }
+  }
+  sync();
+}
 // out[i] = Mm[i,:] . v for i < nrow (row stride nvp), v broadcast-read as float4.
 __device__ __forceinline__ void matvec_rows(float* out, const float* Mm, const float* v, int nrow,
                                             int nvp, int lane) {
@@ -1203,8 +1244,14 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 // Worlds [w0, w1) -- one split of the batch (launch_step).  `sel` & 0xff selects that
 // split's Newton work-list segments; in phases A and C, sel >> 8 = row class + 1 restricts
 // the launch to that class's worlds (0: every world).
+#if MJX_JTDJ_MFMA
+// the MFMA accumulator must not push the Newton kernel past 168 registers (3 waves / SIMD)
+#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#else
+#define MJX_PHASE_ATTR
+#endif
 template <int NR, int PH, int SP>
-__global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P, int w0, int w1,
+__global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params* __restrict__ P, int w0, int w1,
                                                     int sel, int last, int integrate,
                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
@@ -2566,6 +2613,11 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
         if (iter > 0 && scale * gn < fmaxf(o.tolerance, 16.f * FLT_EPSILON * scale * gr)) break;
         // Hessian H = M + J_act^T D J_act in register tiles, factor, solve
         if (refactor) {
+#if MJX_JTDJ_MFMA
+          tiles_store(Mt, T, Lm, nvp);
+          sync();
+          mfma_add_jtdj<NR>(Lm, J, Dv, act, nact, nvp, lane);
+#else
           float A[2][16];
 #pragma unroll
           for (int s2 = 0; s2 < 2; s2++)
@@ -2573,6 +2625,7 @@ __global__ __launch_bounds__(kWave) void step_phase(const Params* __restrict__ P
             for (int e2 = 0; e2 < 16; e2++) A[s2][e2] = Mt[s2][e2];
           tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
           tiles_store(A, T, Lm, nvp);
+#endif
         }
         sync();
         SUBSTAMP(2);

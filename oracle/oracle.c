@@ -1255,9 +1255,13 @@ static void solve_newton(const mjxModelDesc* m, orcData* d) {
 
   d->niter = 0;
   if (nefc == 0) {
-    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    memcpy(d->qacc, d->qacc_given ? d->qacc_given : d->qacc_smooth, sizeof(double) * nv);
     memset(d->qfrc_constraint, 0, sizeof(double) * nv);
     return;
+  }
+  if (d->qacc_given) {  /* orc_step_given_qacc: forces from the given qacc, no iterations */
+    memcpy(x, d->qacc_given, sizeof(double) * nv);
+    goto forces;
   }
   /* warmstart: pick qacc_warmstart if its total cost beats qacc_smooth */
   memcpy(x, d->qacc_warmstart, sizeof(double) * nv);
@@ -1320,6 +1324,9 @@ static void solve_newton(const mjxModelDesc* m, orcData* d) {
     cost = eval_cost(m, d, x, Mx, jar);
     if (scale * (old - cost) < m->tolerance) break;
   }
+forces:
+  mulM(m, d, Mx, x);
+  d->cost = eval_cost(m, d, x, Mx, jar);
   memcpy(d->qacc, x, sizeof(double) * nv);
   /* constraint forces */
   memset(d->qfrc_constraint, 0, sizeof(double) * nv);
@@ -1608,6 +1615,28 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
     }
   if (out_efc_force) memcpy(out_efc_force, d->efc_force, sizeof(double) * d->nefc);
   if (out_niter) *out_niter = d->niter;
+  int ov = d->overflow;
+  orc_data_free(d);
+  return ov;
+}
+
+int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                        const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                        double time, const double* qacc, double* out_qpos, double* out_qvel,
+                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost) {
+  orcData* d = orc_data_new(m, nconmax, njmax);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_warmstart, sizeof(double) * m->nv);
+  memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+  d->time = time;
+  d->qacc_given = qacc;
+  orc_step(m, d);
+  if (out_qpos) memcpy(out_qpos, d->qpos, sizeof(double) * m->nq);
+  if (out_qvel) memcpy(out_qvel, d->qvel, sizeof(double) * m->nv);
+  if (out_sensordata) memcpy(out_sensordata, d->sensordata, sizeof(double) * m->nsensordata);
+  if (out_qfrc_constraint) memcpy(out_qfrc_constraint, d->qfrc_constraint, sizeof(double) * m->nv);
+  if (out_cost) *out_cost = d->cost;
   int ov = d->overflow;
   orc_data_free(d);
   return ov;

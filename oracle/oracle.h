@@ -50,6 +50,10 @@ typedef struct {
   double *efc_J, *efc_pos, *efc_margin, *efc_D, *efc_R, *efc_aref, *efc_vel, *efc_force,
       *efc_diagApprox, *efc_frame_mu;
   int overflow; /* bit0: contacts dropped, bit1: rows dropped, bit2: unsupported pair */
+  /* when set: the constraint stage takes qacc from here instead of running the Newton
+   * solver (forces, qfrc_constraint and the integration follow from it) */
+  const double* qacc_given;
+  double cost;  /* the constraint-problem cost at the final qacc (Gauss + active rows) */
   /* scratch */
   double* work;
 } orcData;
@@ -79,6 +83,16 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
                      double* out_actuator_force, double* out_cacc, int* out_ncon,
                      int* out_nefc, double* out_contact /* ncon*(2+1+3+3) */,
                      double* out_efc_force, int* out_niter);
+
+/* One mj_step whose constraint stage uses the given qacc instead of solving for it:
+ * efc_force = -D (J qacc - aref) on the rows with J qacc < aref, qfrc_constraint = J^T f,
+ * then the implicitfast / Euler integration of orc_step.  The parity tests use it to check
+ * the engine's integration against its own solver output (the solver is checked
+ * separately through qacc). */
+int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                        const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                        double time, const double* qacc, double* out_qpos, double* out_qvel,
+                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost);
 
 #ifdef __cplusplus
 }

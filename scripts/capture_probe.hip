@@ -2,7 +2,12 @@
 // (engine.hip) under HIP stream capture, with a trivial kernel in place of the step phases.
 //
 //   hipcc -O2 --offload-arch=gfx950 -o scripts/capture_probe scripts/capture_probe.hip
-//   ./scripts/capture_probe <nsplit> <nclass> <nsub> <piped> [shared_class_streams]
+//   ./scripts/capture_probe <nsplit> <nclass> <nsub> <piped> [shared_class_streams] [features]
+// features (bit mask, engine-like traits added to the trivial kernels):
+//   1 warm: run the same launch sequence eagerly (and synchronise) before capturing it
+//   2 lds:  kernels take 96 KiB of dynamic LDS (hipFuncSetAttribute beforehand)
+//   4 args: kernels take the engine's 7 arguments
+//   8 wide: the classify launch is one 1024-thread block
 //
 // Topology per substep (as launch_step): origin --split_fork--> split streams; on split
 // stream k: [A] -> classify -> record fork[k] -> class streams wait -> class chains
@@ -27,6 +32,16 @@
 __global__ void work(int* slot) {
   if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(slot, 1);
 }
+__global__ void work_lds(int* slot) {
+  extern __shared__ int sh[];
+  sh[threadIdx.x] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(slot, sh[0]);
+}
+__global__ void work_args(const int* p, int w0, int w1, int sel, int last, int integ, int* slot) {
+  (void)p; (void)w0; (void)w1; (void)sel; (void)last; (void)integ;
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(slot, 1);
+}
 
 int main(int argc, char** argv) {
   const int nsplit = argc > 1 ? atoi(argv[1]) : 2;
@@ -34,8 +49,9 @@ int main(int argc, char** argv) {
   const int nsub = argc > 3 ? atoi(argv[3]) : 3;
   const int piped = argc > 4 ? atoi(argv[4]) : 1;
   const int shared = argc > 5 ? atoi(argv[5]) : 0;
-  printf("probe: nsplit=%d nclass=%d nsub=%d piped=%d shared_class_streams=%d\n", nsplit, nc,
-         nsub, piped, shared);
+  const int feat = argc > 6 ? atoi(argv[6]) : 0;
+  printf("probe: nsplit=%d nclass=%d nsub=%d piped=%d shared_class_streams=%d features=%d\n", nsplit,
+         nc, nsub, piped, shared, feat);
   fflush(stdout);
   hipStream_t origin;
   CK(hipStreamCreateWithFlags(&origin, hipStreamNonBlocking));
@@ -64,12 +80,30 @@ int main(int argc, char** argv) {
   CK(hipMemset(slots, 0, nslot * sizeof(int)));
   CK(hipDeviceSynchronize());
   int expect[nslot] = {};
+  const size_t lds = 96 * 1024;
+  if (feat & 2) CK(hipFuncSetAttribute((const void*)work_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  bool counting = true;
   auto launch = [&](hipStream_t s, int slot) {
-    hipLaunchKernelGGL(work, dim3(4), dim3(64), 0, s, slots + slot);
-    expect[slot]++;
+    if (feat & 2)
+      hipLaunchKernelGGL(work_lds, dim3(131), dim3(64), lds, s, slots + slot);
+    else if (feat & 4)
+      hipLaunchKernelGGL(work_args, dim3(131), dim3(64), 0, s, (const int*)slots, 0, 131, 1, 0, 1, slots + slot);
+    else
+      hipLaunchKernelGGL(work, dim3(4), dim3(64), 0, s, slots + slot);
+    if (counting) expect[slot]++;
+  };
+  auto classify = [&](hipStream_t s, int slot) {
+    if (feat & 8) {
+      hipLaunchKernelGGL(work, dim3(1), dim3(1024), 0, s, slots + slot);
+      if (counting) expect[slot]++;
+    } else {
+      launch(s, slot);
+    }
   };
   for (int k = 0; k < nslot; k++) expect[k] = 0;
-  CK(hipStreamBeginCapture(origin, hipStreamCaptureModeGlobal));
+  for (int pass = (feat & 1) ? 0 : 1; pass < 2; pass++) {
+  counting = pass == 1;
+  if (pass == 1) CK(hipStreamBeginCapture(origin, hipStreamCaptureModeGlobal));
   split[0] = origin;
   if (nsplit > 1) {
     CK(hipEventRecord(split_fork, origin));
@@ -82,7 +116,7 @@ int main(int argc, char** argv) {
       const int base = 8 * k;
       if (!(nc > 0 && piped) || sub == 0) launch(st, base + 0);  // A
       if (nc > 0) {
-        launch(st, base + 1);  // classify
+        classify(st, base + 1);
         CK(hipEventRecord(fork[k], st));
         for (int c = 0; c < nc; c++) {
           CK(hipStreamWaitEvent(cls[k][c], fork[k], 0));
@@ -111,6 +145,15 @@ int main(int argc, char** argv) {
   for (int k = 1; k < nsplit; k++) {
     CK(hipEventRecord(split_join[k], split[k]));
     CK(hipStreamWaitEvent(origin, split_join[k], 0));
+  }
+  if (pass == 0) {  // the eager warm-up run
+    CK(hipStreamSynchronize(origin));
+    CK(hipDeviceSynchronize());
+    CK(hipMemset(slots, 0, nslot * sizeof(int)));
+    CK(hipDeviceSynchronize());
+    printf("eager pass ok\n");
+    fflush(stdout);
+  }
   }
   hipGraph_t graph;
   printf("end capture\n");

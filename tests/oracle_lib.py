@@ -39,6 +39,7 @@ def lib():
     assert _LIB.orc_model_desc_size() == ctypes.sizeof(ModelDesc), "oracle ABI mismatch"
     _LIB.orc_forward_dump.restype = ctypes.c_int
     _LIB.orc_rollout.restype = ctypes.c_int
+    _LIB.orc_step_given_qacc.restype = ctypes.c_int
   return _LIB
 
 
@@ -73,6 +74,27 @@ def forward(model, qpos, qvel=None, qacc_warmstart=None, ctrl=None, time=0.0, st
   out["ncon"], out["nefc"], out["niter"], out["overflow"] = ncon.value, nefc.value, niter.value, ov
   out["contact"] = out["contact"][:ncon.value]
   out["efc_force"] = out["efc_force"][:nefc.value]
+  return out
+
+
+def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, nconmax=256, njmax=1024):
+  """One mj_step whose constraint stage takes `qacc` instead of solving for it (forces,
+  qfrc_constraint, sensors and the integration follow from it), plus the constraint
+  problem's cost at that qacc.  Single world; returns a dict of fp64 arrays."""
+  desc, keep = make_desc(model)
+  f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
+  nq, nv, nu, ns = model.nq, model.nv, model.nu, model.nsensordata
+  out = dict(qpos=np.zeros(nq), qvel=np.zeros(nv), sensordata=np.zeros(max(ns, 1)),
+             qfrc_constraint=np.zeros(nv))
+  cost = ctypes.c_double()
+  a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
+  g = f64(qacc, nv)
+  ov = lib().orc_step_given_qacc(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
+                                 ctypes.c_double(time), _p(g), _p(out["qpos"]), _p(out["qvel"]),
+                                 _p(out["sensordata"]), _p(out["qfrc_constraint"]), ctypes.byref(cost))
+  del keep
+  out["sensordata"] = out["sensordata"][:ns]
+  out["cost"], out["overflow"] = cost.value, ov
   return out
 
 
