@@ -486,7 +486,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   s->gF = s->gC + ((s->lds_ph[2].pack_len + 63) & ~63);
   {
     const int nvp = (s->d.nv + 3) & ~3;
-    s->gstride = s->gF + ((nvp * nvp + 63) & ~63);
+    s->gstride = s->gF + ((mjx::ltr_size(nvp) + 63) & ~63);  // implicit factor, LTR form
   }
   const mjx::Dims& d = s->d;
   // data arena: one allocation, 256-B aligned sub-buffers

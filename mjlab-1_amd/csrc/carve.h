@@ -18,13 +18,23 @@ constexpr int nr_for_nv(int nv) {
        : nvp <= 36 ? 36 : nvp <= 40 ? 40 : nvp <= 48 ? 48 : nvp <= 56 ? 56 : 64;
 }
 
+// Lower-tile rows ("LTR"): the lower triangle of an nvp x nvp matrix (nvp a multiple of 4)
+// stored row by row, row i = 4b + r holding its columns [0, 4(b + 1)) -- the 4x4 tiles on and
+// left of the diagonal -- at offset 8 b (b + 1) + 4 (b + 1) r.  Dense (chunk k of 4 floats is
+// at 4k), 16-byte aligned rows, 8 nb (nb + 1) floats in all (720 for nvp 36 instead of 1296).
+// The phase hand-offs of the symmetric M (A -> B) and of the implicit-integration factor
+// (A -> C) use it.
+constexpr int ltr_off(int i) { return 8 * (i >> 2) * ((i >> 2) + 1) + 4 * ((i >> 2) + 1) * (i & 3); }
+constexpr int ltr_size(int nvp) { return 8 * (nvp >> 2) * ((nvp >> 2) + 1); }
+
 // Phase carves.  Masks: A = 1 (kinematics .. constraint rows), B = 2 (Newton), C = 4
 // (post/integrate).  A phase carve holds only the regions that phase touches (the rest sit
 // past the allocation and are never accessed).  Phase inputs are carved FIRST, in a fixed
 // order, so the per-world global scratch holds them as one contiguous "pack" with the same
 // internal offsets: B pack = [ints M qacc_smooth qfrc_smooth efc_aref efc_D efc_J] (J last,
-// so only the live rows are copied), C pack = [A outputs | B outputs].  Each phase then
-// fills its inputs with a single bulk copy.
+// so only the live rows are copied; M's slot holds M in LTR form, the rest of the slot is
+// neither written nor read), C pack = [A outputs | B outputs].  Each phase then fills its
+// inputs with one or two bulk copies.
 constexpr Lds make_lds(const Dims& d, int ph) {
   Lds L{};
   const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
@@ -52,8 +62,8 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
     {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
-    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, Cp},
-    {&Lds::con_n, 3 * C, A},  // phase A: unit normals (cframe() rebuilds the frame)
+    {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, 0},
+    {&Lds::con_n, 3 * C, A | Cp},  // unit normals: cframe() rebuilds the frame where used
     {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_kb, 2 * C, A}, {&Lds::con_imp, C, A},
     {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
     {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
@@ -70,7 +80,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   int Lds::* const packC[] = {
       &Lds::cdof, &Lds::cdofdot, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
       &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
-      &Lds::con_frame, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
+      &Lds::con_n, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
       // written by phase B:
       &Lds::ints, &Lds::x, &Lds::qfrc_con, &Lds::efc_force};
   constexpr int kAbsent = 1 << 24;

@@ -521,6 +521,79 @@ __device__ __forceinline__ float rows_solve(const float (&M)[NR], float rdiag, c
   for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
   return v * rdiag;
 }
+// The same three steps on a factor kept in lower-tile-rows form (LTR, carve.h: row i holds
+// columns [0, 4(i/4 + 1)) at ltr_off(i)): the phase A -> C hand-off of the implicit factor,
+// 720 instead of 1296 floats for nvp 36.  Columns past a row's tiles are zero in the full
+// form (rows_store_strict), so nothing else changes.
+template <int NR>
+__device__ __forceinline__ void rows_store_strict_ltr(const float (&A)[NR], float rd, float* Lp, int nvp,
+                                                      int lane) {
+  if (lane >= nvp) return;
+  float* row = Lp + ltr_off(lane);
+  const int len = 4 * ((lane >> 2) + 1);
+#pragma unroll
+  for (int c = 0; c < NR; c += 4)
+    if (c < len)
+      st4v(row + c, make_float4(c < lane ? A[c] * rd : c == lane ? rd : 0.f,
+                                c + 1 < lane ? A[c + 1] * rd : c + 1 == lane ? rd : 0.f,
+                                c + 2 < lane ? A[c + 2] * rd : c + 2 == lane ? rd : 0.f,
+                                c + 3 < lane ? A[c + 3] * rd : c + 3 == lane ? rd : 0.f));
+}
+template <int NR>
+__device__ __forceinline__ void rows_load_factor_ltr(float (&A)[NR], float& rd, const float* Lp,
+                                                     int nvp, int lane) {
+  const int row = lane < nvp ? lane : 0;
+  const float* rp = Lp + ltr_off(row);
+  const int len = 4 * ((row >> 2) + 1);
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < len) v = ld4(rp + c);
+    A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
+  }
+  rd = lane < nvp ? rp[lane] : 1.f;
+  const float ljj = __builtin_amdgcn_rcpf(rd);
+#pragma unroll
+  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * (rl(rd, k) * ljj) : 0.f;
+}
+template <int NR>
+__device__ __forceinline__ float rows_solve_ltr(const float (&M)[NR], float rdiag, const float* Lp,
+                                                float x, int nvp, int lane) {
+  float u = x;
+#pragma unroll
+  for (int j = 0; j < NR; j++) u = fmaf(-M[j], rl(u, j), u);
+  float Nc[NR];
+  const int col = lane < nvp ? lane : 0;
+#pragma unroll
+  for (int j = 0; j < NR; j++) Nc[j] = (j < nvp && j > lane) ? Lp[ltr_off(j) + col] : 0.f;
+  float v = u * rdiag;
+#pragma unroll
+  for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
+  return v * rdiag;
+}
+// LDS matrix (row stride nvp) -> its lower 4x4 tiles in LTR form (any memory), chunk k of 4
+// floats at 4k: block b of 4 rows starts at chunk 2 b (b + 1), each row takes b + 1 chunks.
+__device__ __forceinline__ void store_ltr(float* dst, const float* Mm, int nvp, int lane) {
+  const int nchunk = ltr_size(nvp) >> 2;
+  for (int k = lane; k < nchunk; k += kWave) {
+    int b = 0;
+    while (2 * (b + 1) * (b + 2) <= k) b++;
+    const int kk = k - 2 * b * (b + 1), r = kk / (b + 1), cc = kk - r * (b + 1);
+    st4v(dst + 4 * k, ld4(Mm + (4 * b + r) * nvp + 4 * cc));
+  }
+}
+// Lower 4x4 tiles from a matrix in LTR form (tiles_load's layout counterpart).
+__device__ __forceinline__ void tiles_load_ltr(float (&A)[2][16], const Tiles& T, const float* Mp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float4 v = ld4(Mp + ltr_off(4 * T.bi[s] + r) + 4 * T.bj[s]);
+      A[s][4 * r + 0] = v.x; A[s][4 * r + 1] = v.y; A[s][4 * r + 2] = v.z; A[s][4 * r + 3] = v.w;
+    }
+  }
+}
 // Tiles (lower 4x4 blocks) -> LDS matrix (row stride nvp), for rows_load.
 __device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles& T, float* Mm, int nvp) {
 #pragma unroll
@@ -598,6 +671,12 @@ __device__ __forceinline__ CFrame cframe(V3 n) {
   f.t = t * (1.0f / fmaxf(norm(t), MINVAL));
   f.b = cross(n, f.t);
   return f;
+}
+// F^T v for the contact frame F rebuilt from the unit normal at np (the C pack carries the
+// normals only)
+__device__ __forceinline__ V3 frame_tv(const float* np, V3 v) {
+  const CFrame F = cframe(v3(np));
+  return F.n * v.x + F.t * v.y + F.b * v.z;
 }
 __device__ __forceinline__ void append(const ConOut& co, int key, int g1, int g2, float dist,
                                        V3 pos, V3 n) {
@@ -1167,7 +1246,7 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
       float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
       fc = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
     }
-    fg = mulTv(S + L.con_frame + 9 * c, fc);
+    fg = frame_tv(S + L.con_n + 3 * c, fc);
   }
   // the sensors' descriptors, lane k = k-th single-slot contact sensor (ncsens <= 64): the
   // loop below reads them with v_readlane instead of a dependent scalar-load chain per sensor
@@ -1229,8 +1308,8 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
         if (bits & 1) v = lane == 0 ? found : 0.f;
         else if (bits & 8) v = lane == 0 ? rl(dist, cs) : 0.f;
         else if (bits & 16) v = lane < 3 ? S[L.con_pos + 3 * cs + t] : 0.f;
-        else if (bits & 32) v = lane < 3 ? sg * S[L.con_frame + 9 * cs + t] : 0.f;
-        else if (bits & 64) v = lane < 3 ? sg * S[L.con_frame + 9 * cs + 3 + t] : 0.f;
+        else if (bits & 32) v = lane < 3 ? sg * S[L.con_n + 3 * cs + t] : 0.f;
+        else if (bits & 64) v = lane < 3 ? sg * vc(cframe(v3(S + L.con_n + 3 * cs)).t, t) : 0.f;
         else if (bits & 2) {
           const float fx = rl(fc.x, cs), fy = rl(fc.y, cs), fz = rl(fc.z, cs);
           v = lane == 0 ? fx : lane == 1 ? fy : lane == 2 ? fz : 0.f;
@@ -1605,9 +1684,10 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       S[L.M + i * nvp + i] += Dr.arm;
     }
     sync();
-    // M to the B pack now: its LDS slot is reused (in place factor, then contacts).  Phase C
-    // gets the implicit-integration factor of M + h D instead (below, scratch region F).
-    cp4(gw + LB.M, S + L.M, nvp * nvp, lane);
+    // M to the B pack now, as its lower tiles (LTR): its LDS slot is reused (in place factor,
+    // then contacts).  Phase C gets the implicit-integration factor of M + h D instead
+    // (below, scratch region F, also LTR).
+    store_ltr(gw + LB.M, S + L.M, nvp, lane);
     STAMP(2);
     // =========================================================== velocity stage
     // cvel(b) = sum over the dofs moving b of cdof * qvel: broadcast loop over the dofs
@@ -1783,7 +1863,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
       float rd;
       rows_chol<NR>(A, rd, S + L.chol, nvp, lane);
-      rows_store_strict<NR>(A, rd, gf, nvp, lane);
+      rows_store_strict_ltr<NR>(A, rd, gf, nvp, lane);
     }
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
     spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
@@ -2350,7 +2430,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
             float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
             f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
           }
-          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          V3 fg = frame_tv(S + L.con_n + 3 * c, f);
           net = net + fg * (a1 ? 1.f : -1.f);
           float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
                   : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
@@ -2372,8 +2452,8 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
             if (bits & 1) oo[0] = (float)found;
             else if (bits & 8) oo[0] = S[L.con_dist + c];
             else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
-            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
-            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_n + 3 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * vc(cframe(v3(S + L.con_n + 3 * c)).t, t); }
             else if (bits & 2) {
               int r0 = Si[L.con_efc + c];
               if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
@@ -2474,11 +2554,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
     cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
     cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
     cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
-    for (int c = lane; c < C; c += kWave) {  // C pack: the full contact frames
-      const CFrame F = cframe(c < ncon ? v3(S + L.con_n + 3 * c) : V3{0.f, 0.f, 1.f});
-      float* fr = gc + LC.con_frame + 9 * c;
-      st3(fr, F.n); st3(fr + 3, F.t); st3(fr + 6, F.b);
-    }
+    cp4(gc + LC.con_n, S + L.con_n, (3 * C + 3) & ~3, lane);  // normals (C rebuilds frames)
     cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
     cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
     cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
@@ -2491,13 +2567,16 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       // row classes (launch_step, classify_kernel): class k > 0 holds the worlds with
       // row_cap[k-2] < nefc <= row_cap[k-1], class 0 the rest (all worlds without classes)
       const int cls = integrate;
+      // B pack: carve offsets == pack offsets; M's slot holds M in LTR form (the rest of the
+      // slot is neither written nor read)
+      cp_pack(S, gw, L.M + ltr_size(nvp), lane);
       if (cls <= 0) {
-        cp_pack(S, gw, L.efc_J + nefc_in * nvp, lane);  // B pack: carve offsets == pack offsets
+        cp_pack(S + L.qacc_smooth, gw + L.qacc_smooth, L.efc_J + nefc_in * nvp - L.qacc_smooth, lane);
       } else {
         // the pack is laid out with the full-capacity carve LB: [ints M qacc_smooth
         // qfrc_smooth efc_aref] sit at the same offsets in both, efc_D and efc_J move
         const int nr4 = (nefc_in + 3) & ~3;
-        cp_pack(S, gw, LB.efc_aref + nr4, lane);
+        cp_pack(S + L.qacc_smooth, gw + LB.qacc_smooth, LB.efc_aref + nr4 - LB.qacc_smooth, lane);
         cp_pack(S + L.efc_D, gw + LB.efc_D, nr4, lane);
         cp_pack(S + L.efc_J, gw + LB.efc_J, nefc_in * nvp, lane);
       }
@@ -2514,7 +2593,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
     int ncon = ints[4];
     (void)ncon;
     float Mt[2][16];  // M as register tiles; its LDS slot becomes H / jt_mul scratch
-    tiles_load(Mt, T, S + L.M, nvp);
+    tiles_load_ltr(Mt, T, S + L.M);
     sync();
     STAMP(15);
     // =========================================================== Newton solver
@@ -2865,7 +2944,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
             float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
             f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
           }
-          V3 fg = mulTv(S + L.con_frame + 9 * c, f);
+          V3 fg = frame_tv(S + L.con_n + 3 * c, f);
           net = net + fg * (a1 ? 1.f : -1.f);
           float k = reduce == REDUCE_MINDIST ? S[L.con_dist + c]
                   : reduce == REDUCE_MAXFORCE ? -norm(f) : (float)nsel;
@@ -2887,8 +2966,8 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
             if (bits & 1) oo[0] = (float)found;
             else if (bits & 8) oo[0] = S[L.con_dist + c];
             else if (bits & 16) { for (int t = 0; t < 3; t++) oo[t] = S[L.con_pos + 3 * c + t]; }
-            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + t]; }
-            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_frame + 9 * c + 3 + t]; }
+            else if (bits & 32) { for (int t = 0; t < 3; t++) oo[t] = sg * S[L.con_n + 3 * c + t]; }
+            else if (bits & 64) { for (int t = 0; t < 3; t++) oo[t] = sg * vc(cframe(v3(S + L.con_n + 3 * c)).t, t); }
             else if (bits & 2) {
               int r0 = Si[L.con_efc + c];
               if (Si[L.con_dim + c] == 1) { oo[0] = S[L.efc_force + r0]; oo[1] = oo[2] = 0; }
@@ -2951,9 +3030,9 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       SUBSTAMP(10);
       {
         float A[NR], rd;
-        rows_load_factor<NR>(A, rd, gf, nvp, lane);
+        rows_load_factor_ltr<NR>(A, rd, gf, nvp, lane);
         const float f = lane < nvp ? S[L.qfrc_smooth + lane] + S[L.qfrc_con + lane] : 0.f;
-        const float acc = rows_solve<NR>(A, rd, gf, f, nvp, lane);
+        const float acc = rows_solve_ltr<NR>(A, rd, gf, f, nvp, lane);
         if (lane < nv) S[L.qvel + lane] += h * acc;
       }
       sync();

@@ -1257,6 +1257,8 @@ static void solve_newton(const mjxModelDesc* m, orcData* d) {
   if (nefc == 0) {
     memcpy(d->qacc, d->qacc_given ? d->qacc_given : d->qacc_smooth, sizeof(double) * nv);
     memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+    if (d->qacc_given && d->qfrc_constraint_given)
+      memcpy(d->qfrc_constraint, d->qfrc_constraint_given, sizeof(double) * nv);
     return;
   }
   if (d->qacc_given) {  /* orc_step_given_qacc: forces from the given qacc, no iterations */
@@ -1337,6 +1339,8 @@ forces:
     d->efc_force[r] = v < 0 ? -d->efc_D[r] * v : 0;
     for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += J[i] * d->efc_force[r];
   }
+  if (d->qacc_given && d->qfrc_constraint_given)
+    memcpy(d->qfrc_constraint, d->qfrc_constraint_given, sizeof(double) * nv);
 }
 
 /* ------------------------------------------------------------------ sensors */
@@ -1622,8 +1626,9 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
 
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                        double time, const double* qacc, double* out_qpos, double* out_qvel,
-                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost) {
+                        double time, const double* qacc, const double* qfrc_constraint,
+                        double* out_qpos, double* out_qvel, double* out_sensordata,
+                        double* out_qfrc_constraint, double* out_cost) {
   orcData* d = orc_data_new(m, nconmax, njmax);
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -1631,6 +1636,7 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
   memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
   d->time = time;
   d->qacc_given = qacc;
+  d->qfrc_constraint_given = qfrc_constraint;
   orc_step(m, d);
   if (out_qpos) memcpy(out_qpos, d->qpos, sizeof(double) * m->nq);
   if (out_qvel) memcpy(out_qvel, d->qvel, sizeof(double) * m->nv);
@@ -1638,6 +1644,56 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
   if (out_qfrc_constraint) memcpy(out_qfrc_constraint, d->qfrc_constraint, sizeof(double) * m->nv);
   if (out_cost) *out_cost = d->cost;
   int ov = d->overflow;
+  orc_data_free(d);
+  return ov;
+}
+
+int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                         double time, double* out_scale) {
+  orcData* d = orc_data_new(m, nconmax, njmax);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_warmstart, sizeof(double) * m->nv);
+  memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+  d->time = time;
+  orc_forward(m, d);
+  const int nv = m->nv;
+  double* H = (double*)calloc((size_t)nv * nv * 2 + 2 * nv, sizeof(double));
+  double* Hinv = H + nv * nv;
+  double* a = Hinv + nv * nv;
+  double* col = a + nv;
+  memcpy(H, d->qM, sizeof(double) * nv * nv);
+  for (int i = 0; i < nv; i++) {
+    double s = fabs(d->qfrc_smooth[i]);
+    for (int k = 0; k < nv; k++) s += fabs(d->qM[i * nv + k] * d->qacc[k]);
+    a[i] = s;
+  }
+  for (int r = 0; r < d->nefc; r++) {
+    const double* J = d->efc_J + (size_t)r * nv;
+    double v = -d->efc_aref[r];
+    for (int i = 0; i < nv; i++) v += J[i] * d->qacc[i];
+    if (v >= 0) continue;
+    const double Dr = d->efc_D[r];
+    for (int i = 0; i < nv; i++) {
+      if (J[i] == 0) continue;
+      a[i] += fabs(J[i] * Dr * v);
+      for (int j = 0; j < nv; j++) H[i * nv + j] += J[i] * Dr * J[j];
+    }
+  }
+  chol(H, nv);
+  for (int j = 0; j < nv; j++) {
+    for (int i = 0; i < nv; i++) col[i] = i == j ? 1.0 : 0.0;
+    chol_solve(H, nv, col);
+    for (int i = 0; i < nv; i++) Hinv[i * nv + j] = col[i];
+  }
+  for (int i = 0; i < nv; i++) {
+    double s = 0;
+    for (int j = 0; j < nv; j++) s += fabs(Hinv[i * nv + j]) * a[j];
+    out_scale[i] = s;
+  }
+  int ov = d->overflow;
+  free(H);
   orc_data_free(d);
   return ov;
 }

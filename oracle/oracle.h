@@ -53,6 +53,7 @@ typedef struct {
   /* when set: the constraint stage takes qacc from here instead of running the Newton
    * solver (forces, qfrc_constraint and the integration follow from it) */
   const double* qacc_given;
+  const double* qfrc_constraint_given;  /* with qacc_given: the integration uses this */
   double cost;  /* the constraint-problem cost at the final qacc (Gauss + active rows) */
   /* scratch */
   double* work;
@@ -91,8 +92,18 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
  * separately through qacc). */
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                        double time, const double* qacc, double* out_qpos, double* out_qvel,
-                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost);
+                        double time, const double* qacc, const double* qfrc_constraint,
+                        double* out_qpos, double* out_qvel, double* out_sensordata,
+                        double* out_qfrc_constraint, double* out_cost);
+
+/* fp32 error scale of the Newton solution: mj_forward (fp64 solve), then at the solution
+ * x the Hessian H = M + J_a^T D_a J_a of the active rows and, per dof j, the magnitude of
+ * the gradient's terms a_j = sum_r |J_rj D_r jar_r| + sum_k |M_jk x_k| + |qfrc_smooth_j|
+ * (what an fp32 gradient evaluation rounds); out_scale[i] = sum_j |H^-1_ij| a_j.  A solver
+ * whose gradient is exact to eps relative to its terms lands within eps * out_scale of x. */
+int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
+                         double time, double* out_scale);
 
 #ifdef __cplusplus
 }

@@ -2,7 +2,7 @@
 libamdhip64), without torch.cuda.graph, printing after every stage: locates the crash that
 torch.cuda.graph capture of MJX355_SPLIT=2 + row classes hits (tests/test_gpu_split.py).
 
-usage: python scripts/capture_probe_engine.py <split> <row_classes> [capture_mode 0|1|2]
+usage: python scripts/capture_probe_engine.py <split> <row_classes> [capture_mode 0|1|2] [nsub] [pipe 0|1]
 """
 import ctypes
 import os
@@ -14,6 +14,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 split = sys.argv[1] if len(sys.argv) > 1 else "2"
 classes = sys.argv[2] if len(sys.argv) > 2 else "24"
 mode = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+nsub = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+os.environ["MJX355_CLASS_PIPE"] = sys.argv[5] if len(sys.argv) > 5 else "1"
 os.environ["MJX355_SPLIT"] = split
 os.environ["MJX355_ROW_CLASSES"] = classes
 
@@ -47,17 +49,17 @@ def load():
 
 
 load()
-sim.step(nsubstep=3)
+sim.step(nsubstep=nsub)
 torch.cuda.synchronize()
 ref = sim.data.qpos.cpu().numpy().copy()
-say(f"eager ok: split={split} classes={classes} mode={mode}")
+say(f"eager ok: split={split} classes={classes} mode={mode} nsub={nsub} pipe={os.environ['MJX355_CLASS_PIPE']}")
 load()
 torch.cuda.synchronize()
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
   h = vp(s.cuda_stream)
   say("begin capture rc", hip.hipStreamBeginCapture(h, ctypes.c_int(mode)))
-  sim.step(nsubstep=3)
+  sim.step(nsubstep=nsub)
   g = vp()
   say("launches enqueued; end capture ...")
   say("end capture rc", hip.hipStreamEndCapture(h, ctypes.byref(g)))

@@ -77,10 +77,12 @@ def forward(model, qpos, qvel=None, qacc_warmstart=None, ctrl=None, time=0.0, st
   return out
 
 
-def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, nconmax=256, njmax=1024):
+def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, qfrc_constraint=None,
+                    nconmax=256, njmax=1024):
   """One mj_step whose constraint stage takes `qacc` instead of solving for it (forces,
-  qfrc_constraint, sensors and the integration follow from it), plus the constraint
-  problem's cost at that qacc.  Single world; returns a dict of fp64 arrays."""
+  qfrc_constraint, sensors and the integration follow from it; with `qfrc_constraint` the
+  integration uses that instead), plus the constraint problem's cost at that qacc.  Single
+  world; returns a dict of fp64 arrays."""
   desc, keep = make_desc(model)
   f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
   nq, nv, nu, ns = model.nq, model.nv, model.nu, model.nsensordata
@@ -89,12 +91,27 @@ def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, nconmax
   cost = ctypes.c_double()
   a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
   g = f64(qacc, nv)
+  fc = None if qfrc_constraint is None else f64(qfrc_constraint, nv)
   ov = lib().orc_step_given_qacc(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
-                                 ctypes.c_double(time), _p(g), _p(out["qpos"]), _p(out["qvel"]),
+                                 ctypes.c_double(time), _p(g), _p(fc), _p(out["qpos"]), _p(out["qvel"]),
                                  _p(out["sensordata"]), _p(out["qfrc_constraint"]), ctypes.byref(cost))
   del keep
   out["sensordata"] = out["sensordata"][:ns]
   out["cost"], out["overflow"] = cost.value, ov
+  return out
+
+
+def qacc_error_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256, njmax=1024):
+  """Per-dof fp32 error scale of the Newton solution (orc_qacc_error_scale): |H^-1| times
+  the magnitudes of the gradient's terms at the fp64 solution."""
+  desc, keep = make_desc(model)
+  f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
+  nq, nv, nu = model.nq, model.nv, model.nu
+  out = np.zeros(nv)
+  a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
+  lib().orc_qacc_error_scale(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
+                             ctypes.c_double(time), _p(out))
+  del keep
   return out
 
 
