@@ -43,18 +43,26 @@ __global__ void work_args(const int* p, int w0, int w1, int sel, int last, int i
   if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(slot, 1);
 }
 
+// Also built as a shared library (-DPROBE_LIB, scripts/capture_probe_torch.py): probe_run()
+// runs the same capture inside a process that has initialised torch, on torch's stream.
+static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, hipStream_t given);
+#ifdef PROBE_LIB
+extern "C" int probe_run(int nsplit, int nc, int nsub, int piped, int shared, int feat, void* stream) {
+  return probe(nsplit, nc, nsub, piped, shared, feat, (hipStream_t)stream);
+}
+#else
 int main(int argc, char** argv) {
-  const int nsplit = argc > 1 ? atoi(argv[1]) : 2;
-  const int nc = argc > 2 ? atoi(argv[2]) : 1;
-  const int nsub = argc > 3 ? atoi(argv[3]) : 3;
-  const int piped = argc > 4 ? atoi(argv[4]) : 1;
-  const int shared = argc > 5 ? atoi(argv[5]) : 0;
-  const int feat = argc > 6 ? atoi(argv[6]) : 0;
+  return probe(argc > 1 ? atoi(argv[1]) : 2, argc > 2 ? atoi(argv[2]) : 1, argc > 3 ? atoi(argv[3]) : 3,
+               argc > 4 ? atoi(argv[4]) : 1, argc > 5 ? atoi(argv[5]) : 0, argc > 6 ? atoi(argv[6]) : 0,
+               nullptr);
+}
+#endif
+static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, hipStream_t given) {
   printf("probe: nsplit=%d nclass=%d nsub=%d piped=%d shared_class_streams=%d features=%d\n", nsplit,
          nc, nsub, piped, shared, feat);
   fflush(stdout);
-  hipStream_t origin;
-  CK(hipStreamCreateWithFlags(&origin, hipStreamNonBlocking));
+  hipStream_t origin = given;
+  if (!origin) CK(hipStreamCreateWithFlags(&origin, hipStreamNonBlocking));
   std::vector<hipStream_t> split(nsplit);
   std::vector<hipEvent_t> split_join(nsplit);
   hipEvent_t split_fork;

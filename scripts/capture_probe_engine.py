@@ -2,7 +2,8 @@
 libamdhip64), without torch.cuda.graph, printing after every stage: locates the crash that
 torch.cuda.graph capture of MJX355_SPLIT=2 + row classes hits (tests/test_gpu_split.py).
 
-usage: python scripts/capture_probe_engine.py <split> <row_classes> [capture_mode 0|1|2] [nsub] [pipe 0|1]
+usage: python scripts/capture_probe_engine.py <split> <row_classes> [capture_mode 0|1|2] [nsub] [pipe 0|1] [hip_origin 0|1]
+hip_origin=1: the capture origin is a stream made by hipStreamCreateWithFlags, not by torch.
 """
 import ctypes
 import os
@@ -55,7 +56,13 @@ ref = sim.data.qpos.cpu().numpy().copy()
 say(f"eager ok: split={split} classes={classes} mode={mode} nsub={nsub} pipe={os.environ['MJX355_CLASS_PIPE']}")
 load()
 torch.cuda.synchronize()
-s = torch.cuda.Stream()
+hip_origin = len(sys.argv) > 6 and sys.argv[6] == "1"
+if hip_origin:
+  hs = vp()
+  say("hipStreamCreateWithFlags rc", hip.hipStreamCreateWithFlags(ctypes.byref(hs), ctypes.c_uint(1)))
+  s = torch.cuda.ExternalStream(hs.value)
+else:
+  s = torch.cuda.Stream()
 with torch.cuda.stream(s):
   h = vp(s.cuda_stream)
   say("begin capture rc", hip.hipStreamBeginCapture(h, ctypes.c_int(mode)))
