@@ -1650,7 +1650,7 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
 
 int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                          const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                         double time, double* out_scale) {
+                         double time, double* out_scale, double* out_vscale) {
   orcData* d = orc_data_new(m, nconmax, njmax);
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -1691,6 +1691,48 @@ int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const do
     double s = 0;
     for (int j = 0; j < nv; j++) s += fabs(Hinv[i * nv + j]) * a[j];
     out_scale[i] = s;
+  }
+  if (out_vscale) {
+    /* A = M + h D as orc_step builds it (implicitfast: damping and actuator velocity
+     * derivatives on the diagonal), its inverse, and the update dv = h A^-1 f */
+    const double h = m->timestep;
+    double* A = H;  /* reuse */
+    memcpy(A, d->qM, sizeof(double) * nv * nv);
+    for (int i = 0; i < nv; i++) if (m->dof_damping[i] > 0) A[i * nv + i] += h * m->dof_damping[i];
+    if (m->integrator == MJX_INT_IMPLICITFAST)
+      for (int u = 0; u < m->nu; u++) {
+        if (m->actuator_forcelimited[u]) {
+          double fo = d->actuator_force[u];
+          if (fo <= m->actuator_forcerange[2 * u] || fo >= m->actuator_forcerange[2 * u + 1]) continue;
+        }
+        double bv = m->actuator_biasprm[3 * u + 2];
+        if (bv == 0) continue;
+        int dof = m->jnt_dofadr[m->actuator_trnid[u]];
+        A[dof * nv + dof] -= h * m->actuator_gear[u] * m->actuator_gear[u] * bv;
+      }
+    double* Af = (double*)malloc(sizeof(double) * (nv * nv + 2 * nv));
+    double* dv = Af + nv * nv;
+    double* t = dv + nv;
+    memcpy(Af, A, sizeof(double) * nv * nv);
+    chol(Af, nv);
+    for (int i = 0; i < nv; i++) dv[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
+    chol_solve(Af, nv, dv);
+    for (int j = 0; j < nv; j++) {
+      double s = fabs(d->qfrc_smooth[j]) + fabs(d->qfrc_constraint[j]);
+      for (int k = 0; k < nv; k++) s += fabs(A[j * nv + k] * dv[k]);
+      t[j] = s;
+    }
+    for (int j = 0; j < nv; j++) {
+      for (int i = 0; i < nv; i++) col[i] = i == j ? 1.0 : 0.0;
+      chol_solve(Af, nv, col);
+      for (int i = 0; i < nv; i++) Hinv[i * nv + j] = col[i];
+    }
+    for (int i = 0; i < nv; i++) {
+      double s = 0;
+      for (int j = 0; j < nv; j++) s += fabs(Hinv[i * nv + j]) * t[j];
+      out_vscale[i] = h * s;
+    }
+    free(Af);
   }
   int ov = d->overflow;
   free(H);

@@ -100,10 +100,13 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
  * x the Hessian H = M + J_a^T D_a J_a of the active rows and, per dof j, the magnitude of
  * the gradient's terms a_j = sum_r |J_rj D_r jar_r| + sum_k |M_jk x_k| + |qfrc_smooth_j|
  * (what an fp32 gradient evaluation rounds); out_scale[i] = sum_j |H^-1_ij| a_j.  A solver
- * whose gradient is exact to eps relative to its terms lands within eps * out_scale of x. */
+ * whose gradient is exact to eps relative to its terms lands within eps * out_scale of x.
+ * out_vscale (may be NULL): the same for the implicit integration's velocity update,
+ * h * sum_j |A^-1_ij| (|qfrc_smooth_j| + |qfrc_constraint_j| + sum_k |A_jk dv_k|) with
+ * A = M + h D (the implicitfast matrix) and dv the update. */
 int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                          const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                         double time, double* out_scale);
+                         double time, double* out_scale, double* out_vscale);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,11 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+T="--timeout 300 --timeout-method thread"
+MJX_PARITY_SOFT=1 MJX_PARITY_STATS=gpurun_out/parity4 timeout -k 10 900 python -u -m pytest \
+  tests/test_gpu_rollout_parity.py -x -v -s $T > gpurun_out/r03_parity4.log 2>&1 \
+  || { tail -40 gpurun_out/r03_parity4.log; exit 1; }
+tail -3 gpurun_out/r03_parity4.log
 MJX355_STAMP_MINROWS=61 timeout -k 10 300 python -u scripts/stage_profile.py > gpurun_out/r03_stamps_heavy.log 2>&1 \
   || { tail -20 gpurun_out/r03_stamps_heavy.log; exit 1; }
 timeout -k 10 300 python -u scripts/stage_profile.py > gpurun_out/r03_stamps_all.log 2>&1 \

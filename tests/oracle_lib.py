@@ -102,17 +102,19 @@ def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, qfrc_co
 
 
 def qacc_error_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256, njmax=1024):
-  """Per-dof fp32 error scale of the Newton solution (orc_qacc_error_scale): |H^-1| times
-  the magnitudes of the gradient's terms at the fp64 solution."""
+  """Per-dof fp32 error scales (orc_qacc_error_scale): of the Newton solution, |H^-1| times
+  the magnitudes of the gradient's terms at the fp64 solution; and of the implicitfast
+  velocity update, h |A^-1| times the magnitudes of its right-hand side's terms.  Returns
+  (qacc_scale, qvel_scale)."""
   desc, keep = make_desc(model)
   f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
   nq, nv, nu = model.nq, model.nv, model.nu
-  out = np.zeros(nv)
+  out, vout = np.zeros(nv), np.zeros(nv)
   a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
   lib().orc_qacc_error_scale(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
-                             ctypes.c_double(time), _p(out))
+                             ctypes.c_double(time), _p(out), _p(vout))
   del keep
-  return out
+  return out, vout
 
 
 def rollout(model, qpos, qvel, qacc_warmstart, ctrl, time, nstep, nconmax=256, njmax=1024,
