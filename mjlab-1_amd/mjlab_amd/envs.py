@@ -481,14 +481,23 @@ def unitree_g1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/g1/env_cfgs.py:20-148` (rough): the flat G1 task on the
   box-stair terrain grid in curriculum layout (`velocity_env_cfg.py:318-324`,
   max_init_terrain_level 5) with the terrain-level curriculum
-  (`velocity_env_cfg.py:296-300`).  Play mode keeps the training terrain (the
-  reference re-generates a smaller random grid for play)."""
-  cfg = _g1_velocity_cfg("g1_velocity_rough", play)
+  (`velocity_env_cfg.py:296-300`).  Play mode: the random-layout 5 x 5 grid and the
+  randomize_terrain reset event (`tasks/velocity/config/g1/env_cfgs.py:131-148`)."""
+  cfg = _g1_velocity_cfg("g1_velocity_rough_play" if play else "g1_velocity_rough", play)
   cfg.scene.max_init_terrain_level = 5
   cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
                                                         params={"command_name": "twist"}),
                     **cfg.curriculum}
+  if play:
+    _rough_play_events(cfg)
   return cfg
+
+
+def _rough_play_events(cfg) -> None:
+  """Play mode of the rough tasks (`tasks/velocity/config/{g1,go1}/env_cfgs.py`, play
+  overrides): every reset puts the env on a random sub-terrain (`randomize_terrain`); the
+  scene is the random-layout 5 x 5 grid with a 10 m border (scenes._rough_play_cfg)."""
+  cfg.events["randomize_terrain"] = EventTermCfg(func=mdp.randomize_terrain, mode="reset", params={})
 
 
 def _g1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
@@ -541,11 +550,13 @@ def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
 def unitree_go1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/go1/env_cfgs.py:15-112` (rough): the flat Go1 task on the
   curriculum box-stair grid with the terrain-level curriculum (as unitree_g1_rough_env_cfg)."""
-  cfg = _go1_velocity_cfg("go1_velocity_rough", play)
+  cfg = _go1_velocity_cfg("go1_velocity_rough_play" if play else "go1_velocity_rough", play)
   cfg.scene.max_init_terrain_level = 5
   cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
                                                         params={"command_name": "twist"}),
                     **cfg.curriculum}
+  if play:
+    _rough_play_events(cfg)
   return cfg
 
 

@@ -556,6 +556,26 @@ def randomize_field(env, env_ids, field: str, ranges, distribution: str = "unifo
     t[eg, ig] = rnd
 
 
+def randomize_terrain(env, env_ids):
+  """`envs/mdp/events.py:26-37`: a random sub-terrain (level row and type column) for each
+  resetting env (play / evaluation mode)."""
+  terrain = env.scene.terrain
+  if terrain is None:
+    return
+  if env_ids is None:
+    env_ids = torch.arange(env.num_envs, device=env.device)
+  terrain.randomize_env_origins(env_ids)
+
+
+def _randomize_terrain_masked(env, mask):
+  terrain = env.scene.terrain
+  if terrain is not None:
+    terrain.randomize_env_origins_masked(mask)
+
+
+randomize_terrain.masked = _randomize_terrain_masked
+
+
 def randomize_encoder_bias(env, env_ids, bias_range, asset_cfg=_ROBOT):
   """`envs/mdp/events.py:709-745`: per-env joint encoder offsets (read by
   joint_pos_rel(biased=True) and subtracted by the joint-position action)."""

@@ -627,6 +627,20 @@ class Terrain:
       from ._lib import MjxError
       raise MjxError(L.mjx_task_last_error().decode())
 
+  def randomize_env_origins_masked(self, mask) -> None:
+    """randomize_env_origins over a reset mask (sync-free, graph-capturable): every env
+    draws, the unmasked keep their level, type and origin."""
+    rows, cols = self.terrain_origins.shape[:2]
+    n = self.env_origins.shape[0]
+    dev = self.env_origins.device
+    lv = torch.randint(0, rows, (n,), device=dev)
+    ty = torch.randint(0, cols, (n,), device=dev)
+    self.terrain_levels.copy_(torch.where(mask, lv, self.terrain_levels))
+    self.terrain_types.copy_(torch.where(mask, ty, self.terrain_types))
+    self.env_origins.copy_(torch.where(mask.unsqueeze(1),
+                                       self.terrain_origins[self.terrain_levels, self.terrain_types],
+                                       self.env_origins))
+
   def randomize_env_origins(self, env_ids) -> None:
     """`terrain_importer.py:203-222` (play mode)."""
     rows, cols = self.terrain_origins.shape[:2]

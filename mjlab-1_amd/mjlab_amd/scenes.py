@@ -134,6 +134,35 @@ def build_g1_velocity_rough(xml_path: str) -> Model:
   return m
 
 
+def _rough_play_cfg():
+  """The play-mode terrain of the rough velocity tasks (`tasks/velocity/config/g1/env_cfgs.py:
+  131-148`, go1 likewise): curriculum off (random sub-terrain per patch), 5 x 5 patches, 10 m
+  border.  The reference draws the generator seed at random; the compiled asset fixes it."""
+  from .terrains import rough_terrains_cfg
+  return rough_terrains_cfg(seed=0, curriculum=False, num_rows=5, num_cols=5, border_width=10.0)
+
+
+def build_g1_velocity_rough_play(xml_path: str) -> Model:
+  from .terrains import TerrainGenerator
+  cfg = _rough_play_cfg()
+  geoms, origins = TerrainGenerator(cfg).generate()
+  m = compile_scene([_g1_entity(xml_path)], terrain="generator", terrain_geoms=geoms,
+                    contact_sensors=_g1_contact_sensors(), **VELOCITY_SIM)
+  m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  m.arrays["terrain_size"] = np.asarray(cfg.size, np.float64)
+  return m
+
+
+def build_go1_velocity_rough_play(xml_path: str) -> Model:
+  from .terrains import TerrainGenerator
+  cfg = _rough_play_cfg()
+  geoms, origins = TerrainGenerator(cfg).generate()
+  m = build_go1_velocity(xml_path, terrain="generator", terrain_geoms=geoms)
+  m.arrays["terrain_origins"] = np.asarray(origins, np.float64)
+  m.arrays["terrain_size"] = np.asarray(cfg.size, np.float64)
+  return m
+
+
 SCENE_BUILDERS = {
   "g1_velocity": ("unitree_g1/xmls/g1.xml", build_g1_velocity),
   "g1_tracking": ("unitree_g1/xmls/g1.xml", build_g1_tracking),
@@ -142,6 +171,8 @@ SCENE_BUILDERS = {
   "go1_velocity": ("unitree_go1/xmls/go1.xml", build_go1_velocity),
   "g1_velocity_rough": ("unitree_g1/xmls/g1.xml", build_g1_velocity_rough),
   "go1_velocity_rough": ("unitree_go1/xmls/go1.xml", build_go1_velocity_rough),
+  "g1_velocity_rough_play": ("unitree_g1/xmls/g1.xml", build_g1_velocity_rough_play),
+  "go1_velocity_rough_play": ("unitree_go1/xmls/go1.xml", build_go1_velocity_rough_play),
 }
 
 

@@ -377,13 +377,17 @@ class TerrainGenerator:
     return self.geoms, self.terrain_origins
 
 
-def rough_terrains_cfg(seed: int | None = None, curriculum: bool = False) -> TerrainGeneratorCfg:
+def rough_terrains_cfg(seed: int | None = None, curriculum: bool = False, num_rows: int = 10,
+                       num_cols: int = 20, border_width: float = 20.0) -> TerrainGeneratorCfg:
   """ROUGH_TERRAINS_CFG (`terrains/config.py:7-57`): 8 m x 8 m patches, 10 x 20 grid, 20 m
   border; 40% flat boxes, 30% pyramid stairs, 30% inverted pyramid stairs (its heightfield
-  entries are commented out in the reference)."""
+  entries are commented out in the reference).  Play mode
+  (`tasks/velocity/config/{g1,go1}/env_cfgs.py`, play overrides) asks for the random layout
+  (curriculum off) on a 5 x 5 grid with a 10 m border."""
   stairs = dict(step_height_range=(0.0, 0.1), step_width=0.3, platform_width=3.0, border_width=1.0)
   return TerrainGeneratorCfg(
-    seed=seed, curriculum=curriculum, size=(8.0, 8.0), border_width=20.0, num_rows=10, num_cols=20,
+    seed=seed, curriculum=curriculum, size=(8.0, 8.0), border_width=border_width,
+    num_rows=num_rows, num_cols=num_cols,
     sub_terrains={
       "flat": BoxFlatTerrainCfg(proportion=0.4),
       "pyramid_stairs": BoxPyramidStairsTerrainCfg(proportion=0.3, **stairs),
