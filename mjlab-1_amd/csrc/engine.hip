@@ -189,6 +189,89 @@ hipError_t prepare_step(const Params& host) {
   return hipSuccess;
 }
 
+// Batch split together with Newton row classes: every fork starts from the launch stream
+// and every side stream joins back into it before the next fork ("flat" fork / join).  Per
+// substep: [A of each split, classify] on the split streams, join; [each split's class
+// chains (B, and piped C + next A) on the class streams, the smallest class on the split
+// stream], join.  A fork from one side stream to another (split stream -> its class
+// streams, the natural nesting) crashes hipStreamEndCapture under the HIP runtime torch
+// bundles (a synthetic probe with no engine code reproduces it in a torch process and not
+// standalone on ROCm 7.2: scripts/capture_probe*.{hip,py}), and the
+// flat form keeps the capture to the fork / join shape the unsplit class path uses.
+static hipError_t launch_split_classes(const Params& host, const Params* dev, int nworld,
+                                       int nsubstep, int integrate, hipStream_t stream,
+                                       const SideStream* side, int nsplit, bool piped) {
+  const StepFn fA = step_fn(host, 0), fB = step_fn(host, 1), fC = step_fn(host, 2);
+  const int nc = host.nrowclass;
+  hipStream_t sst[kMaxSplit];
+  int wb[kMaxSplit + 1];
+  for (int k = 0; k <= nsplit; k++) wb[k] = (int)(((long long)nworld * k) / nsplit);
+  sst[0] = stream;
+  for (int k = 1; k < nsplit; k++) sst[k] = side->split[k];
+  hipError_t e = hipSuccess;
+  auto fork_all = [&](bool classes) {
+    e = hipEventRecord(side->split_fork, stream);
+    for (int k = 1; k < nsplit && e == hipSuccess; k++) e = hipStreamWaitEvent(sst[k], side->split_fork, 0);
+    for (int k = 0; k < nsplit && classes; k++)
+      for (int c = 0; c < nc && e == hipSuccess; c++)
+        e = hipStreamWaitEvent(side->stream[k][c], side->split_fork, 0);
+    return e;
+  };
+  auto join_all = [&](bool classes) {
+    for (int k = 0; k < nsplit && classes; k++)
+      for (int c = 0; c < nc && e == hipSuccess; c++) {
+        e = hipEventRecord(side->join[k][c], side->stream[k][c]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->join[k][c], 0);
+      }
+    for (int k = 1; k < nsplit && e == hipSuccess; k++) {
+      e = hipEventRecord(side->split_join[k], sst[k]);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream, side->split_join[k], 0);
+    }
+    return e;
+  };
+  for (int sub = 0; sub < nsubstep; sub++) {
+    const int last = sub == nsubstep - 1;
+    if (fork_all(false) != hipSuccess) return e;
+    for (int k = 0; k < nsplit; k++) {
+      const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
+      if (n <= 0) continue;
+      if (!piped || sub == 0)
+        hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), sst[k], dev, w0, w1, k,
+                           last, integrate, nullptr);
+      hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, sst[k], dev, w0, w1,
+                         k, nullptr);
+    }
+    if (join_all(false) != hipSuccess || fork_all(true) != hipSuccess) return e;
+    for (int k = 0; k < nsplit; k++) {
+      const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
+      if (n <= 0) continue;
+      auto class_chain = [&](hipStream_t cs, int cls) {
+        hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1), cs, dev,
+                           w0, w1, k, last, cls, nullptr);
+        if (!piped) return;
+        hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
+                           k | (cls + 1) << 8, last, integrate, nullptr);
+        if (!last)
+          hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
+                             k | (cls + 1) << 8, sub + 1 == nsubstep - 1, integrate, nullptr);
+      };
+      for (int c = 0; c < nc; c++) class_chain(side->stream[k][c], c == 0 ? 0 : nc + 1 - c);
+      class_chain(sst[k], 1);
+    }
+    if (join_all(true) != hipSuccess) return e;
+    if (piped) continue;
+    if (fork_all(false) != hipSuccess) return e;
+    for (int k = 0; k < nsplit; k++) {
+      const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
+      if (n > 0)
+        hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), sst[k], dev, w0, w1, k,
+                           last, integrate, nullptr);
+    }
+    if (join_all(false) != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side) {
@@ -200,9 +283,15 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   // its own stream.  The ranges are independent, so one range's launches fill the tail of
   // the other's (the last, partly filled round of workgroups per CU) and the launch gaps.
   // Measured: Go1 8192 worlds 4.91 -> 5.61 M env-steps/s at 2 splits (3: 5.47, 4: 5.38).
-  // With row classes each split forks its own class streams (SideStream); the default for
-  // those models is one split (capi.cpp).  Masked forwards (reset worlds) stay one launch set.
+  // With row classes: launch_split_classes (flat fork / join); the default for those models
+  // is one split (capi.cpp).  Masked forwards (reset worlds) stay one launch set.
   const int nsplit = (!mask && side) ? std::max(1, std::min(side->nsplit, kMaxSplit)) : 1;
+  static const bool pipe = [] {
+    const char* e = getenv("MJX355_CLASS_PIPE");
+    return !e || atoi(e) != 0;
+  }();
+  if (nsplit > 1 && nc > 0)
+    return launch_split_classes(host, dev, nworld, nsubstep, integrate, stream, side, nsplit, pipe);
   hipStream_t sst[kMaxSplit];
   int wb[kMaxSplit + 1];
   for (int k = 0; k <= nsplit; k++) wb[k] = (int)(((long long)nworld * k) / nsplit);
@@ -221,10 +310,6 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   // so the bulk class's C and next A overlap the heavy class's Newton tail; the streams
   // join before the next classify.  MJX355_CLASS_PIPE=0: phase C / A over every world
   // after the join (diagnostic).
-  static const bool pipe = [] {
-    const char* e = getenv("MJX355_CLASS_PIPE");
-    return !e || atoi(e) != 0;
-  }();
   for (int sub = 0; sub < nsubstep; sub++) {
     const int last = sub == nsubstep - 1;
     for (int k = 0; k < nsplit; k++) {

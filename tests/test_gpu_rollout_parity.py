@@ -123,7 +123,8 @@ def _select(env, rng):
 
 
 _STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time")
-_OUT = ("qacc", "qfrc_constraint", "sensordata", "ncon", "nefc", "solver_niter", "contact_dist")
+_OUT = ("qacc", "qfrc_constraint", "qfrc_smooth", "actuator_force", "sensordata", "ncon", "nefc",
+        "solver_niter", "contact_dist")
 
 
 def _snap(sim, sel, keys):
@@ -197,6 +198,15 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
   ev = np.abs(st1["qvel"][i] - itg["qvel"])
   vb = QVEL_FLOOR + QVEL_EPS_MUL * FP32_EPS * (vscale + np.abs(st0["qvel"][i]))
   stats["qvel_ratio"] = max(stats["qvel_ratio"], float((ev / vb).max()))
+  if not (ev <= vb).all() and len(stats.setdefault("qvel_detail", [])) < 12:
+    j = int(np.argmax(ev / vb))
+    fs_o = ol.forward(m, *args[:4], args[4], step=False, nconmax=sim.nconmax, njmax=sim.njmax)
+    stats["qvel_detail"].append(dict(
+      where=where, dof=j, err=float(ev[j]), bound=float(vb[j]), vscale=float(vscale[j]),
+      qfrc_smooth_gpu=float(out["qfrc_smooth"][i][j]),
+      qfrc_smooth_err=float(np.abs(out["qfrc_smooth"][i] - (fs_o["qacc_smooth"] @ fs_o["qM"].T)).max()),
+      act_force_err=float(np.abs(out["actuator_force"][i] - fs_o["actuator_force"]).max()),
+      qvel_in=float(st0["qvel"][i][j]), dv=float(itg["qvel"][j] - st0["qvel"][i][j])))
   _expect((ev <= vb).all(), f"{where}: qvel err {ev.max():.3e} (dof {int(np.argmax(ev / vb))})", stats)
   ep = np.abs(st1["qpos"][i] - itg["qpos"])
   pb = QPOS_ABS + QPOS_ULPS * np.abs(itg["qpos"]) + m.timestep * vb.max()
