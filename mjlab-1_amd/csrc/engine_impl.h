@@ -86,6 +86,22 @@ __device__ __forceinline__ void qmat(float* M, Q4 q) {
   M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
   M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
 }
+// entry t (row-major) of qmat(M, q), same arithmetic
+__device__ __forceinline__ float qmat_elem(Q4 q, int t) {
+  q = qnorm(q);
+  const float w = q.w, x = q.x, y = q.y, z = q.z;
+  switch (t) {
+    case 0: return 1 - 2 * (y * y + z * z);
+    case 1: return 2 * (x * y - w * z);
+    case 2: return 2 * (x * z + w * y);
+    case 3: return 2 * (x * y + w * z);
+    case 4: return 1 - 2 * (x * x + z * z);
+    case 5: return 2 * (y * z - w * x);
+    case 6: return 2 * (x * z - w * y);
+    case 7: return 2 * (y * z + w * x);
+    default: return 1 - 2 * (x * x + y * y);
+  }
+}
 // q v q* for a unit quaternion (18 FMAs, no normalisation)
 __device__ __forceinline__ V3 qrot(Q4 q, V3 v) {
   const V3 u = {q.x, q.y, q.z};
@@ -671,6 +687,13 @@ __device__ __forceinline__ CFrame cframe(V3 n) {
   f.t = t * (1.0f / fmaxf(norm(t), MINVAL));
   f.b = cross(n, f.t);
   return f;
+}
+// entry t (row-major: n, t, b) of the contact frame rebuilt from the unit normal n
+__device__ __forceinline__ float cframe_elem(V3 n, int t) {
+  const CFrame F = cframe(n);
+  const V3 r = t < 3 ? F.n : t < 6 ? F.t : F.b;
+  const int k = t - 3 * (t / 3);
+  return k == 0 ? r.x : k == 1 ? r.y : r.z;
 }
 // F^T v for the contact frame F rebuilt from the unit normal at np (the C pack carries the
 // normals only)
@@ -2483,30 +2506,30 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
         D.subtree_com[wb * 3 + i] = S[L.subtree_com + i];
       }
       for (int i = lane; i < 4 * nb; i += kWave) D.xquat[wb * 4 + i] = S[L.xquat + i];
-      if (bl) {  // lane per body: xmat and ximat from the quaternions
-        float R[9], Ri[9];
-        qmat(R, xq);
-        qmat(Ri, qmul(xq, B.iquat));
-        float* om = D.xmat + (wb + B.b) * 9;
-        float* oi = D.ximat + (wb + B.b) * 9;
-#pragma unroll
-        for (int t = 0; t < 9; t++) { om[t] = R[t]; oi[t] = Ri[t]; }
+      // element-parallel (lane per output float): consecutive lanes store consecutive words,
+      // where a lane per body / geom / contact storing its 9 (or 3) floats at a 36-byte lane
+      // stride touches ~9x the cache lines per store instruction
+      for (int i = lane; i < 9 * nb; i += kWave) {  // xmat / ximat from the quaternions
+        const int b = i / 9, t = i - 9 * b;
+        const Q4 q = q4(S + L.xquat + 4 * b);
+        D.xmat[wb * 9 + i] = qmat_elem(q, t);
+        D.ximat[wb * 9 + i] = qmat_elem(qmul(q, q4(body_iquat + 4 * b)), t);
       }
       for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
-      // lane per geom: one model-index load per lane up front, not one per element (a
-      // dependent global load in every iteration of an element loop serialises on latency);
-      // heightfield frames are static (set at sim creation)
+      // heightfield / terrain-box frames are static (set at sim creation)
       size_t wg = (size_t)w * d.ngeom;
-      for (int i = lane; i < d.ngeom_lds; i += kWave) {
-        const size_t g = wg + m.lds_geom[i];
-        const float* xp = S + L.gxpos + 3 * i;
-        const float* xm = S + L.gxmat + 9 * i;
-        float* op = D.geom_xpos + g * 3;
-        float* om = D.geom_xmat + g * 9;
-#pragma unroll
-        for (int t = 0; t < 3; t++) op[t] = xp[t];
-#pragma unroll
-        for (int t = 0; t < 9; t++) om[t] = xm[t];
+      if (d.ngeom_lds == d.ngeom) {  // every geom keeps a frame in LDS, in model order
+        for (int i = lane; i < 3 * d.ngeom; i += kWave) D.geom_xpos[wg * 3 + i] = S[L.gxpos + i];
+        for (int i = lane; i < 9 * d.ngeom; i += kWave) D.geom_xmat[wg * 9 + i] = S[L.gxmat + i];
+      } else {
+        for (int i = lane; i < 3 * d.ngeom_lds; i += kWave) {
+          const int k = i / 3;
+          D.geom_xpos[(wg + m.lds_geom[k]) * 3 + i - 3 * k] = S[L.gxpos + i];
+        }
+        for (int i = lane; i < 9 * d.ngeom_lds; i += kWave) {
+          const int k = i / 9;
+          D.geom_xmat[(wg + m.lds_geom[k]) * 9 + i - 9 * k] = S[L.gxmat + i];
+        }
       }
       size_t ws = (size_t)w * d.nsite;
       for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
@@ -2521,15 +2544,17 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       }
       for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
       size_t wc = (size_t)w * d.nconmax;
-      for (int c = lane; c < d.nconmax; c += kWave) {
-        bool v = c < ncon;
-        D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
-        D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
-        D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
-        for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
-        const CFrame F = cframe(v ? v3(S + L.con_n + 3 * c) : V3{0.f, 0.f, 1.f});
-        const float fr[9] = {F.n.x, F.n.y, F.n.z, F.t.x, F.t.y, F.t.z, F.b.x, F.b.y, F.b.z};
-        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? fr[t] : 0.f;
+      const int C = d.nconmax;
+      for (int c = lane; c < C; c += kWave) D.contact_dist[wc + c] = c < ncon ? S[L.con_dist + c] : 0.f;
+      for (int i = lane; i < 2 * C; i += kWave) {
+        const int c = i >> 1;
+        D.contact_geom[wc * 2 + i] = c < ncon ? Si[(i & 1) ? L.con_g2 + c : L.con_g1 + c] : -1;
+      }
+      for (int i = lane; i < 3 * C; i += kWave)
+        D.contact_pos[wc * 3 + i] = i < 3 * ncon ? S[L.con_pos + i] : 0.f;
+      for (int i = lane; i < 9 * C; i += kWave) {
+        const int c = i / 9;
+        D.contact_frame[wc * 9 + i] = c < ncon ? cframe_elem(v3(S + L.con_n + 3 * c), i - 9 * c) : 0.f;
       }
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
@@ -2989,20 +3014,22 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
       size_t wc = (size_t)w * d.nconmax;
-      for (int c = lane; c < d.nconmax; c += kWave) {
-        V3 f = {0, 0, 0};
+      // element-parallel (lane per output float, coalesced): contact force in its frame
+      for (int i = lane; i < 3 * d.nconmax; i += kWave) {
+        const int c = i / 3, t = i - 3 * c;
+        float f = 0.f;
         if (c < ncon && nefc > 0) {
-          int r0 = Si[L.con_efc + c];
-          if (Si[L.con_dim + c] == 1) f.x = S[L.efc_force + r0];
-          else {
-            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
-            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
-            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+          const int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) {
+            f = t == 0 ? S[L.efc_force + r0] : 0.f;
+          } else {
+            const float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            const float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = t == 0 ? e0 + e1 + e2 + e3 : t == 1 ? (e0 - e1) * S[L.con_mu + 2 * c]
+                                                    : (e2 - e3) * S[L.con_mu + 2 * c + 1];
           }
         }
-        D.contact_force[(wc + c) * 3] = f.x;
-        D.contact_force[(wc + c) * 3 + 1] = f.y;
-        D.contact_force[(wc + c) * 3 + 2] = f.z;
+        D.contact_force[wc * 3 + i] = f;
       }
     }
     // per-world counters, every substep (a fused multi-substep step must not lose the

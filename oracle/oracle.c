@@ -1480,6 +1480,8 @@ void orc_forward(const mjxModelDesc* m, orcData* d) {
 void orc_step(const mjxModelDesc* m, orcData* d) {
   int nv = m->nv;
   orc_forward(m, d);
+  if (d->qacc_given && d->qfrc_smooth_given)  /* orc_step_given_qacc: integrate given forces */
+    memcpy(d->qfrc_smooth, d->qfrc_smooth_given, sizeof(double) * nv);
   double h = m->timestep;
   double* A = (double*)malloc(sizeof(double) * (nv * nv + nv));
   double* f = A + nv * nv;
@@ -1627,8 +1629,8 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
                         double time, const double* qacc, const double* qfrc_constraint,
-                        double* out_qpos, double* out_qvel, double* out_sensordata,
-                        double* out_qfrc_constraint, double* out_cost) {
+                        const double* qfrc_smooth, double* out_qpos, double* out_qvel,
+                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost) {
   orcData* d = orc_data_new(m, nconmax, njmax);
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -1637,6 +1639,7 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
   d->time = time;
   d->qacc_given = qacc;
   d->qfrc_constraint_given = qfrc_constraint;
+  d->qfrc_smooth_given = qfrc_smooth;
   orc_step(m, d);
   if (out_qpos) memcpy(out_qpos, d->qpos, sizeof(double) * m->nq);
   if (out_qvel) memcpy(out_qvel, d->qvel, sizeof(double) * m->nv);

@@ -54,6 +54,7 @@ typedef struct {
    * solver (forces, qfrc_constraint and the integration follow from it) */
   const double* qacc_given;
   const double* qfrc_constraint_given;  /* with qacc_given: the integration uses this */
+  const double* qfrc_smooth_given;      /* with qacc_given: and this */
   double cost;  /* the constraint-problem cost at the final qacc (Gauss + active rows) */
   /* scratch */
   double* work;
@@ -93,8 +94,8 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
                         double time, const double* qacc, const double* qfrc_constraint,
-                        double* out_qpos, double* out_qvel, double* out_sensordata,
-                        double* out_qfrc_constraint, double* out_cost);
+                        const double* qfrc_smooth, double* out_qpos, double* out_qvel,
+                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost);
 
 /* fp32 error scale of the Newton solution: mj_forward (fp64 solve), then at the solution
  * x the Hessian H = M + J_a^T D_a J_a of the active rows and, per dof j, the magnitude of

@@ -78,11 +78,11 @@ def forward(model, qpos, qvel=None, qacc_warmstart=None, ctrl=None, time=0.0, st
 
 
 def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, qfrc_constraint=None,
-                    nconmax=256, njmax=1024):
+                    qfrc_smooth=None, nconmax=256, njmax=1024):
   """One mj_step whose constraint stage takes `qacc` instead of solving for it (forces,
-  qfrc_constraint, sensors and the integration follow from it; with `qfrc_constraint` the
-  integration uses that instead), plus the constraint problem's cost at that qacc.  Single
-  world; returns a dict of fp64 arrays."""
+  qfrc_constraint, sensors and the integration follow from it; with `qfrc_constraint` and
+  `qfrc_smooth` the integration uses those instead), plus the constraint problem's cost at
+  that qacc.  Single world; returns a dict of fp64 arrays."""
   desc, keep = make_desc(model)
   f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
   nq, nv, nu, ns = model.nq, model.nv, model.nu, model.nsensordata
@@ -92,8 +92,9 @@ def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, qfrc_co
   a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
   g = f64(qacc, nv)
   fc = None if qfrc_constraint is None else f64(qfrc_constraint, nv)
+  fs = None if qfrc_smooth is None else f64(qfrc_smooth, nv)
   ov = lib().orc_step_given_qacc(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
-                                 ctypes.c_double(time), _p(g), _p(fc), _p(out["qpos"]), _p(out["qvel"]),
+                                 ctypes.c_double(time), _p(g), _p(fc), _p(fs), _p(out["qpos"]), _p(out["qvel"]),
                                  _p(out["sensordata"]), _p(out["qfrc_constraint"]), ctypes.byref(cost))
   del keep
   out["sensordata"] = out["sensordata"][:ns]

@@ -29,10 +29,12 @@ Checks per shadowed substep (fp32 engine vs fp64 oracle):
     must still be a near-minimiser of the same problem: the problem's fp64 cost at the
     engine's qacc within COST_GAP_REL (relative) of the cost at the oracle's, and the
     mass-matrix energy-norm error sqrt(dq' M dq) / sqrt(q' M q) <= QACC_ENERGY_REL;
-  - the integration: the oracle's step from the engine's own qacc and qfrc_constraint
-    (oracle_lib.step_given_qacc) against the engine's next state -- qvel per dof within
-    QVEL_FLOOR + QVEL_EPS_MUL * eps32 * (v_i + |qvel_i|), v_i the fp32 error scale of the
-    implicitfast update; qpos within QPOS_ABS + 4 fp32 ulps of the coordinate + h * that;
+  - the smooth forces: qfrc_smooth (bias, passive, actuator) per dof within QFRC_ABS +
+    QFRC_REL |f_i| of the oracle's;
+  - the integration: the oracle's step from the engine's own qacc, qfrc_constraint and
+    qfrc_smooth (oracle_lib.step_given_qacc) against the engine's next state -- qvel per dof
+    within QVEL_FLOOR + QVEL_EPS_MUL * eps32 * (v_i + |qvel_i|), v_i the fp32 error scale of
+    the implicitfast update; qpos within QPOS_ABS + 4 fp32 ulps of the coordinate + h * that;
   - sensordata against the oracle's own step within SENS_ABS + SENS_REL |s| (worlds inside
     the solver model);
   - the env step's fused `decimation`-substep mjx_step equal, bit for bit, to that many
@@ -78,6 +80,7 @@ COST_GAP_REL = 1e-3
 QPOS_ABS = 1e-6
 QPOS_ULPS = 2.0 ** -21  # 4 fp32 ulps of the coordinate
 SENS_ABS, SENS_REL = 2e-2, 2e-3
+QFRC_ABS, QFRC_REL = 2e-3, 1e-4
 TIE = 2e-5
 # MJX_PARITY_SOFT=1: record violations in the stats instead of failing (tolerance measurement)
 SOFT = os.environ.get("MJX_PARITY_SOFT", "0") != "0"
@@ -190,11 +193,20 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
     _expect(gap <= COST_GAP_REL and rel_m <= QACC_ENERGY_REL,
             f"{where}: qacc dof {k} err {e[k]:.3e} > fp32 bound {fb[k]:.3e} with cost gap {gap:.2e}, "
             f"energy error {rel_m:.2e}", stats)
-  # (2) the integration: the oracle's step from the engine's own qacc and qfrc_constraint
-  # (the constraint force recomputed from a rounded qacc would carry D * J * dq: stiff rows
-  # amplify an fp32 rounding of qacc many times), within the fp32 error scale of the
+  # (2) the smooth forces: the engine's qfrc_smooth (bias, passive, actuator) against the
+  # oracle's, per dof
+  fs_ref = ref["qM"] @ ref["qacc_smooth"]
+  efs = np.abs(out["qfrc_smooth"][i] - fs_ref)
+  fsb = QFRC_ABS + QFRC_REL * np.abs(fs_ref)
+  stats["qfrc_smooth_ratio"] = max(stats.get("qfrc_smooth_ratio", 0.0), float((efs / fsb).max()))
+  _expect((efs <= fsb).all(), f"{where}: qfrc_smooth dof {int(np.argmax(efs / fsb))} err {efs.max():.3e}", stats)
+  # (3) the integration: the oracle's step from the engine's own qacc, qfrc_constraint and
+  # qfrc_smooth (the constraint force recomputed from a rounded qacc would carry D * J * dq:
+  # stiff rows amplify an fp32 rounding of qacc many times; a small-inertia dof turns the
+  # fp32 error of its smooth force into h * df / A_ii), within the fp32 error scale of the
   # implicitfast velocity update
-  itg = ol.step_given_qacc(m, *args, qa, out["qfrc_constraint"][i], nconmax=sim.nconmax, njmax=sim.njmax)
+  itg = ol.step_given_qacc(m, *args, qa, out["qfrc_constraint"][i], out["qfrc_smooth"][i],
+                           nconmax=sim.nconmax, njmax=sim.njmax)
   ev = np.abs(st1["qvel"][i] - itg["qvel"])
   vb = QVEL_FLOOR + QVEL_EPS_MUL * FP32_EPS * (vscale + np.abs(st0["qvel"][i]))
   stats["qvel_ratio"] = max(stats["qvel_ratio"], float((ev / vb).max()))
