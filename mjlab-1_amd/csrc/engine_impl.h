@@ -86,22 +86,6 @@ __device__ __forceinline__ void qmat(float* M, Q4 q) {
   M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
   M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
 }
-// entry t (row-major) of qmat(M, q), same arithmetic
-__device__ __forceinline__ float qmat_elem(Q4 q, int t) {
-  q = qnorm(q);
-  const float w = q.w, x = q.x, y = q.y, z = q.z;
-  switch (t) {
-    case 0: return 1 - 2 * (y * y + z * z);
-    case 1: return 2 * (x * y - w * z);
-    case 2: return 2 * (x * z + w * y);
-    case 3: return 2 * (x * y + w * z);
-    case 4: return 1 - 2 * (x * x + z * z);
-    case 5: return 2 * (y * z - w * x);
-    case 6: return 2 * (x * z - w * y);
-    case 7: return 2 * (y * z + w * x);
-    default: return 1 - 2 * (x * x + y * y);
-  }
-}
 // q v q* for a unit quaternion (18 FMAs, no normalisation)
 __device__ __forceinline__ V3 qrot(Q4 q, V3 v) {
   const V3 u = {q.x, q.y, q.z};
@@ -688,13 +672,6 @@ __device__ __forceinline__ CFrame cframe(V3 n) {
   f.b = cross(n, f.t);
   return f;
 }
-// entry t (row-major: n, t, b) of the contact frame rebuilt from the unit normal n
-__device__ __forceinline__ float cframe_elem(V3 n, int t) {
-  const CFrame F = cframe(n);
-  const V3 r = t < 3 ? F.n : t < 6 ? F.t : F.b;
-  const int k = t - 3 * (t / 3);
-  return k == 0 ? r.x : k == 1 ? r.y : r.z;
-}
 // F^T v for the contact frame F rebuilt from the unit normal at np (the C pack carries the
 // normals only)
 __device__ __forceinline__ V3 frame_tv(const float* np, V3 v) {
@@ -735,6 +712,41 @@ __device__ __forceinline__ int sphere_sphere(const ConOut& co, int key, int g1, 
   return 1;
 }
 __device__ __forceinline__ float clamp01(float t) { return t < 0 ? 0 : (t > 1 ? 1 : t); }
+__device__ __forceinline__ float clamp11(float t) { return t < -1 ? -1 : (t > 1 ? 1 : t); }
+// Capsule-capsule as MuJoCo's mjc_CapsuleCapsule (engine_collision_primitive.c; restated
+// from its published algorithm, mujoco_warp is absent here): segment parameters x1, x2 in
+// [-1, 1] along the half-length-scaled axes A1, A2; the stationary point of the squared
+// distance is clipped x1 first, then x2 (x1 re-solved and clipped), and the spheres at the
+// two points collide.  Parallel axes give up to two contacts: each end of capsule 1 against
+// its closest point on capsule 2, then, while fewer than two touch, each end of capsule 2.
+// Parallel is MuJoCo's |det| < mjMINVAL, with det = ma mc - mb^2 evaluated as |A1 x A2|^2
+// (Lagrange's identity): the difference form loses every digit to cancellation in fp32
+// (rounding noise ~1e-7 ma mc, far above mjMINVAL), the cross-product form keeps
+// exactly parallel axes below it in fp32 as in fp64.
+__device__ __forceinline__ int capsule_capsule(const ConOut& co, int key, int g1, int g2, V3 p1,
+                                               V3 A1, float r1, V3 p2, V3 A2, float r2,
+                                               float margin) {
+  const V3 dif = p1 - p2;
+  const float ma = dot(A1, A1), mb = -dot(A1, A2), mc = dot(A2, A2);
+  const float u = -dot(A1, dif), v = dot(A2, dif);
+  const V3 cx = cross(A1, A2);
+  const float det = dot(cx, cx);
+  if (det >= MINVAL) {
+    float x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+    if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+    else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+    if (x2 > 1) { x2 = 1; x1 = clamp11((u - mb) / ma); }
+    else if (x2 < -1) { x2 = -1; x1 = clamp11((u + mb) / ma); }
+    return sphere_sphere(co, key, g1, g2, p1 + A1 * x1, r1, p2 + A2 * x2, r2, margin);
+  }
+  int n = sphere_sphere(co, key, g1, g2, p1 + A1, r1, p2 + A2 * clamp11((v - mb) / mc), r2, margin);
+  n += sphere_sphere(co, key + n, g1, g2, p1 - A1, r1, p2 + A2 * clamp11((v + mb) / mc), r2, margin);
+  if (n >= 2) return n;
+  n += sphere_sphere(co, key + n, g1, g2, p1 + A1 * clamp11((u - mb) / ma), r1, p2 + A2, r2, margin);
+  if (n >= 2) return n;
+  n += sphere_sphere(co, key + n, g1, g2, p1 + A1 * clamp11((u + mb) / ma), r1, p2 - A2, r2, margin);
+  return n;
+}
 __device__ __forceinline__ void seg_seg(V3 a0, V3 a1, V3 b0, V3 b1, V3* pa, V3* pb) {
   V3 u = a1 - a0, v = b1 - b0, wv = a0 - b0;
   float a = dot(u, u), b = dot(u, v), c = dot(v, v), dd = dot(u, wv), e = dot(v, wv);
@@ -1478,8 +1490,14 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
     //     chain reaches an absolute frame -- ceil(log2(depth)) rounds of one LDS round trip
     //     instead of one per tree level;
     // (3) after the body frames: anchors / axes to the world by the parent frame.
+    // A free body's tree is built about the free body's own position (root-relative frame)
+    // and moved to the world only after cinert / cdof: their offsets (xipos - subtree_com,
+    // subtree_com - anchor) are then differences of O(1 m) numbers, not of world
+    // coordinates up to ~100 m from the origin (fp32 ulp(80) = 7.6e-6 m, which a light
+    // wrist's mass-matrix entry, a difference of O(m d^2) terms, amplifies to 1e-3 relative).
     int* par = Si + L.efc_cid;  // scratch ancestor pointers (the row block is dead until rows)
     bool absb = false;
+    V3 proot = {0.f, 0.f, 0.f};  // free body: its world position (added back below)
     V3 kpos = {0.f, 0.f, 0.f};
     Q4 kq = {1.f, 0.f, 0.f, 0.f};
     if (bl) {
@@ -1501,7 +1519,8 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
         const int a = J.qa;
         float R[9];
         if (J.jt == JNT_FREE) {  // MuJoCo: the only joint of a top-level body
-          kpos = v3(S + L.qpos + a);
+          proot = v3(S + L.qpos + a);
+          kpos = {0.f, 0.f, 0.f};
           kq = qnorm(q4(S + L.qpos + a + 3));
           st3(S + L.xanchor + 3 * k, kpos);
           qmat(R, kq);
@@ -1562,16 +1581,6 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       for (int k = B.j0; k < B.j0 + B.jn; k++) {
         st3(S + L.xanchor + 3 * k, pp + qrot(qp, v3(S + L.xanchor + 3 * k)));
         st3(S + L.xaxis + 3 * k, qrot(qp, v3(S + L.xaxis + 3 * k)));
-      }
-    }
-    {
-      const float* spos = MF(site_pos);
-      const float* squat = MF(site_quat);
-      for (int s = lane; s < d.nsite; s += kWave) {
-        int b = m.site_bodyid[s];
-        const Q4 qb = q4(S + L.xquat + 4 * b);
-        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + qrot(qb, v3(spos + 3 * s)));
-        qmat(S + L.sxmat + 9 * s, qmul(qb, q4(squat + 4 * s)));
       }
     }
     STAMP(0);
@@ -1663,6 +1672,32 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       }
     }
     sync();
+    {  // root-relative frames to the world (anchors are not used past cdof)
+      const V3 P = {__shfl(proot.x, B.root), __shfl(proot.y, B.root), __shfl(proot.z, B.root)};
+      V3 mxi = {0.f, 0.f, 0.f};
+      if (bl && B.b > 0) {
+        const V3 xi = v3(S + L.xipos + 3 * B.b) + P;
+        mxi = xi * B.mass;
+        st3(S + L.xpos + 3 * B.b, v3(S + L.xpos + 3 * B.b) + P);
+        st3(S + L.xipos + 3 * B.b, xi);
+        st3(S + L.subtree_com + 3 * B.b, v3(S + L.subtree_com + 3 * B.b) + P);
+      }
+      // the world's subtree spans every tree, each summed in its own frame above: its com
+      // again from the world-frame body coms (lane 0 holds the total mass in stm)
+      const V3 ms = {wave_sum(mxi.x), wave_sum(mxi.y), wave_sum(mxi.z)};
+      if (lane == 0 && stm > MINVAL) st3(S + L.subtree_com, ms * (1.0f / stm));
+    }
+    sync();
+    {
+      const float* spos = MF(site_pos);
+      const float* squat = MF(site_quat);
+      for (int s = lane; s < d.nsite; s += kWave) {
+        int b = m.site_bodyid[s];
+        const Q4 qb = q4(S + L.xquat + 4 * b);
+        st3(S + L.sxpos + 3 * s, v3(S + L.xpos + 3 * b) + qrot(qb, v3(spos + 3 * s)));
+        qmat(S + L.sxmat + 9 * s, qmul(qb, q4(squat + 4 * s)));
+      }
+    }
     STAMP(1);
     // =========================================================== CRB + mass matrix
     {
@@ -2008,10 +2043,8 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
         } else if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
           const float* R1 = S + L.gxmat + 9 * l1;
           const float* R2 = S + L.gxmat + 9 * l2;
-          V3 a1 = {R1[2], R1[5], R1[8]}, a2 = {R2[2], R2[5], R2[8]};
-          V3 pa, pb;
-          seg_seg(p1 + a1 * s1[1], p1 - a1 * s1[1], p2 + a2 * s2[1], p2 - a2 * s2[1], &pa, &pb);
-          sphere_sphere(co, key, g1, g2, pa, s1[0], pb, s2[0], margin);
+          const V3 a1 = {R1[2], R1[5], R1[8]}, a2 = {R2[2], R2[5], R2[8]};
+          capsule_capsule(co, key, g1, g2, p1, a1 * s1[1], s1[0], p2, a2 * s2[1], s2[0], margin);
         } else if (t1 == GEOM_BOX && t2 == GEOM_BOX) {
           HFrame F1, F2;
           F1.p = p1; F2.p = p2;
@@ -2506,30 +2539,30 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
         D.subtree_com[wb * 3 + i] = S[L.subtree_com + i];
       }
       for (int i = lane; i < 4 * nb; i += kWave) D.xquat[wb * 4 + i] = S[L.xquat + i];
-      // element-parallel (lane per output float): consecutive lanes store consecutive words,
-      // where a lane per body / geom / contact storing its 9 (or 3) floats at a 36-byte lane
-      // stride touches ~9x the cache lines per store instruction
-      for (int i = lane; i < 9 * nb; i += kWave) {  // xmat / ximat from the quaternions
-        const int b = i / 9, t = i - 9 * b;
-        const Q4 q = q4(S + L.xquat + 4 * b);
-        D.xmat[wb * 9 + i] = qmat_elem(q, t);
-        D.ximat[wb * 9 + i] = qmat_elem(qmul(q, q4(body_iquat + 4 * b)), t);
+      if (bl) {  // lane per body: xmat and ximat from the quaternions
+        float R[9], Ri[9];
+        qmat(R, xq);
+        qmat(Ri, qmul(xq, B.iquat));
+        float* om = D.xmat + (wb + B.b) * 9;
+        float* oi = D.ximat + (wb + B.b) * 9;
+#pragma unroll
+        for (int t = 0; t < 9; t++) { om[t] = R[t]; oi[t] = Ri[t]; }
       }
       for (int i = lane; i < 6 * nb; i += kWave) D.cvel[wb * 6 + i] = S[L.cvel + i];
-      // heightfield / terrain-box frames are static (set at sim creation)
+      // lane per geom: one model-index load per lane up front, not one per element (a
+      // dependent global load in every iteration of an element loop serialises on latency);
+      // heightfield frames are static (set at sim creation)
       size_t wg = (size_t)w * d.ngeom;
-      if (d.ngeom_lds == d.ngeom) {  // every geom keeps a frame in LDS, in model order
-        for (int i = lane; i < 3 * d.ngeom; i += kWave) D.geom_xpos[wg * 3 + i] = S[L.gxpos + i];
-        for (int i = lane; i < 9 * d.ngeom; i += kWave) D.geom_xmat[wg * 9 + i] = S[L.gxmat + i];
-      } else {
-        for (int i = lane; i < 3 * d.ngeom_lds; i += kWave) {
-          const int k = i / 3;
-          D.geom_xpos[(wg + m.lds_geom[k]) * 3 + i - 3 * k] = S[L.gxpos + i];
-        }
-        for (int i = lane; i < 9 * d.ngeom_lds; i += kWave) {
-          const int k = i / 9;
-          D.geom_xmat[(wg + m.lds_geom[k]) * 9 + i - 9 * k] = S[L.gxmat + i];
-        }
+      for (int i = lane; i < d.ngeom_lds; i += kWave) {
+        const size_t g = wg + m.lds_geom[i];
+        const float* xp = S + L.gxpos + 3 * i;
+        const float* xm = S + L.gxmat + 9 * i;
+        float* op = D.geom_xpos + g * 3;
+        float* om = D.geom_xmat + g * 9;
+#pragma unroll
+        for (int t = 0; t < 3; t++) op[t] = xp[t];
+#pragma unroll
+        for (int t = 0; t < 9; t++) om[t] = xm[t];
       }
       size_t ws = (size_t)w * d.nsite;
       for (int i = lane; i < 3 * d.nsite; i += kWave) D.site_xpos[ws * 3 + i] = S[L.sxpos + i];
@@ -2544,17 +2577,15 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       }
       for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
       size_t wc = (size_t)w * d.nconmax;
-      const int C = d.nconmax;
-      for (int c = lane; c < C; c += kWave) D.contact_dist[wc + c] = c < ncon ? S[L.con_dist + c] : 0.f;
-      for (int i = lane; i < 2 * C; i += kWave) {
-        const int c = i >> 1;
-        D.contact_geom[wc * 2 + i] = c < ncon ? Si[(i & 1) ? L.con_g2 + c : L.con_g1 + c] : -1;
-      }
-      for (int i = lane; i < 3 * C; i += kWave)
-        D.contact_pos[wc * 3 + i] = i < 3 * ncon ? S[L.con_pos + i] : 0.f;
-      for (int i = lane; i < 9 * C; i += kWave) {
-        const int c = i / 9;
-        D.contact_frame[wc * 9 + i] = c < ncon ? cframe_elem(v3(S + L.con_n + 3 * c), i - 9 * c) : 0.f;
+      for (int c = lane; c < d.nconmax; c += kWave) {
+        bool v = c < ncon;
+        D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
+        D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
+        D.contact_geom[(wc + c) * 2 + 1] = v ? Si[L.con_g2 + c] : -1;
+        for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = v ? S[L.con_pos + 3 * c + t] : 0.f;
+        const CFrame F = cframe(v ? v3(S + L.con_n + 3 * c) : V3{0.f, 0.f, 1.f});
+        const float fr[9] = {F.n.x, F.n.y, F.n.z, F.t.x, F.t.y, F.t.z, F.b.x, F.b.y, F.b.z};
+        for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? fr[t] : 0.f;
       }
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
@@ -3014,22 +3045,20 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
       size_t wc = (size_t)w * d.nconmax;
-      // element-parallel (lane per output float, coalesced): contact force in its frame
-      for (int i = lane; i < 3 * d.nconmax; i += kWave) {
-        const int c = i / 3, t = i - 3 * c;
-        float f = 0.f;
+      for (int c = lane; c < d.nconmax; c += kWave) {
+        V3 f = {0, 0, 0};
         if (c < ncon && nefc > 0) {
-          const int r0 = Si[L.con_efc + c];
-          if (Si[L.con_dim + c] == 1) {
-            f = t == 0 ? S[L.efc_force + r0] : 0.f;
-          } else {
-            const float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
-            const float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
-            f = t == 0 ? e0 + e1 + e2 + e3 : t == 1 ? (e0 - e1) * S[L.con_mu + 2 * c]
-                                                    : (e2 - e3) * S[L.con_mu + 2 * c + 1];
+          int r0 = Si[L.con_efc + c];
+          if (Si[L.con_dim + c] == 1) f.x = S[L.efc_force + r0];
+          else {
+            float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+            float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+            f = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
           }
         }
-        D.contact_force[wc * 3 + i] = f;
+        D.contact_force[(wc + c) * 3] = f.x;
+        D.contact_force[(wc + c) * 3 + 1] = f.y;
+        D.contact_force[(wc + c) * 3 + 2] = f.z;
       }
     }
     // per-world counters, every substep (a fused multi-substep step must not lose the

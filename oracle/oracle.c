@@ -453,6 +453,54 @@ static void seg_seg(const double* a0, const double* a1, const double* b0, const 
   for (int i = 0; i < 3; i++) { pa[i] = a0[i] + s * u[i]; pb[i] = b0[i] + t * v[i]; }
 }
 
+static double clip11(double t) { return t < -1 ? -1 : (t > 1 ? 1 : t); }
+/* capsule-capsule: MuJoCo's mjc_CapsuleCapsule (engine_collision_primitive.c, restated from
+ * its published algorithm) -- segment parameters in [-1, 1] along the half-length-scaled
+ * axes, x1 clipped first, then x2; parallel axes (det < MINVAL) give up to two contacts
+ * from the segment ends.  det = ma mc - mb^2 is evaluated as |A1 x A2|^2, as the engine
+ * does (engine_impl.h capsule_capsule: the difference form cancels in fp32). */
+static int col_capsule_capsule(orcData* d, const mjxModelDesc* m, int g1, int g2,
+                               double margin) {
+  const double *p1 = d->geom_xpos + 3 * g1, *p2 = d->geom_xpos + 3 * g2;
+  const double *R1 = d->geom_xmat + 9 * g1, *R2 = d->geom_xmat + 9 * g2;
+  const double h1 = m->geom_size[3 * g1 + 1], h2 = m->geom_size[3 * g2 + 1];
+  const double r1 = m->geom_size[3 * g1], r2 = m->geom_size[3 * g2];
+  double A1[3], A2[3], dif[3];
+  for (int i = 0; i < 3; i++) {
+    A1[i] = R1[3 * i + 2] * h1;
+    A2[i] = R2[3 * i + 2] * h2;
+    dif[i] = p1[i] - p2[i];
+  }
+  const double ma = v3_dot(A1, A1), mb = -v3_dot(A1, A2), mc = v3_dot(A2, A2);
+  const double u = -v3_dot(A1, dif), v = v3_dot(A2, dif);
+  double cx[3];
+  v3_cross(cx, A1, A2);
+  const double det = v3_dot(cx, cx);
+  double x1[4], x2[4];
+  int np;
+  if (det >= MINVAL) {
+    double a = (mc * u - mb * v) / det, b = (ma * v - mb * u) / det;
+    if (a > 1) { a = 1; b = (v - mb) / mc; }
+    else if (a < -1) { a = -1; b = (v + mb) / mc; }
+    if (b > 1) { b = 1; a = clip11((u - mb) / ma); }
+    else if (b < -1) { b = -1; a = clip11((u + mb) / ma); }
+    x1[0] = a; x2[0] = b; np = 1;
+  } else {
+    x1[0] = 1;                      x2[0] = clip11((v - mb) / mc);
+    x1[1] = -1;                     x2[1] = clip11((v + mb) / mc);
+    x1[2] = clip11((u - mb) / ma);  x2[2] = 1;
+    x1[3] = clip11((u + mb) / ma);  x2[3] = -1;
+    np = 4;
+  }
+  int n = 0;
+  for (int k = 0; k < np && n < 2; k++) {
+    double pa[3], pb[3];
+    for (int i = 0; i < 3; i++) { pa[i] = p1[i] + x1[k] * A1[i]; pb[i] = p2[i] + x2[k] * A2[i]; }
+    n += col_sphere_sphere(d, g1, g2, pa, r1, pb, r2, margin);
+  }
+  return n;
+}
+
 static void capsule_ends(const orcData* d, const mjxModelDesc* m, int g, double* e0, double* e1) {
   const double* p = d->geom_xpos + 3 * g;
   const double* R = d->geom_xmat + 9 * g;
@@ -874,11 +922,7 @@ static void collision(const mjxModelDesc* m, orcData* d) {
       seg_seg(p1, p1, e0, e1, pa, pb);
       col_sphere_sphere(d, g1, g2, p1, s1[0], pb, s2[0], margin);
     } else if (t1 == MJX_GEOM_CAPSULE && t2 == MJX_GEOM_CAPSULE) {
-      double a0[3], a1[3], b0[3], b1[3], pa[3], pb[3];
-      capsule_ends(d, m, g1, a0, a1);
-      capsule_ends(d, m, g2, b0, b1);
-      seg_seg(a0, a1, b0, b1, pa, pb);
-      col_sphere_sphere(d, g1, g2, pa, s1[0], pb, s2[0], margin);
+      col_capsule_capsule(d, m, g1, g2, margin);
     } else {
       d->overflow |= 4;
     }

@@ -63,7 +63,7 @@ def _check_step(m, sim, q, qv, ctrl, min_contact_worlds=1):
     sc = max(1.0, np.abs(r["qacc"]).max())
     np.testing.assert_allclose(qacc[i], r["qacc"], atol=2e-3 * sc, err_msg=f"qacc world {i}")
     np.testing.assert_allclose(qvel[i], r["qvel"], atol=2e-3 * sc * m.timestep + 1e-5)
-    np.testing.assert_allclose(qpos[i], r["qpos"], atol=1e-5)
+    np.testing.assert_allclose(qpos[i], r["qpos"], atol=2e-3 * sc * m.timestep ** 2 + 1e-5)  # h x the qvel bound
     ssc = max(1.0, np.abs(r["sensordata"]).max())
     np.testing.assert_allclose(sens[i], r["sensordata"], atol=3e-3 * ssc, err_msg=f"sens {i}")
   assert hit >= min_contact_worlds
