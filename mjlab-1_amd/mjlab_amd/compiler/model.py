@@ -59,6 +59,51 @@ class PositionActuatorGroup:
 
 
 @dataclass
+class MotorActuatorGroup:
+  """`BuiltinMotorActuatorCfg` (`src/mjlab/actuator/builtin_actuator.py:80-97`): a <motor>
+  per joint, `create_motor_actuator` (`src/mjlab/utils/spec.py:91-119`): force = ctrl,
+  ctrl and force both limited to +-effort_limit."""
+  joint_names_expr: tuple[str, ...]
+  effort_limit: float
+  gear: float = 1.0
+  armature: float = 0.0
+  frictionloss: float = 0.0
+
+
+@dataclass
+class VelocityActuatorGroup:
+  """`BuiltinVelocityActuatorCfg` (`src/mjlab/actuator/builtin_actuator.py:130-147`): a
+  <velocity> per joint, `create_velocity_actuator` (`src/mjlab/utils/spec.py:168-202`):
+  force = damping * (ctrl - qvel), ctrl limited through `inheritrange` (the joint range about
+  its middle), force limited when effort_limit is given."""
+  joint_names_expr: tuple[str, ...]
+  damping: float
+  effort_limit: float | None = None
+  armature: float = 0.0
+  frictionloss: float = 0.0
+  inheritrange: float = 1.0
+
+
+@dataclass
+class ActuatorSpec:
+  """One joint-transmission actuator with fixed gain and affine bias (the MjsActuator subset
+  the engine runs, `mjlab_amd.spec.SpecActuator.to_actuator_spec`): force = gain * ctrl + b0 +
+  b1 * length + b2 * velocity, length = gear * qpos, velocity = gear * qvel; ctrl clamped to
+  ctrlrange when ctrllimited, force to forcerange when forcelimited; inheritrange > 0 sets
+  ctrlrange from the joint's range (MuJoCo compiler semantics).  `joint` is unprefixed."""
+  name: str
+  joint: str
+  gain: float = 1.0
+  bias: tuple = (0.0, 0.0, 0.0)
+  gear: float = 1.0
+  ctrllimited: bool = False
+  ctrlrange: tuple = (0.0, 0.0)
+  forcelimited: bool = False
+  forcerange: tuple = (0.0, 0.0)
+  inheritrange: float = 0.0
+
+
+@dataclass
 class CollisionEdit:
   """`CollisionCfg` (`src/mjlab/utils/spec_config.py:137-238`)."""
   geom_names_expr: tuple[str, ...]
@@ -174,6 +219,25 @@ def _resolve(value, names, default):
 def _filter_exp(exprs, names):
   """`filter_exp` (utils/string.py:24-30): prefix match (re.match)."""
   return [n for n in names if any(re.match(e, n) for e in exprs)]
+
+
+def _group_actuator(grp, name: str) -> dict:
+  """Builtin actuator group -> one actuator record per joint (`src/mjlab/utils/spec.py:
+  91-202`: motor, position, velocity)."""
+  rec = dict(name=name, joint=name, gear=1.0, gain=0.0, bias=(0.0, 0.0, 0.0), ctrllim=False,
+             crange=(0.0, 0.0), forcelim=False, frange=(0.0, 0.0), inherit=0.0)
+  eff = grp.effort_limit
+  if isinstance(grp, PositionActuatorGroup):
+    rec.update(gain=grp.stiffness, bias=(0.0, -grp.stiffness, -grp.damping))
+  elif isinstance(grp, MotorActuatorGroup):
+    rec.update(gain=1.0, gear=grp.gear, ctrllim=True, crange=(-eff, eff))
+  elif isinstance(grp, VelocityActuatorGroup):
+    rec.update(gain=grp.damping, bias=(0.0, 0.0, -grp.damping), inherit=grp.inheritrange)
+  else:
+    raise TypeError(f"unsupported actuator group {type(grp).__name__}")
+  if eff is not None:
+    rec.update(forcelim=True, frange=(-eff, eff))
+  return rec
 
 
 def _find_names(exprs, names):
@@ -341,7 +405,7 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
 
   # ---------------------------------------------------------------- entities
   for ent in entities:
-    prefix = f"{ent.name}/"
+    prefix = f"{ent.name}/" if ent.name else ""
     xml = ent.xml
     # entity-level geom edits (CollisionCfg), applied on unprefixed names
     all_geom_names = []
@@ -413,6 +477,14 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
                           prefix + attrs.get("name", "")))
     # actuators (cfg order, joints in natural order)
     for grp in ent.actuators:
+      if isinstance(grp, ActuatorSpec):
+        if grp.joint not in joint_name_order:
+          raise ValueError(f"actuator '{grp.name}': no joint '{grp.joint}'")
+        actuators.append(dict(name=prefix + grp.name, joint=prefix + grp.joint, gear=grp.gear,
+                              gain=grp.gain, bias=tuple(grp.bias), ctrllim=bool(grp.ctrllimited),
+                              crange=tuple(grp.ctrlrange), forcelim=bool(grp.forcelimited),
+                              frange=tuple(grp.forcerange), inherit=grp.inheritrange))
+        continue
       names = _find_names(grp.joint_names_expr, joint_name_order)
       if not names:
         raise ValueError(f"no joints for actuator {grp.joint_names_expr}")
@@ -420,8 +492,7 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
         for j in joints:
           if j["name"] == prefix + n:
             j["attrs"] = dict(j["attrs"], armature=grp.armature, frictionloss=grp.frictionloss)
-        actuators.append(dict(name=prefix + n, joint=prefix + n, kp=grp.stiffness,
-                              kv=grp.damping, effort=grp.effort_limit))
+        actuators.append(_group_actuator(grp, prefix + n))
     keyframe_parts.append((ent, joint_name_order))
 
   # ---------------------------------------------------------------- flatten
@@ -517,6 +588,10 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
       dof_parentid[i] = body_dofadr[p] + body_dofnum[p] - 1 if p > 0 else -1
   A["dof_bodyid"], A["dof_jntid"], A["dof_parentid"] = dof_bodyid, dof_jntid, dof_parentid
   A["dof_armature"], A["dof_damping"], A["dof_frictionloss"] = dof_armature, dof_damping, dof_frictionloss
+  if (dof_frictionloss > 0).any():  # MuJoCo adds a friction-loss constraint row per such dof
+    raise NotImplementedError(
+      "dof frictionloss > 0: the engine has no friction-loss constraint rows "
+      f"(dofs {np.nonzero(dof_frictionloss > 0)[0].tolist()})")
 
   # root / weld ids, tree levels
   rootid = np.zeros(nbody, np.int32)
@@ -592,11 +667,23 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
   A["actuator_ctrllimited"] = np.zeros(m.nu, np.int32)
   A["actuator_ctrlrange"] = np.zeros((m.nu, 2))
   for i, a in enumerate(actuators):
-    A["actuator_gainprm"][i, 0] = a["kp"]
-    A["actuator_biasprm"][i] = (0.0, -a["kp"], -a["kv"])
-    if a["effort"] is not None:
+    A["actuator_gear"][i] = a["gear"]
+    A["actuator_gainprm"][i, 0] = a["gain"]
+    A["actuator_biasprm"][i] = a["bias"]
+    if a["forcelim"]:
       A["actuator_forcelimited"][i] = 1
-      A["actuator_forcerange"][i] = (-a["effort"], a["effort"])
+      A["actuator_forcerange"][i] = a["frange"]
+    if a["ctrllim"]:
+      A["actuator_ctrllimited"][i] = 1
+      A["actuator_ctrlrange"][i] = a["crange"]
+    if a["inherit"] > 0:  # MuJoCo: ctrlrange = range midpoint +- inheritrange * half range
+      k = int(A["actuator_trnid"][i])
+      lo, hi = (float(x) for x in A["jnt_range"][k])
+      if not A["jnt_limited"][k] or not lo < hi:
+        raise ValueError(f"actuator '{a['name']}': inheritrange needs a limited joint")
+      mid, half = 0.5 * (lo + hi), 0.5 * (hi - lo) * a["inherit"]
+      A["actuator_ctrllimited"][i] = 1
+      A["actuator_ctrlrange"][i] = (mid - half, mid + half)
 
   # collision candidate pairs (static broadphase filter, MuJoCo filterBodyPair rules),
   # vectorised over the geom pairs i < j (a generated terrain has thousands of geoms)
@@ -736,7 +823,7 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
   # keyframe "init_state" (src/mjlab/entity/entity.py:170-207)
   key = qpos0.copy()
   for ent, jorder in keyframe_parts:
-    prefix = f"{ent.name}/"
+    prefix = f"{ent.name}/" if ent.name else ""
     for k, j in enumerate(joints):
       if not j["name"].startswith(prefix):
         continue

@@ -71,3 +71,49 @@ def test_specialised_matches_generic(scene, gpu_device):
     b = getattr(s_gen.data, f).cpu().numpy()
     scale = max(1.0, float(np.abs(b).max()))
     assert np.abs(a - b).max() <= 1e-4 * scale, f"{scene} {f}: spec vs generic {np.abs(a - b).max()}"
+
+
+def test_spec_built_motor_velocity_position_actuators(gpu_device):
+  """A model built with the MjSpec-like surface (mjlab_amd/spec.py): motor, velocity and
+  position actuators (`utils/spec.py:91-202`) with their ctrl / force clamps, on the GPU
+  against the oracle (actuator_force, qacc_smooth, one step)."""
+  from mjlab_amd import spec as S
+  from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+  from parity_util import oracle_step
+  sp = S.Spec()
+  b = sp.worldbody.add_body(name="base", pos=(0, 0, 1.0))
+  for k, ax in enumerate(([0, 1, 0], [1, 0, 0], [0, 1, 0])):
+    b = b.add_body(name=f"l{k}", pos=(0, 0, -0.15) if k else (0, 0, 0))
+    b.add_joint(name=f"j{k}", axis=ax, range=[-1.5, 1.5], damping=0.05)
+    b.add_geom(name=f"g{k}", type=S.mjtGeom.mjGEOM_CAPSULE, size=[0.03, 0.06], pos=(0, 0, -0.07),
+               mass=0.4, contype=0, conaffinity=0)
+  S.create_motor_actuator(sp, "j0", effort_limit=2.0, gear=1.5, armature=0.01)
+  S.create_velocity_actuator(sp, "j1", damping=0.8, effort_limit=1.0, armature=0.01)
+  S.create_position_actuator(sp, "j2", stiffness=20.0, damping=1.0, effort_limit=3.0,
+                             armature=0.01)
+  m = sp.compile()
+  n = 32
+  rng = np.random.default_rng(2)
+  q = rng.uniform(-1.2, 1.2, (n, m.nq))
+  qv = rng.normal(0, 1.5, (n, m.nv))
+  ctrl = rng.uniform(-4, 4, (n, m.nu))
+  cfg = SimulationCfg(nconmax=8, njmax=16,
+                      mujoco=MujocoCfg(timestep=m.timestep, iterations=10, ls_iterations=20))
+  sim = Simulation(n, cfg, m, gpu_device)
+  d = sim.data
+  d.qpos[:] = torch.as_tensor(q, dtype=torch.float32)
+  d.qvel[:] = torch.as_tensor(qv, dtype=torch.float32)
+  d.ctrl[:] = torch.as_tensor(ctrl, dtype=torch.float32)
+  d.qacc_warmstart.zero_()
+  sim.step()
+  torch.cuda.synchronize()
+  ref = oracle_step(m, q, qv, np.zeros_like(qv), ctrl, step=True, nconmax=8, njmax=16)
+  af = d.actuator_force.cpu().numpy()
+  qa = d.qacc.cpu().numpy()
+  clipped = 0
+  for i, r in enumerate(ref):
+    np.testing.assert_allclose(af[i], r["actuator_force"], atol=1e-4, rtol=1e-5)
+    clipped += int(np.isclose(np.abs(r["actuator_force"]), [2.0, 1.0, 3.0]).any())
+    sc = max(1.0, np.abs(r["qacc"]).max())
+    np.testing.assert_allclose(qa[i], r["qacc"], atol=1e-3 * sc)
+  assert clipped >= n // 4  # the force clamps are exercised
