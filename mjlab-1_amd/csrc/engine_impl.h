@@ -409,6 +409,14 @@ __device__ __forceinline__ int build_active(int* act, const float* jar, int nefc
 __device__ __forceinline__ float rl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+// The lane index as a value the compiler cannot hoist: the per-column lane tests of the
+// register-row code (c < lane, c == lane) are then formed where they are used (one v_cmp
+// + v_cndmask each) instead of being hoisted out of the Newton loop as ~36 SGPR-pair masks
+// that spill into VGPR lanes and turn every select into an exec-mask branch.
+__device__ __forceinline__ int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
 template <int NR>
 __device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int nvp, int lane) {
   const int row = lane < nvp ? lane : 0;
@@ -418,9 +426,11 @@ __device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int n
     if (c < nvp) v = ld4(Mm + row * nvp + c);
     A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
   }
-  if (lane >= nvp) {
+  if (NR > nvp || kWave > NR) {  // identity rows past nvp (wave-uniform test)
+    const int ln = opaque_lane(lane);
+    const bool pad = ln >= nvp;
 #pragma unroll
-    for (int c = 0; c < NR; c++) A[c] = c == lane ? 1.f : 0.f;
+    for (int c = 0; c < NR; c++) A[c] = pad ? (c == ln ? 1.f : 0.f) : A[c];
   }
 }
 // In-place blocked right-looking Cholesky of the lower triangle: afterwards A[c] (c <= lane)
@@ -438,12 +448,13 @@ __device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, float* c
   // no per-step guards (guards get hoisted into spilled SGPR masks).
 #pragma unroll
   for (int j0 = 0; j0 < NR; j0 += 4) {
+    const int ln = opaque_lane(lane);
 #pragma unroll
     for (int t = 0; t < 4; t++) {
       const int j = j0 + t;
       const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
       A[j] *= r;
-      rdiag = lane == j ? r : rdiag;
+      rdiag = ln == j ? r : rdiag;
 #pragma unroll
       for (int u = t + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
     }
@@ -478,20 +489,25 @@ template <int NR>
 __device__ __forceinline__ void rows_store_strict(const float (&A)[NR], float rd, float* Lm, int nvp,
                                                   int lane) {
   if (lane >= nvp) return;
+  const int ln = opaque_lane(lane);
 #pragma unroll
   for (int c = 0; c < NR; c += 4)
     if (c < nvp)
       st4v(Lm + lane * nvp + c,
-           make_float4(c < lane ? A[c] * rd : c == lane ? rd : 0.f,
-                       c + 1 < lane ? A[c + 1] * rd : c + 1 == lane ? rd : 0.f,
-                       c + 2 < lane ? A[c + 2] * rd : c + 2 == lane ? rd : 0.f,
-                       c + 3 < lane ? A[c + 3] * rd : c + 3 == lane ? rd : 0.f));
+           make_float4(c < ln ? A[c] * rd : c == ln ? rd : 0.f,
+                       c + 1 < ln ? A[c + 1] * rd : c + 1 == ln ? rd : 0.f,
+                       c + 2 < ln ? A[c + 2] * rd : c + 2 == ln ? rd : 0.f,
+                       c + 3 < ln ? A[c + 3] * rd : c + 3 == ln ? rd : 0.f));
 }
 // Factor rows L (rows_chol) -> forward rows M (strictly lower, column-scaled).
 template <int NR>
 __device__ __forceinline__ void rows_fwd_rows(float (&A)[NR], float rd, int lane) {
+  const int ln = opaque_lane(lane);
 #pragma unroll
-  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * rl(rd, k) : 0.f;
+  for (int k = 0; k < NR; k++) {
+    const float s = rl(rd, k);  // outside the select: a readlane under a lane test is a branch
+    A[k] = k < ln ? A[k] * s : 0.f;
+  }
 }
 // Forward rows M of a factor published by rows_store_strict (M_jk = N_jk L_jj / L_kk), and
 // this lane's 1/L[i][i].
@@ -499,10 +515,16 @@ template <int NR>
 __device__ __forceinline__ void rows_load_factor(float (&A)[NR], float& rd, const float* Lm, int nvp,
                                                  int lane) {
   rows_load<NR>(A, Lm, nvp, lane);
-  rd = lane < nvp ? Lm[lane * nvp + lane] : 1.f;
+  const int ln = opaque_lane(lane);
+  const int dl = ln < nvp ? ln : 0;
+  const float dv = Lm[dl * nvp + dl];  // unconditional load, then select (no exec branch)
+  rd = ln < nvp ? dv : 1.f;
   const float ljj = __builtin_amdgcn_rcpf(rd);
 #pragma unroll
-  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * (rl(rd, k) * ljj) : 0.f;
+  for (int k = 0; k < NR; k++) {
+    const float s = rl(rd, k);
+    A[k] = k < ln ? A[k] * (s * ljj) : 0.f;
+  }
 }
 // x (lane i holds x[i]) <- (L L^T)^-1 x, from the forward rows M (registers) and the columns
 // of N in Lm (rows_store_strict, then synced).  Lanes >= nvp hold x = 0 and stay 0.
@@ -513,12 +535,112 @@ __device__ __forceinline__ float rows_solve(const float (&M)[NR], float rdiag, c
 #pragma unroll
   for (int j = 0; j < NR; j++) u = fmaf(-M[j], rl(u, j), u);  // M[j] = 0 on lanes <= j
   float Nc[NR];
-  const int col = lane < nvp ? lane : 0;
+  const int ln = opaque_lane(lane);
+  const int col = ln < nvp ? ln : 0;
 #pragma unroll
-  for (int j = 0; j < NR; j++) Nc[j] = (j < nvp && j > lane) ? Lm[j * nvp + col] : 0.f;
+  for (int j = 0; j < NR; j++) {
+    const float t = Lm[(j < nvp ? j : 0) * nvp + col];  // load, then select (no exec branch)
+    Nc[j] = (j < nvp && j > ln) ? t : 0.f;
+  }
   float v = u * rdiag;  // y = u / L_jj: the backward sweep starts at v = y
 #pragma unroll
   for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
+  return v * rdiag;
+}
+// Block-parallel variants.  On a dof order in which every 4-column block's pivots are
+// mutually uncoupled (a leaves-first order of the kinematic tree: legs / arms of one level
+// side by side), the diagonal 4 x 4 block is diagonal when the block
+// is reached, so its four pivots need no chain: four v_readlane + four rsq at once instead
+// of four dependent (readlane -> rsq -> scale -> readlane -> fma) steps.  Which blocks
+// qualify is decided at run time (one ballot per block: the block rows' strictly-lower
+// entries are exactly zero), so a contact that couples two branches only sends its blocks
+// down the chained path; the result is bit-identical to rows_chol on the same matrix (the
+// skipped updates are fma(-a, 0, x) = x).  Returns the mask of parallel blocks for the
+// solves.
+template <int NR>
+__device__ __forceinline__ unsigned rows_chol_blk(float (&A)[NR], float& rdiag, float* cb, int nvp, int lane) {
+  static_assert(NR % 4 == 0 && NR <= 128, "register rows come in column blocks of 4");
+  rdiag = 1.f;
+  unsigned fast = 0;
+#pragma unroll
+  for (int j0 = 0; j0 < NR; j0 += 4) {
+    const int t = opaque_lane(lane) - j0;
+    const bool nz = (t >= 1 && t < 4 && A[j0] != 0.f) || (t >= 2 && t < 4 && A[j0 + 1] != 0.f) ||
+                    (t == 3 && A[j0 + 2] != 0.f);
+    if (__ballot(nz) == 0ull) {
+      fast |= 1u << (j0 >> 2);
+      const float r0 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0], j0), MINVAL));
+      const float r1 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 1], j0 + 1), MINVAL));
+      const float r2 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 2], j0 + 2), MINVAL));
+      const float r3 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 3], j0 + 3), MINVAL));
+      A[j0] *= r0; A[j0 + 1] *= r1; A[j0 + 2] *= r2; A[j0 + 3] *= r3;
+      rdiag = t == 0 ? r0 : t == 1 ? r1 : t == 2 ? r2 : t == 3 ? r3 : rdiag;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; s++) {
+        const int j = j0 + s;
+        const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
+        A[j] *= r;
+        rdiag = t == s ? r : rdiag;
+#pragma unroll
+        for (int u = s + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
+      }
+    }
+    if (j0 + 4 < NR) {
+      st4v(cb + 4 * lane, make_float4(A[j0], A[j0 + 1], A[j0 + 2], A[j0 + 3]));
+      sync();
+#pragma unroll
+      for (int k0 = j0 + 4; k0 < NR; k0 += 4) {
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) c[u] = ld4(cb + 4 * (k0 + u));
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          A[k0 + u] = fmaf(-A[j0 + 3], c[u].w, fmaf(-A[j0 + 2], c[u].z,
+                      fmaf(-A[j0 + 1], c[u].y, fmaf(-A[j0], c[u].x, A[k0 + u]))));
+      }
+      sync();
+    }
+  }
+  (void)nvp;
+  return fast;
+}
+// rows_solve with the blocks of `fast` (rows_chol_blk) swept as one step each: their four
+// values are read before any of them is updated, which is exact because the block's own
+// forward (M) and backward (N) entries are zero.
+template <int NR>
+__device__ __forceinline__ float rows_solve_blk(const float (&M)[NR], float rdiag, const float* Lm,
+                                                float x, int nvp, int lane, unsigned fast) {
+  float u = x;
+#pragma unroll
+  for (int j0 = 0; j0 < NR; j0 += 4) {
+    if ((fast >> (j0 >> 2)) & 1u) {
+      const float u0 = rl(u, j0), u1 = rl(u, j0 + 1), u2 = rl(u, j0 + 2), u3 = rl(u, j0 + 3);
+      u = fmaf(-M[j0 + 3], u3, fmaf(-M[j0 + 2], u2, fmaf(-M[j0 + 1], u1, fmaf(-M[j0], u0, u))));
+    } else {
+#pragma unroll
+      for (int j = j0; j < j0 + 4; j++) u = fmaf(-M[j], rl(u, j), u);
+    }
+  }
+  float Nc[NR];
+  const int ln = opaque_lane(lane);
+  const int col = ln < nvp ? ln : 0;
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const float t = Lm[(j < nvp ? j : 0) * nvp + col];  // load, then select (no exec branch)
+    Nc[j] = (j < nvp && j > ln) ? t : 0.f;
+  }
+  float v = u * rdiag;
+#pragma unroll
+  for (int j0 = NR - 4; j0 >= 0; j0 -= 4) {
+    if ((fast >> (j0 >> 2)) & 1u) {
+      const float v0 = rl(v, j0), v1 = rl(v, j0 + 1), v2 = rl(v, j0 + 2), v3 = rl(v, j0 + 3);
+      v = fmaf(-Nc[j0], v0, fmaf(-Nc[j0 + 1], v1, fmaf(-Nc[j0 + 2], v2, fmaf(-Nc[j0 + 3], v3, v))));
+    } else {
+#pragma unroll
+      for (int j = j0 + 3; j >= j0; j--) v = fmaf(-Nc[j], rl(v, j), v);
+    }
+  }
   return v * rdiag;
 }
 // The same three steps on a factor kept in lower-tile-rows form (LTR, carve.h: row i holds
@@ -529,32 +651,40 @@ template <int NR>
 __device__ __forceinline__ void rows_store_strict_ltr(const float (&A)[NR], float rd, float* Lp, int nvp,
                                                       int lane) {
   if (lane >= nvp) return;
+  const int ln = opaque_lane(lane);
   float* row = Lp + ltr_off(lane);
   const int len = 4 * ((lane >> 2) + 1);
 #pragma unroll
   for (int c = 0; c < NR; c += 4)
     if (c < len)
-      st4v(row + c, make_float4(c < lane ? A[c] * rd : c == lane ? rd : 0.f,
-                                c + 1 < lane ? A[c + 1] * rd : c + 1 == lane ? rd : 0.f,
-                                c + 2 < lane ? A[c + 2] * rd : c + 2 == lane ? rd : 0.f,
-                                c + 3 < lane ? A[c + 3] * rd : c + 3 == lane ? rd : 0.f));
+      st4v(row + c, make_float4(c < ln ? A[c] * rd : c == ln ? rd : 0.f,
+                                c + 1 < ln ? A[c + 1] * rd : c + 1 == ln ? rd : 0.f,
+                                c + 2 < ln ? A[c + 2] * rd : c + 2 == ln ? rd : 0.f,
+                                c + 3 < ln ? A[c + 3] * rd : c + 3 == ln ? rd : 0.f));
 }
 template <int NR>
 __device__ __forceinline__ void rows_load_factor_ltr(float (&A)[NR], float& rd, const float* Lp,
                                                      int nvp, int lane) {
-  const int row = lane < nvp ? lane : 0;
+  const int ln = opaque_lane(lane);
+  const int row = ln < nvp ? ln : 0;
   const float* rp = Lp + ltr_off(row);
   const int len = 4 * ((row >> 2) + 1);
 #pragma unroll
   for (int c = 0; c < NR; c += 4) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < len) v = ld4(rp + c);
-    A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
+    // in-row address for every lane, then a select: a per-lane row length under an `if`
+    // is an exec-mask branch per column block
+    const float4 v = ld4(rp + (c < len ? c : 0));
+    const bool in = c < len;
+    A[c] = in ? v.x : 0.f; A[c + 1] = in ? v.y : 0.f; A[c + 2] = in ? v.z : 0.f; A[c + 3] = in ? v.w : 0.f;
   }
-  rd = lane < nvp ? rp[lane] : 1.f;
+  const float dv = rp[row];
+  rd = ln < nvp ? dv : 1.f;
   const float ljj = __builtin_amdgcn_rcpf(rd);
 #pragma unroll
-  for (int k = 0; k < NR; k++) A[k] = k < lane ? A[k] * (rl(rd, k) * ljj) : 0.f;
+  for (int k = 0; k < NR; k++) {
+    const float s = rl(rd, k);
+    A[k] = k < ln ? A[k] * (s * ljj) : 0.f;
+  }
 }
 template <int NR>
 __device__ __forceinline__ float rows_solve_ltr(const float (&M)[NR], float rdiag, const float* Lp,
@@ -563,9 +693,13 @@ __device__ __forceinline__ float rows_solve_ltr(const float (&M)[NR], float rdia
 #pragma unroll
   for (int j = 0; j < NR; j++) u = fmaf(-M[j], rl(u, j), u);
   float Nc[NR];
-  const int col = lane < nvp ? lane : 0;
+  const int ln = opaque_lane(lane);
+  const int col = ln < nvp ? ln : 0;
 #pragma unroll
-  for (int j = 0; j < NR; j++) Nc[j] = (j < nvp && j > lane) ? Lp[ltr_off(j) + col] : 0.f;
+  for (int j = 0; j < NR; j++) {
+    const float t = Lp[ltr_off(j < nvp ? j : 0) + col];  // inside the LTR block, then select
+    Nc[j] = (j < nvp && j > ln) ? t : 0.f;
+  }
   float v = u * rdiag;
 #pragma unroll
   for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
