@@ -109,7 +109,8 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
 template <int NR>
 static StepFn phase_fn_nr(int ph) {
-  return ph == 0 ? step_phase<NR, 0, 0> : ph == 1 ? step_phase<NR, 1, 0> : step_phase<NR, 2, 0>;
+  return ph == 0 ? step_phase<NR, 0, 0> : ph == 1 ? step_phase<NR, 1, 0>
+       : ph == 2 ? step_phase<NR, 2, 0> : step_newton_lat<NR, 0>;
 }
 static StepFn generic_fn(int nv, int ph) {
   // exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36), multiples of 8 otherwise
@@ -141,6 +142,15 @@ static StepFn spec_fn(int spec, int ph) {
 static StepFn step_fn(const Params& host, int ph) {
   StepFn f = host.spec > 0 ? spec_fn(host.spec, ph) : nullptr;
   return f ? f : generic_fn(host.d.nv, ph);
+}
+// The full-capacity Newton class and the masked forward run the latency kernel
+// (step_newton_lat); MJX355_NEWTON_LAT=0 keeps them on step_phase<NR, 1> (A/B diagnostic).
+static bool newton_lat() {
+  static const bool on = [] {
+    const char* e = getenv("MJX355_NEWTON_LAT");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
 }
 
 int find_spec(const Dims& d) {
@@ -179,10 +189,11 @@ static size_t lds_bytes(const Params& host, int ph) {
 hipError_t prepare_step(const Params& host) {
   size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
   for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
-  for (int ph = 0; ph < 3; ph++) {
-    if (shmem[ph] > 64 * 1024) {
+  for (int ph = 0; ph < 4; ph++) {
+    if (shmem[ph == 3 ? 1 : ph] > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)step_fn(host, ph),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem[ph]);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)shmem[ph == 3 ? 1 : ph]);
       if (e != hipSuccess) return e;
     }
   }
@@ -202,6 +213,7 @@ static hipError_t launch_split_classes(const Params& host, const Params* dev, in
                                        int nsubstep, int integrate, hipStream_t stream,
                                        const SideStream* side, int nsplit, bool piped) {
   const StepFn fA = step_fn(host, 0), fB = step_fn(host, 1), fC = step_fn(host, 2);
+  const StepFn fBL = newton_lat() ? step_fn(host, 3) : fB;
   const int nc = host.nrowclass;
   hipStream_t sst[kMaxSplit];
   int wb[kMaxSplit + 1];
@@ -246,7 +258,7 @@ static hipError_t launch_split_classes(const Params& host, const Params* dev, in
       const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
       if (n <= 0) continue;
       auto class_chain = [&](hipStream_t cs, int cls) {
-        hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1), cs, dev,
+        hipLaunchKernelGGL(cls ? fB : fBL, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1), cs, dev,
                            w0, w1, k, last, cls, nullptr);
         if (!piped) return;
         hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
@@ -277,6 +289,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                        const SideStream* side) {
   if (nworld <= 0) return hipSuccess;
   const StepFn fA = step_fn(host, 0), fB = step_fn(host, 1), fC = step_fn(host, 2);
+  const StepFn fBL = newton_lat() ? step_fn(host, 3) : fB;
   const int nc = host.nrowclass;
   if (nc > 0 && !side) return hipErrorInvalidValue;
   // Batch split: the worlds in nsplit contiguous ranges, each range's A -> B -> C chain on
@@ -323,7 +336,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       if (nc > 0 && mask) {
         // masked forward (a few reset worlds): one Newton launch at full capacity over the
         // masked worlds -- no classify launch, no fork/join latency on this short critical path
-        hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k,
+        hipLaunchKernelGGL(fBL, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k,
                            last, -1, mask);
       } else if (nc > 0) {
         hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, st, dev, w0, w1,
@@ -337,8 +350,8 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         if (e != hipSuccess) return e;
         // class c's stream: B, then (piped) C and the next substep's A of the same worlds
         auto class_chain = [&](hipStream_t cs, int cls) {
-          hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1), cs, dev,
-                             w0, w1, k, last, cls, mask);
+          hipLaunchKernelGGL(cls ? fB : fBL, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
+                             cs, dev, w0, w1, k, last, cls, mask);
           if (!piped) return;
           hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
                              k | (cls + 1) << 8, last, integrate, mask);

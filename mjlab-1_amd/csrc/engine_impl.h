@@ -440,7 +440,10 @@ __device__ __forceinline__ void rows_load(float (&A)[NR], const float* Mm, int n
 // `cb` (LDS, 4*64 floats: every lane writes, no branch) and every lane reads the block rows of the trailing columns back
 // as broadcast float4s -- one LDS round trip per 4 columns instead of one v_readlane per
 // trailing element (630 for NR 36).
-template <int NR>
+// PIPE (the latency kernel): each trailing group's four broadcast reads are issued before the
+// previous group's FMAs, so the LDS latency is paid once per block instead of once per group
+// (16 more VGPRs; -10 % factor latency on one wave, scripts/chol_bench.hip).
+template <int NR, bool PIPE = false>
 __device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, float* cb, int nvp, int lane) {
   static_assert(NR % 4 == 0, "register rows come in column blocks of 4");
   rdiag = 1.f;
@@ -461,6 +464,31 @@ __device__ __forceinline__ void rows_chol(float (&A)[NR], float& rdiag, float* c
     if (j0 + 4 < NR) {
       st4v(cb + 4 * lane, make_float4(A[j0], A[j0 + 1], A[j0 + 2], A[j0 + 3]));  // all 64 lanes (no branch)
       sync();
+      if constexpr (PIPE) {
+        float4 c[4], n[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) c[u] = ld4(cb + 4 * (j0 + 4 + u));
+#pragma unroll
+        for (int k0 = j0 + 4; k0 < NR; k0 += 4) {
+          if (k0 + 4 < NR) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) n[u] = ld4(cb + 4 * (k0 + 4 + u));
+          }
+          float q[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) q[u] = fmaf(-A[j0], c[u].x, A[k0 + u]);
+#pragma unroll
+          for (int u = 0; u < 4; u++) q[u] = fmaf(-A[j0 + 1], c[u].y, q[u]);
+#pragma unroll
+          for (int u = 0; u < 4; u++) q[u] = fmaf(-A[j0 + 2], c[u].z, q[u]);
+#pragma unroll
+          for (int u = 0; u < 4; u++) A[k0 + u] = fmaf(-A[j0 + 3], c[u].w, q[u]);
+#pragma unroll
+          for (int u = 0; u < 4; u++) c[u] = n[u];
+        }
+        sync();
+        continue;
+      }
       // trailing columns in groups of 4 (at most 16 broadcast VGPRs in flight: unbounded,
       // the scheduler hoists every read of the block and the kernel loses occupancy)
 #pragma unroll
@@ -1498,11 +1526,12 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 #else
 #define MJX_PHASE_ATTR
 #endif
-template <int NR, int PH, int SP>
-__global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params* __restrict__ P, int w0, int w1,
-                                                    int sel, int last, int integrate,
-                                                    const uint8_t* __restrict__ mask) {
-  extern __shared__ __attribute__((aligned(16))) float S[];
+// LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
+// more registers in flight, for the launch that holds the heavy worlds.
+template <int NR, int PH, int SP, bool LAT>
+__device__ __forceinline__ void step_body(float* __restrict__ S, const Params* __restrict__ P, int w0,
+                                          int w1, int sel, int last, int integrate,
+                                          const uint8_t* __restrict__ mask) {
   const auto& d = dims_of<SP>(P);
   const Opt& o = P->o;
   const DModel& m = P->m;
@@ -2903,7 +2932,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
           float rd;
           if (refactor) {
             rows_load<NR>(R, Lm, nvp, lane);
-            rows_chol<NR>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
+            rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
             rows_store_strict<NR>(R, rd, Lm, nvp, lane);
             rows_fwd_rows<NR>(R, rd, lane);
           } else {
@@ -3283,6 +3312,26 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
     D.wtrace[(size_t)w * 8 + 2 * PH + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+template <int NR, int PH, int SP>
+__global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params* __restrict__ P, int w0, int w1,
+                                                    int sel, int last, int integrate,
+                                                    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  step_body<NR, PH, SP, false>(S, P, w0, w1, sel, last, integrate, mask);
+}
+// Phase B for the full-capacity row class (the heavy worlds: more constraint rows than the
+// class capacity) and the masked forward.  That launch holds a few hundred worlds on 256 CUs,
+// one wave per SIMD at most, so its span is one world's latency, not throughput: the kernel
+// may take 256 VGPRs (2 waves / SIMD, still above its LDS-bound residency) and spends them
+// on loads issued ahead of their use (rows_chol<NR, true>).
+template <int NR, int SP>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_newton_lat(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask);
 }
 
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
