@@ -575,102 +575,6 @@ __device__ __forceinline__ float rows_solve(const float (&M)[NR], float rdiag, c
   for (int j = NR - 1; j >= 0; j--) v = fmaf(-Nc[j], rl(v, j), v);
   return v * rdiag;
 }
-// Block-parallel variants.  On a dof order in which every 4-column block's pivots are
-// mutually uncoupled (a leaves-first order of the kinematic tree: legs / arms of one level
-// side by side), the diagonal 4 x 4 block is diagonal when the block
-// is reached, so its four pivots need no chain: four v_readlane + four rsq at once instead
-// of four dependent (readlane -> rsq -> scale -> readlane -> fma) steps.  Which blocks
-// qualify is decided at run time (one ballot per block: the block rows' strictly-lower
-// entries are exactly zero), so a contact that couples two branches only sends its blocks
-// down the chained path; the result is bit-identical to rows_chol on the same matrix (the
-// skipped updates are fma(-a, 0, x) = x).  Returns the mask of parallel blocks for the
-// solves.
-template <int NR>
-__device__ __forceinline__ unsigned rows_chol_blk(float (&A)[NR], float& rdiag, float* cb, int nvp, int lane) {
-  static_assert(NR % 4 == 0 && NR <= 128, "register rows come in column blocks of 4");
-  rdiag = 1.f;
-  unsigned fast = 0;
-#pragma unroll
-  for (int j0 = 0; j0 < NR; j0 += 4) {
-    const int t = opaque_lane(lane) - j0;
-    const bool nz = (t >= 1 && t < 4 && A[j0] != 0.f) || (t >= 2 && t < 4 && A[j0 + 1] != 0.f) ||
-                    (t == 3 && A[j0 + 2] != 0.f);
-    if (__ballot(nz) == 0ull) {
-      fast |= 1u << (j0 >> 2);
-      const float r0 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0], j0), MINVAL));
-      const float r1 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 1], j0 + 1), MINVAL));
-      const float r2 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 2], j0 + 2), MINVAL));
-      const float r3 = __builtin_amdgcn_rsqf(fmaxf(rl(A[j0 + 3], j0 + 3), MINVAL));
-      A[j0] *= r0; A[j0 + 1] *= r1; A[j0 + 2] *= r2; A[j0 + 3] *= r3;
-      rdiag = t == 0 ? r0 : t == 1 ? r1 : t == 2 ? r2 : t == 3 ? r3 : rdiag;
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; s++) {
-        const int j = j0 + s;
-        const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
-        A[j] *= r;
-        rdiag = t == s ? r : rdiag;
-#pragma unroll
-        for (int u = s + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
-      }
-    }
-    if (j0 + 4 < NR) {
-      st4v(cb + 4 * lane, make_float4(A[j0], A[j0 + 1], A[j0 + 2], A[j0 + 3]));
-      sync();
-#pragma unroll
-      for (int k0 = j0 + 4; k0 < NR; k0 += 4) {
-        float4 c[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) c[u] = ld4(cb + 4 * (k0 + u));
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          A[k0 + u] = fmaf(-A[j0 + 3], c[u].w, fmaf(-A[j0 + 2], c[u].z,
-                      fmaf(-A[j0 + 1], c[u].y, fmaf(-A[j0], c[u].x, A[k0 + u]))));
-      }
-      sync();
-    }
-  }
-  (void)nvp;
-  return fast;
-}
-// rows_solve with the blocks of `fast` (rows_chol_blk) swept as one step each: their four
-// values are read before any of them is updated, which is exact because the block's own
-// forward (M) and backward (N) entries are zero.
-template <int NR>
-__device__ __forceinline__ float rows_solve_blk(const float (&M)[NR], float rdiag, const float* Lm,
-                                                float x, int nvp, int lane, unsigned fast) {
-  float u = x;
-#pragma unroll
-  for (int j0 = 0; j0 < NR; j0 += 4) {
-    if ((fast >> (j0 >> 2)) & 1u) {
-      const float u0 = rl(u, j0), u1 = rl(u, j0 + 1), u2 = rl(u, j0 + 2), u3 = rl(u, j0 + 3);
-      u = fmaf(-M[j0 + 3], u3, fmaf(-M[j0 + 2], u2, fmaf(-M[j0 + 1], u1, fmaf(-M[j0], u0, u))));
-    } else {
-#pragma unroll
-      for (int j = j0; j < j0 + 4; j++) u = fmaf(-M[j], rl(u, j), u);
-    }
-  }
-  float Nc[NR];
-  const int ln = opaque_lane(lane);
-  const int col = ln < nvp ? ln : 0;
-#pragma unroll
-  for (int j = 0; j < NR; j++) {
-    const float t = Lm[(j < nvp ? j : 0) * nvp + col];  // load, then select (no exec branch)
-    Nc[j] = (j < nvp && j > ln) ? t : 0.f;
-  }
-  float v = u * rdiag;
-#pragma unroll
-  for (int j0 = NR - 4; j0 >= 0; j0 -= 4) {
-    if ((fast >> (j0 >> 2)) & 1u) {
-      const float v0 = rl(v, j0), v1 = rl(v, j0 + 1), v2 = rl(v, j0 + 2), v3 = rl(v, j0 + 3);
-      v = fmaf(-Nc[j0], v0, fmaf(-Nc[j0 + 1], v1, fmaf(-Nc[j0 + 2], v2, fmaf(-Nc[j0 + 3], v3, v))));
-    } else {
-#pragma unroll
-      for (int j = j0 + 3; j >= j0; j--) v = fmaf(-Nc[j], rl(v, j), v);
-    }
-  }
-  return v * rdiag;
-}
 // The same three steps on a factor kept in lower-tile-rows form (LTR, carve.h: row i holds
 // columns [0, 4(i/4 + 1)) at ltr_off(i)): the phase A -> C hand-off of the implicit factor,
 // 720 instead of 1296 floats for nvp 36.  Columns past a row's tiles are zero in the full

@@ -1,10 +1,10 @@
 // Latency microbenchmark of the register-row SPD factor + solve on one wave (the Newton
-// Hessian of a heavy world): the engine's dense chain against the block-parallel variant
-// on a leaves-first dof order.  One workgroup per "world"; s_memtime per world.
+// Hessian of a heavy world).  One workgroup per "world"; s_memtime per world.  Measured
+// and dropped: a block-parallel factor on a leaves-first dof order
+// and a chunked-LTR factor (chunk registers, rank-4 updates).
 // build: hipcc -O3 --offload-arch=gfx950 -I mjlab-1_amd/csrc -I scripts -o scripts/chol_bench scripts/chol_bench.hip
-// modes: 0 engine (branch-free), 1 pre-round-3 forms, 2 block-parallel, 3 factor only,
-// 4 load_factor + solve only, 5/6 pipelined-LDS / readlane trailing updates (+ solve),
-// 7/8 the same factor only
+// modes: 0 engine (branch-free), 1 pre-round-3 forms, 3 factor only, 4 load_factor + solve
+// only, 5 factor only in the latency form (rows_chol<NR, true>)
 // usage: chol_bench <H file (NR*NR floats)> <rhs file (NR floats)> <mode> <nworld> <reps>
 #include <cstdio>
 #include <cstdlib>
@@ -14,75 +14,6 @@
 
 using namespace mjx;
 constexpr int NR = 36;
-
-// ---- latency variants of the trailing update (bench-local until measured)
-// (b) LDS-published block, next group's broadcast reads issued before this group's FMAs
-template <int NR>
-__device__ __forceinline__ void chol_pipe(float (&A)[NR], float& rdiag, float* cb, int lane) {
-  rdiag = 1.f;
-#pragma unroll
-  for (int j0 = 0; j0 < NR; j0 += 4) {
-    const int ln = opaque_lane(lane);
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int j = j0 + t;
-      const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
-      A[j] *= r;
-      rdiag = ln == j ? r : rdiag;
-#pragma unroll
-      for (int u = t + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
-    }
-    if (j0 + 4 < NR) {
-      st4v(cb + 4 * lane, make_float4(A[j0], A[j0 + 1], A[j0 + 2], A[j0 + 3]));
-      sync();
-      float4 c[4], n[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) c[u] = ld4(cb + 4 * (j0 + 4 + u));
-#pragma unroll
-      for (int k0 = j0 + 4; k0 < NR; k0 += 4) {
-        if (k0 + 4 < NR) {
-#pragma unroll
-          for (int u = 0; u < 4; u++) n[u] = ld4(cb + 4 * (k0 + 4 + u));
-        }
-        float s[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) s[u] = fmaf(-A[j0], c[u].x, A[k0 + u]);
-#pragma unroll
-        for (int u = 0; u < 4; u++) s[u] = fmaf(-A[j0 + 1], c[u].y, s[u]);
-#pragma unroll
-        for (int u = 0; u < 4; u++) s[u] = fmaf(-A[j0 + 2], c[u].z, s[u]);
-#pragma unroll
-        for (int u = 0; u < 4; u++) A[k0 + u] = fmaf(-A[j0 + 3], c[u].w, s[u]);
-#pragma unroll
-        for (int u = 0; u < 4; u++) c[u] = n[u];
-      }
-      sync();
-    }
-  }
-}
-// (c) trailing entries broadcast by v_readlane (no LDS)
-template <int NR>
-__device__ __forceinline__ void chol_rl(float (&A)[NR], float& rdiag, int lane) {
-  rdiag = 1.f;
-#pragma unroll
-  for (int j0 = 0; j0 < NR; j0 += 4) {
-    const int ln = opaque_lane(lane);
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int j = j0 + t;
-      const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
-      A[j] *= r;
-      rdiag = ln == j ? r : rdiag;
-#pragma unroll
-      for (int u = t + 1; u < 4; u++) A[j0 + u] = fmaf(-A[j], rl(A[j], j0 + u), A[j0 + u]);
-    }
-#pragma unroll
-    for (int k = j0 + 4; k < NR; k++) {
-      const float s0 = rl(A[j0], k), s1 = rl(A[j0 + 1], k), s2 = rl(A[j0 + 2], k), s3 = rl(A[j0 + 3], k);
-      A[k] = fmaf(-A[j0 + 3], s3, fmaf(-A[j0 + 2], s2, fmaf(-A[j0 + 1], s1, fmaf(-A[j0], s0, A[k]))));
-    }
-  }
-}
 
 __global__ __launch_bounds__(64) void kbench(const float* Hg, const float* bg, float* xout,
                                              unsigned long long* cyc, int reps, int mode) {
@@ -99,26 +30,14 @@ __global__ __launch_bounds__(64) void kbench(const float* Hg, const float* bg, f
     float A[NR];
     float rd;
     rows_load<NR>(A, Hm, NR, lane);
-    if (mode == 2) {
-      const unsigned fast = rows_chol_blk<NR>(A, rd, cb, NR, lane);
-      rows_store_strict<NR>(A, rd, Lm, NR, lane);
-      rows_fwd_rows<NR>(A, rd, lane);
-      sync();
-      x = rows_solve_blk<NR>(A, rd, Lm, b + x * 1e-30f, NR, lane, fast);
-    } else if (mode == 1) {
+    if (mode == 1) {
       old_rows_chol<NR>(A, rd, cb, NR, lane);
       old_rows_store_strict<NR>(A, rd, Lm, NR, lane);
       old_rows_fwd_rows<NR>(A, rd, lane);
       sync();
       x = old_rows_solve<NR>(A, rd, Lm, b + x * 1e-30f, NR, lane);
-    } else if (mode == 5 || mode == 6) {
-      if (mode == 5) chol_pipe<NR>(A, rd, cb, lane); else chol_rl<NR>(A, rd, lane);
-      rows_store_strict<NR>(A, rd, Lm, NR, lane);
-      rows_fwd_rows<NR>(A, rd, lane);
-      sync();
-      x = rows_solve<NR>(A, rd, Lm, b + x * 1e-30f, NR, lane);
-    } else if (mode == 7 || mode == 8) {  // factor only
-      if (mode == 7) chol_pipe<NR>(A, rd, cb, lane); else chol_rl<NR>(A, rd, lane);
+    } else if (mode == 5) {  // latency form: trailing reads a group ahead
+      rows_chol<NR, true>(A, rd, cb, NR, lane);
       rows_store_strict<NR>(A, rd, Lm, NR, lane);
       x += rd;
     } else if (mode == 3) {  // factor only

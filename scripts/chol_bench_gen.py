@@ -1,6 +1,7 @@
 """Inputs of scripts/chol_bench: a G1-shaped Newton Hessian H = M + J^T D J (tree-sparse M,
-foot contact rows on leg chains + root) in the natural dof order and in the leaves-first
-block order (mjlab_amd.sim.tree_order), padded to 36, plus a right-hand side."""
+foot contact rows on leg chains + root) in the natural dof order and in a leaves-first
+block order (the order the dropped block-parallel factor used), padded to 36, plus a
+right-hand side."""
 import os
 import sys
 
@@ -8,7 +9,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mjlab-1_amd"))
 from mjlab_amd.scenes import load_scene  # noqa: E402
-from mjlab_amd.sim.tree_order import block_order  # noqa: E402
+
 
 NR = 36
 m = load_scene("g1_velocity")
@@ -38,7 +39,9 @@ for foot in (11, 17, 27, 34):  # contact rows on the foot / hand chains
     u = np.zeros(nv)
     u[c] = rng.normal(size=len(c))
     H += 30.0 * np.outer(u, u)
-perm = block_order(par, NR)
+# leaves first: the four chain ends level by level, then waist and root (G1 dof tree)
+perm = [27, 34, 11, 17, 26, 33, 10, 16, 25, 32, 9, 15, 24, 31, 8, 14, 23, 30, 7, 13, 22, 29, 6, 12,
+        21, 28, -1, 20, 19, 18, 5, 4, 3, 2, 1, 0]
 Hn = np.eye(NR)
 Hn[:nv, :nv] = H
 Hp = np.eye(NR)
