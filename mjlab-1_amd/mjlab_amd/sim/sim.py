@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 from dataclasses import dataclass, field
 from typing import Literal
 
@@ -185,6 +186,9 @@ def _stream_handle(device: torch.device) -> int:
 
 def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   """Per-world contact/row capacities held in LDS."""
+  if os.environ.get("MJX355_WORLD_CAPACITY"):  # diagnostic: "ncon,rows"
+    c, r = (int(v) for v in os.environ["MJX355_WORLD_CAPACITY"].split(","))
+    return c, r
   ncon = cfg.nconmax if cfg.nconmax is not None else 48
   ncon = int(min(64, max(ncon, 48)))
   rows = cfg.njmax if cfg.njmax is not None else 160
