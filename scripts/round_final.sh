@@ -6,11 +6,11 @@
 set -e
 ROUND=${ROUND:-r02}
 mkdir -p gpurun_out/profiles_new
-bash scripts/bench_configs.sh > gpurun_out/final_bench.txt 2>&1
+[ -z "$NO_BENCH" ] && bash scripts/bench_configs.sh > gpurun_out/final_bench.txt 2>&1
 for spec in "g1 Mjlab-Velocity-Flat-Unitree-G1 4096 35" "go1 Mjlab-Velocity-Flat-Unitree-Go1 8192 18"; do
   set -- $spec
   TAG=$1 TASK=$2 NENV=$3 bash scripts/profile_round.sh > gpurun_out/final_prof_$1.txt 2>&1
-  python3 scripts/profile_summary.py gpurun_out/prof_$1 "$ROUND" "$2" "$3" "$4" >> gpurun_out/final_prof_$1.txt 2>&1
+  python3 scripts/profile_bench.py gpurun_out/prof_$1 "$ROUND" "$2" "$3" "$4" 20 >> gpurun_out/final_prof_$1.txt 2>&1
   cp profiles/${ROUND}_$1_* gpurun_out/profiles_new/
   rm -rf gpurun_out/prof_$1
 done
