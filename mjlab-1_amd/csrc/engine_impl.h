@@ -2905,6 +2905,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           bool done = false;
           for (int it = 0; it < o.ls_iterations; it++) {
             float der, der2, nz;
+#ifdef MJX_STAMPS
+            stamp_acc[45] += 1;
+#endif
             ls_eval(a, &der, &der2, &nz);
             if (fabsf(der) <= fmaxf(gtol, nz)) { alpha = a; done = true; break; }
             if (der < 0) { lo = a; best = a; } else { hi = a; }
@@ -2914,6 +2917,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
             a = next;
           }
           if (!done) alpha = best > 0 ? best : a;
+#ifdef MJX_STAMPS
+          stamp_acc[46] += 1;
+#endif
         }
         niter = iter + 1;
         SUBSTAMP(6);
