@@ -384,6 +384,28 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     m->dm.st_aabb = (const float*)p;
     if (upload(chunk.data(), sizeof(float) * chunk.size(), &p)) { delete m; return -1; }
     m->dm.st_chunk_aabb = (const float*)p;
+    // regular-pair records: the pair loop of phase A reads one coalesced 16-B record per
+    // lane instead of a chain of dependent per-geom loads (pair -> geom -> type / slot /
+    // margin / rbound); the cull radius is formed in fp32 exactly as the kernel forms it
+    bool packable = ng < 65536 && d.ngeom_lds < 4096;
+    for (int g = 0; g < ng && packable; g++) packable = desc->geom_type[g] >= 0 && desc->geom_type[g] < 16;
+    m->dm.pair_rec = nullptr;
+    if (packable && nreg > 0) {
+      std::vector<int32_t> rec((size_t)4 * nreg);
+      for (int q = 0; q < nreg; q++) {
+        const int g1 = desc->pair_geom1[q], g2 = desc->pair_geom2[q];
+        const int t1 = desc->geom_type[g1], t2 = desc->geom_type[g2];
+        const float r1 = (float)desc->geom_rbound[g1], r2 = (float)desc->geom_rbound[g2];
+        const float mg = std::fmax((float)desc->geom_margin[g1], (float)desc->geom_margin[g2]);
+        const float cull = (r1 > 0 && r2 > 0 && t1 != mjx::GEOM_HFIELD) ? r1 + r2 + mg : INFINITY;
+        rec[4 * q] = g1 | g2 << 16;
+        rec[4 * q + 1] = geom_lds[g1] | geom_lds[g2] << 12 | t1 << 24 | (int32_t)((uint32_t)t2 << 28);
+        std::memcpy(&rec[4 * q + 2], &mg, 4);
+        std::memcpy(&rec[4 * q + 3], &cull, 4);
+      }
+      if (upload(rec.data(), sizeof(int32_t) * rec.size(), &p)) { delete m; return -1; }
+      m->dm.pair_rec = (const int32_t*)p;
+    }
   }
   if (upload(desc->sensor_geommask1, sizeof(uint32_t) * (size_t)desc->nmaskword * d.nsensor, &p)) { delete m; return -1; }
   m->dm.sensor_geommask1 = (const uint32_t*)p;

@@ -73,6 +73,11 @@ struct DModel {
   const int32_t* st_partner;
   const float* st_aabb;
   const float* st_chunk_aabb;
+  // regular pairs as one 16-B record each (capi.cpp): {g1 | g2 << 16, l1 | l2 << 12 |
+  // t1 << 24 | t2 << 28 (LDS frame slots, geom types), margin, bounding-sphere cull radius
+  // r1 + r2 + margin (+inf: no cull)}; null when ids exceed the packing.  Valid while
+  // geom_rbound / geom_margin are not expanded per world.
+  const int32_t* pair_rec;
   int nmaskword;  // 32-bit words per contact-sensor geom mask
   const uint32_t* sensor_geommask1;
   const uint32_t* sensor_geommask2;

@@ -2060,16 +2060,29 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       const float* gsize = MF(geom_size);
       const float* grb = MF(geom_rbound);
       const float* gmargin = MF(geom_margin);
+      // one packed record per pair (capi.cpp pair_rec) while rbound / margin are shared by
+      // all worlds; the per-geom load chain otherwise (same values, same fp32 cull radius)
+      const bool rec = m.pair_rec != nullptr && m.geom_rbound_ws == 0 && m.geom_margin_ws == 0;
       for (int p = lane; p < d.npair; p += kWave) {
-        int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
-        int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-        const int l1 = m.geom_lds[g1], l2 = m.geom_lds[g2];  // LDS frame slots
-        float margin = fmaxf(gmargin[g1], gmargin[g2]);
-        V3 p1 = v3(S + L.gxpos + 3 * l1), p2 = v3(S + L.gxpos + 3 * l2);
-        float r1 = grb[g1], r2 = grb[g2];
-        if (r1 > 0 && r2 > 0 && t1 != GEOM_HFIELD) {
-          if (norm(p2 - p1) > r1 + r2 + margin) continue;
+        int g1, g2, t1, t2, l1, l2;  // geoms, types, LDS frame slots
+        float margin, cull;
+        if (rec) {
+          const int4 rc = reinterpret_cast<const int4*>(m.pair_rec)[p];
+          g1 = rc.x & 0xffff; g2 = (int)((unsigned)rc.x >> 16);
+          l1 = rc.y & 0xfff; l2 = (rc.y >> 12) & 0xfff;
+          t1 = (rc.y >> 24) & 15; t2 = (int)((unsigned)rc.y >> 28);
+          margin = __int_as_float(rc.z);
+          cull = __int_as_float(rc.w);
+        } else {
+          g1 = m.pair_geom1[p]; g2 = m.pair_geom2[p];
+          t1 = m.geom_type[g1]; t2 = m.geom_type[g2];
+          l1 = m.geom_lds[g1]; l2 = m.geom_lds[g2];
+          margin = fmaxf(gmargin[g1], gmargin[g2]);
+          const float r1 = grb[g1], r2 = grb[g2];
+          cull = (r1 > 0 && r2 > 0 && t1 != GEOM_HFIELD) ? r1 + r2 + margin : INFINITY;
         }
+        V3 p1 = v3(S + L.gxpos + 3 * l1), p2 = v3(S + L.gxpos + 3 * l2);
+        if (norm(p2 - p1) > cull) continue;
         const float* s1 = gsize + 3 * g1;
         const float* s2 = gsize + 3 * g2;
         int key = p * 8;
