@@ -67,6 +67,7 @@ struct mjxModel_ {
   std::vector<void*> allocs;
   // host fp32 copies of float fields (defaults for expansion)
   std::map<std::string, std::vector<float>> host_float;
+  std::vector<int> dof_parentid;  // host copy: find_spec checks a specialisation's dof tree
   std::map<std::string, std::pair<int64_t, int64_t>> float_dims;  // count, width
   std::map<std::string, std::pair<int64_t, int64_t>> int_dims;
   // static world frames of heightfield geoms (terrain bodies are welded to the world)
@@ -223,6 +224,7 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   if (upload(desc->dof_bodymask, sizeof(uint64_t) * d.nv, &p)) { delete m; return -1; }
   m->dm.dof_bodymask = (const uint64_t*)p;
   {
+    m->dof_parentid.assign(desc->dof_parentid, desc->dof_parentid + d.nv);
     // ancestor masks along dof_parentid (parents precede children in dof order)
     std::vector<uint64_t> anc(d.nv > 0 ? d.nv : 1, 0);
     for (int i = 0; i < d.nv; i++) {
@@ -472,7 +474,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
   }
-  s->spec = mjx::find_spec(s->d);
+  s->spec = mjx::find_spec(s->d, model->dof_parentid.data());
   s->nrowclass = mjx::choose_row_classes(s->d, s->spec, s->row_cap);
   for (int k = 0; k < mjx::kRowClasses; k++) {
     mjx::Dims ds = s->d;

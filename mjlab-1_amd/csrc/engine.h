@@ -131,9 +131,10 @@ namespace mjx {
 
 // Model specialisation: 0 = generic kernels (dims and carves read from Params at run
 // time), k > 0 = kernels compiled for the k-th entry of specs.inc (dims and carves are
-// compile-time constants).  find_spec returns the entry equal to d in every field, else 0.
+// compile-time constants).  find_spec returns the entry equal to d in every field and in
+// the dof tree (dof_parentid, for the tree-form SPD factors), else 0.
 constexpr int kMaxSpecs = 8;
-int find_spec(const Dims& d);
+int find_spec(const Dims& d, const int* dof_parentid);
 
 // Everything a launch needs, resident in device memory (read through the scalar cache
 // instead of occupying ~500 SGPRs of kernarg space).

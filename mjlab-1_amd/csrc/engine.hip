@@ -153,7 +153,7 @@ static bool newton_lat() {
   return on;
 }
 
-int find_spec(const Dims& d) {
+int find_spec(const Dims& d, const int* dof_parentid) {
   if (const char* e = getenv("MJX355_NO_SPEC"))  // diagnostic: force the generic kernels
     if (atoi(e) != 0) return 0;
   auto eq = [](const Dims& a, const Dims& b) {
@@ -165,7 +165,15 @@ int find_spec(const Dims& d) {
            a.npair_all == b.npair_all && a.nstatic == b.nstatic &&
            a.nstpartner == b.nstpartner && a.nboxbox == b.nboxbox && a.nconmax == b.nconmax && a.njmax == b.njmax;
   };
-#define MJX_SPEC(id, scene, ...) if (eq(d, ModelSpec<id>::dims())) return id;
+  // and the dof tree of the entry's tree-form SPD factors (rows_chol_tree)
+  auto same_tree = [&](const int* par, int n) {
+    if (n != d.nv) return false;
+    for (int i = 0; i < n; i++)
+      if (dof_parentid[i] != par[i]) return false;
+    return true;
+  };
+#define MJX_SPEC(id, scene, ...) \
+  if (eq(d, ModelSpec<id>::dims()) && same_tree(SpecTree<id>::par, SpecTree<id>::npar)) return id;
 #include "specs.inc"
 #undef MJX_SPEC
   return 0;

@@ -671,6 +671,20 @@ __device__ __forceinline__ void tiles_store(const float (&A)[2][16], const Tiles
            make_float4(A[s][4 * r], A[s][4 * r + 1], A[s][4 * r + 2], A[s][4 * r + 3]));
   }
 }
+// Tiles -> the full symmetric LDS matrix: the lower tiles and, off the diagonal, their
+// transposes (rows_load_rev reads the natural upper triangle).
+__device__ __forceinline__ void tiles_store_sym(const float (&A)[2][16], const Tiles& T, float* Mm,
+                                                int nvp) {
+  tiles_store(A, T, Mm, nvp);
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s] || T.bi[s] == T.bj[s]) continue;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      st4v(Mm + (4 * T.bj[s] + c) * nvp + 4 * T.bi[s],
+           make_float4(A[s][c], A[s][4 + c], A[s][8 + c], A[s][12 + c]));
+  }
+}
 // out = A v for the symmetric matrix held as lower 4x4 register tiles (diagonal blocks
 // full); each tile contributes its block and, off the diagonal, its transpose, through LDS
 // float atomics.  Ends synced.
@@ -1179,6 +1193,144 @@ template <int SP, int K>
 __device__ __forceinline__ decltype(auto) lds_of(const Params* P) {
   if constexpr (SP > 0) return SpecLds<SP, K>::get();
   else return static_cast<const Lds&>(P->LP[K]);
+}
+
+// --------------------------------------------------------------------------- tree-sparse SPD
+// A matrix whose pattern is the dof tree's (entry (i, j) != 0 only when one dof is an ancestor
+// of the other: M, the implicit-integration matrix, and the Newton Hessian while every
+// constraint row lies on one root-to-leaf chain) factors WITHOUT fill when children are
+// eliminated before their parents (MuJoCo's L^T D L order).  The tree form of the
+// register-row factor works in the reversed dof order (permuted index c = nvp-1-natural: pads
+// first, leaves before their ancestors), where L[k][j] != 0 (k > j) iff natural(k) is an
+// ancestor of natural(j).  For each 4-column block the trailing columns that block touches
+// are a compile-time bit mask (the union of the block columns' ancestors), so the trailing
+// update skips the structural zeros: 280 instead of 576 FMAs per lane for G1, 100 instead of
+// 160 for Go1.  Skipped terms are exact zeros in the dense sweep, so on the reversed matrix
+// the result equals the dense factor bit for bit.
+struct TreeChol {
+  bool on;
+  uint64_t trail[16];  // per block b: permuted columns k >= 4b+4 with L[k][4b..4b+3] != 0
+  uint32_t inblk[16];  // per block b: bit 4t+u set when L[4b+u][4b+t] != 0 (t < u)
+};
+constexpr TreeChol make_tree_chol(const int* par, int nv) {
+  TreeChol t{};
+  const int nvp = (nv + 3) & ~3;
+  if (nv < 1 || nvp > 64) return t;
+  for (int i = 0; i < nv; i++)
+    if (par[i] >= i || par[i] < -1) return t;  // parents precede children
+  t.on = true;
+  for (int c = 0; c < nvp; c++) {
+    const int n = nvp - 1 - c;
+    if (n >= nv) continue;  // padding dof: identity row and column
+    const int b = c >> 2;
+    for (int a = par[n]; a >= 0; a = par[a]) {
+      const int k = nvp - 1 - a;  // an ancestor's permuted index exceeds c
+      if (k >= 4 * b + 4) t.trail[b] |= 1ull << k;
+      else t.inblk[b] |= 1u << (4 * (c & 3) + (k & 3));
+    }
+  }
+  return t;
+}
+template <int SP> struct SpecTree {
+  static constexpr TreeChol get() { return TreeChol{}; }
+  static constexpr int npar = 0;
+  static constexpr int par[1] = {-1};
+};
+#define MJX_SPEC_TREE(id, ...)                                                \
+  template <> struct SpecTree<id> {                                           \
+    static constexpr int par[] = {__VA_ARGS__};                               \
+    static constexpr int npar = sizeof(par) / sizeof(int);                    \
+    static constexpr TreeChol get() { return make_tree_chol(par, npar); }     \
+  };
+#include "specs.inc"
+#undef MJX_SPEC_TREE
+// the tree form is compiled for a specialisation whose dof tree is known and matches its nv
+template <int SP> constexpr bool kTree =
+    SP > 0 && SpecTree<SP>::npar == ModelSpec<SP>::dims().nv && SpecTree<SP>::get().on;
+
+// Register rows of the reversed matrix: lane i holds row nvp-1-i of Mm (row stride nvp, the
+// natural order), columns reversed; lanes >= nvp identity.  The reversed lower triangle is
+// the natural UPPER one: Mm must hold the full symmetric matrix (tiles_store_sym).
+template <int NR>
+__device__ __forceinline__ void rows_load_rev(float (&A)[NR], const float* Mm, int nvp, int lane) {
+  const int row = lane < nvp ? nvp - 1 - lane : 0;
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < nvp) v = ld4(Mm + row * nvp + (nvp - 4 - c));
+    A[c] = v.w; A[c + 1] = v.z; A[c + 2] = v.y; A[c + 3] = v.x;
+  }
+  if (NR > nvp || kWave > NR) {
+    const int ln = opaque_lane(lane);
+    const bool pad = ln >= nvp;
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] = pad ? (c == ln ? 1.f : 0.f) : A[c];
+  }
+}
+// rows_chol on the reversed matrix of a tree-pattern SPD matrix: the same blocked sweep with
+// the structurally-zero in-block updates and trailing columns left out.  One instantiation
+// per column block, so each block's masks are compile-time immediates.
+template <int NR, int SP, int J0>
+__device__ __forceinline__ void rows_chol_tree_blk(float (&A)[NR], float& rdiag, float* cb, int lane) {
+  if constexpr (J0 < NR) {
+    constexpr uint32_t ib = J0 < 64 ? SpecTree<SP>::get().inblk[J0 >> 2] : 0u;
+    constexpr uint64_t tr = J0 < 64 ? SpecTree<SP>::get().trail[J0 >> 2] : 0ull;
+    const int ln = opaque_lane(lane);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = J0 + t;
+      const float r = __builtin_amdgcn_rsqf(fmaxf(rl(A[j], j), MINVAL));
+      A[j] *= r;
+      rdiag = ln == j ? r : rdiag;
+#pragma unroll
+      for (int u = t + 1; u < 4; u++)
+        if ((ib >> (4 * t + u)) & 1u) A[J0 + u] = fmaf(-A[j], rl(A[j], J0 + u), A[J0 + u]);
+    }
+    if constexpr (tr != 0ull) {
+      st4v(cb + 4 * lane, make_float4(A[J0], A[J0 + 1], A[J0 + 2], A[J0 + 3]));
+      sync();
+#pragma unroll
+      for (int k0 = J0 + 4; k0 < NR; k0 += 4) {
+        if (((tr >> k0) & 0xfull) == 0ull) continue;
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if ((tr >> (k0 + u)) & 1ull) c[u] = ld4(cb + 4 * (k0 + u));
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if ((tr >> (k0 + u)) & 1ull)
+            A[k0 + u] = fmaf(-A[J0 + 3], c[u].w, fmaf(-A[J0 + 2], c[u].z,
+                        fmaf(-A[J0 + 1], c[u].y, fmaf(-A[J0], c[u].x, A[k0 + u]))));
+      }
+      sync();
+    }
+    rows_chol_tree_blk<NR, SP, J0 + 4>(A, rdiag, cb, lane);
+  }
+}
+template <int NR, int SP>
+__device__ __forceinline__ void rows_chol_tree(float (&A)[NR], float& rdiag, float* cb, int lane) {
+  static_assert(NR % 4 == 0, "register rows come in column blocks of 4");
+  rdiag = 1.f;
+  rows_chol_tree_blk<NR, SP, 0>(A, rdiag, cb, lane);
+}
+// spd_factor_solve for a tree-pattern matrix: factor of the reversed matrix into Lm (reversed
+// order), v solved in place (natural order in LDS).
+template <int NR, int SP>
+__device__ __forceinline__ void spd_factor_solve_tree(const float* Mm, float* Lm, float* v, float* cb,
+                                                      int nvp, int lane) {
+  float A[NR];
+  rows_load_rev<NR>(A, Mm, nvp, lane);
+  float rd;
+  rows_chol_tree<NR, SP>(A, rd, cb, lane);
+  rows_store_strict<NR>(A, rd, Lm, nvp, lane);
+  rows_fwd_rows<NR>(A, rd, lane);
+  sync();
+  const int pl = nvp - 1 - lane;  // this lane's natural index (lanes < nvp)
+  float x = lane < nvp ? v[pl] : 0.f;
+  x = rows_solve<NR>(A, rd, Lm, x, nvp, lane);
+  sync();
+  if (lane < nvp) v[pl] = x;
+  sync();
 }
 
 // --------------------------------------------------------------------------- kernels
@@ -1983,15 +2135,26 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         if (lane == __builtin_amdgcn_readlane(Ar.dof, u)) da += cu;
       }
       float A[NR];
-      rows_load<NR>(A, S + L.M, nvp, lane);
-#pragma unroll
-      for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
       float rd;
-      rows_chol<NR>(A, rd, S + L.chol, nvp, lane);
+      if constexpr (kTree<SP>) {  // the factor of the reversed matrix (phase C solves in that order)
+        rows_load_rev<NR>(A, S + L.M, nvp, lane);
+        const float dp = __shfl(da, lane < nvp ? nvp - 1 - lane : lane);
+#pragma unroll
+        for (int c = 0; c < NR; c++) A[c] += c == lane ? dp : 0.f;
+        rows_chol_tree<NR, SP>(A, rd, S + L.chol, lane);
+      } else {
+        rows_load<NR>(A, S + L.M, nvp, lane);
+#pragma unroll
+        for (int c = 0; c < NR; c++) A[c] += c == lane ? da : 0.f;
+        rows_chol<NR>(A, rd, S + L.chol, nvp, lane);
+      }
       rows_store_strict_ltr<NR>(A, rd, gf, nvp, lane);
     }
     // H <- chol(M); qacc_smooth = M^-1 qfrc_smooth
-    spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
+    if constexpr (kTree<SP>)
+      spd_factor_solve_tree<NR, SP>(S + L.M, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
+    else
+      spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
     STAMP(7);
     // subtree com velocity and angular momentum about the subtree com, as sums over the
     // subtree (broadcast loop): V = sum m vc / M, L = sum h + sum m (x - X) x (vc - V) --
@@ -2391,6 +2554,18 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           r++;
         }
       }
+      // ints[6]: some contact couples two branches of the dof tree (neither body's dofs
+      // contain the other's), so its rows fill the Newton Hessian outside the tree pattern
+      // and phase B factors it densely; otherwise the tree form (rows_chol_tree)
+      bool xbranch = false;
+      if constexpr (kTree<SP>) {
+        if (lane < ncon) {
+          const int cbk = Si[L.con_key + lane];
+          const uint64_t m1 = m.body_dofmask[cb_b1(cbk)], m2 = m.body_dofmask[cb_b2(cbk)];
+          xbranch = (m1 & ~m2) != 0ull && (m2 & ~m1) != 0ull;
+        }
+      }
+      const int dense_h = __ballot(xbranch) != 0ull || !kTree<SP>;
       if (lane < ncon) {
         int r0 = lim_total + con_off;
         Si[L.con_efc + lane] = r0;
@@ -2492,7 +2667,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         S[L.efc_D + r] = 1.0f / Rr;
         S[L.efc_aref + r] = -B * vel - K * imp * (pos - margin);
       }
-      if (lane == 0) { ints[1] = nefc; ints[2] = lim_total; ints[4] = ncon; }
+      if (lane == 0) { ints[1] = nefc; ints[2] = lim_total; ints[4] = ncon; ints[6] = dense_h; }
       sync();
     }
     const int nefc = ints[1];
@@ -2728,6 +2903,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     const int nefc = ints[1];
     int ncon = ints[4];
     (void)ncon;
+    // tree-pattern Hessian (no contact across two branches of the dof tree, phase A's
+    // ints[6]): factored in the fill-free reversed order, rows_chol_tree
+    const bool tree_h = kTree<SP> && !MJX_JTDJ_MFMA && __builtin_amdgcn_readfirstlane(ints[6]) == 0;
     float Mt[2][16];  // M as register tiles; its LDS slot becomes H / jt_mul scratch
     tiles_load_ltr(Mt, T, S + L.M);
     sync();
@@ -2839,7 +3017,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
 #pragma unroll
             for (int e2 = 0; e2 < 16; e2++) A[s2][e2] = Mt[s2][e2];
           tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
-          tiles_store(A, T, Lm, nvp);
+          if (tree_h) tiles_store_sym(A, T, Lm, nvp);  // rows_load_rev reads the upper triangle
+          else tiles_store(A, T, Lm, nvp);
 #endif
         }
         sync();
@@ -2848,8 +3027,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           float R[NR];
           float rd;
           if (refactor) {
-            rows_load<NR>(R, Lm, nvp, lane);
-            rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
+            if (tree_h) {
+              rows_load_rev<NR>(R, Lm, nvp, lane);
+              if constexpr (kTree<SP>) rows_chol_tree<NR, SP>(R, rd, S + LB.chol, lane);
+            } else {
+              rows_load<NR>(R, Lm, nvp, lane);
+              rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
+            }
             rows_store_strict<NR>(R, rd, Lm, nvp, lane);
             rows_fwd_rows<NR>(R, rd, lane);
           } else {
@@ -2857,9 +3041,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           }
           sync();
           SUBSTAMP(3);
-          float xs = lane < nvp ? S[L.srch + lane] : 0.f;
+          // the tree-form factor is of the reversed matrix: lane i solves for dof nvp-1-i
+          const int pl = tree_h ? nvp - 1 - lane : lane;
+          float xs = lane < nvp ? S[L.srch + pl] : 0.f;
           xs = rows_solve<NR>(R, rd, Lm, xs, nvp, lane);
-          if (lane < nvp) S[L.srch + lane] = xs;
+          sync();
+          if (lane < nvp) S[L.srch + pl] = xs;
           sync();
         }
         SUBSTAMP(4);
@@ -3173,9 +3360,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       {
         float A[NR], rd;
         rows_load_factor_ltr<NR>(A, rd, gf, nvp, lane);
-        const float f = lane < nvp ? S[L.qfrc_smooth + lane] + S[L.qfrc_con + lane] : 0.f;
+        // a tree-form factor (phase A) is of the reversed matrix: lane i solves for dof nvp-1-i
+        const int pl = kTree<SP> ? nvp - 1 - lane : lane;
+        const float f = lane < nvp ? S[L.qfrc_smooth + pl] + S[L.qfrc_con + pl] : 0.f;
         const float acc = rows_solve_ltr<NR>(A, rd, gf, f, nvp, lane);
-        if (lane < nv) S[L.qvel + lane] += h * acc;
+        if (lane < nvp && pl < nv) S[L.qvel + pl] += h * acc;
       }
       sync();
       SUBSTAMP(11);

@@ -4,7 +4,8 @@
 // and a chunked-LTR factor (chunk registers, rank-4 updates).
 // build: hipcc -O3 --offload-arch=gfx950 -I mjlab-1_amd/csrc -I scripts -o scripts/chol_bench scripts/chol_bench.hip
 // modes: 0 engine (branch-free), 1 pre-round-3 forms, 3 factor only, 4 load_factor + solve
-// only, 5 factor only in the latency form (rows_chol<NR, true>)
+// only, 5 factor only in the latency form (rows_chol<NR, true>), 6 tree form (reversed dof
+// order, rows_chol_tree) factor + solve, 7 tree form factor only
 // usage: chol_bench <H file (NR*NR floats)> <rhs file (NR floats)> <mode> <nworld> <reps>
 #include <cstdio>
 #include <cstdlib>
@@ -36,6 +37,19 @@ __global__ __launch_bounds__(64) void kbench(const float* Hg, const float* bg, f
       old_rows_fwd_rows<NR>(A, rd, lane);
       sync();
       x = old_rows_solve<NR>(A, rd, Lm, b + x * 1e-30f, NR, lane);
+    } else if (mode == 6 || mode == 7) {  // tree form (reversed order), G1 dof tree (spec 1)
+      rows_load_rev<NR>(A, Hm, NR, lane);
+      rows_chol_tree<NR, 1>(A, rd, cb, lane);
+      rows_store_strict<NR>(A, rd, Lm, NR, lane);
+      if (mode == 7) {
+        x += rd;
+      } else {
+        rows_fwd_rows<NR>(A, rd, lane);
+        sync();
+        const float bp = lane < NR ? __shfl(b, NR - 1 - lane) : 0.f;
+        const float xp = rows_solve<NR>(A, rd, Lm, bp + x * 1e-30f, NR, lane);
+        x = __shfl(xp, lane < NR ? NR - 1 - lane : lane);
+      }
     } else if (mode == 5) {  // latency form: trailing reads a group ahead
       rows_chol<NR, true>(A, rd, cb, NR, lane);
       rows_store_strict<NR>(A, rd, Lm, NR, lane);

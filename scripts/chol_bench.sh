@@ -4,7 +4,7 @@ set -e
 mkdir -p gpurun_out/cb
 python scripts/chol_bench_gen.py gpurun_out/cb > gpurun_out/cb/gen.txt
 for nw in 1 256 2560; do
-  for mode in 1 0 3 5 4; do
-    timeout -k 5 30 ./scripts/chol_bench gpurun_out/cb/H_perm.bin gpurun_out/cb/b_perm.bin $mode $nw 200
+  for mode in 0 6 3 7 5 4; do
+    timeout -k 5 30 ./scripts/chol_bench gpurun_out/cb/H_nat.bin gpurun_out/cb/b_nat.bin $mode $nw 200
   done
 done
