@@ -2929,6 +2929,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
 #ifdef MJX_STAMPS
       sub_prev = __builtin_amdgcn_s_memtime();
+      stamp_acc[38] += 1;         // solves with rows
+      stamp_acc[39] += !tree_h;   // of them with the dense factor (a contact across branches)
 #endif
       // jar = J x - aref for every row (lane per row)
       auto set_jar = [&](const float* xv) {

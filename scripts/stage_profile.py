@@ -38,5 +38,6 @@ for task in sys.argv[1:] or ["Mjlab-Velocity-Flat-Unitree-G1"]:
   print(f"  newton: iterations {d[40] / nsub:.2f}/world-substep, refactors after the first {d[41] / nsub:.2f}, "
         f"changed rows per later iteration {d[42] / max(d[40] - nsub, 1):.2f}, refactors with <=4 changes {d[43] / nsub:.2f}, "
         f"active rows at iteration 0 {d[44] / nsub:.1f}")
+  print(f"  factor form: {d[39]} of {d[38]} Newton solves dense (a contact across two branches of the dof tree)")
   print(f"  line search: {d[45] / max(d[46], 1):.2f} evaluations per search, {d[46] / nsub:.2f} searches per world-substep")
   print("  stats", env.sim.stats(), "mean niter", float(env.sim.field("solver_niter").float().mean()))
