@@ -3067,6 +3067,17 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         g2 = wave_sum(g2);
         sn = sqrtf(wave_sum(sn));
         const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
+        // With at most one row per lane (every world of the bulk row class) the line search
+        // holds its rows' J s, J x - aref and D in registers: they are constant across its
+        // evaluations, which otherwise re-read them from LDS each time.  Lanes past nefc hold
+        // zeros (v = 0 is never active), so every sum is the loop form's, bit for bit.
+        const bool reg_rows = nefc <= kWave;
+        float rjs = 0.f, rja = 0.f, rD = 0.f;
+        if (reg_rows && lane < nefc) {
+          rjs = Js[lane];
+          rja = jar[lane];
+          rD = Dv[lane];
+        }
         SUBSTAMP(5);
         // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
         // The derivative is a sum of O(nefc) terms; once |der| is within its fp32
@@ -3074,15 +3085,25 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         // working precision (gtol itself, 1e-10 relative by default, is an fp64 target).
         auto ls_eval = [&](float alpha, float* der, float* der2, float* noise) {
           float f1 = 0.f, f2 = 0.f, fa = 0.f;
-          for (int r = lane; r < nefc; r += kWave) {
-            float js = Js[r];
-            float v = jar[r] + alpha * js;
+          if (reg_rows) {
+            const float v = rja + alpha * rjs;
             if (v < 0) {
-              float Dr = Dv[r];
-              float t = Dr * v * js;
+              const float t = rD * v * rjs;
               f1 += t;
               fa += fabsf(t);
-              f2 += Dr * js * js;
+              f2 += rD * rjs * rjs;
+            }
+          } else {
+            for (int r = lane; r < nefc; r += kWave) {
+              float js = Js[r];
+              float v = jar[r] + alpha * js;
+              if (v < 0) {
+                float Dr = Dv[r];
+                float t = Dr * v * js;
+                f1 += t;
+                fa += fabsf(t);
+                f2 += Dr * js * js;
+              }
             }
           }
           f1 = wave_sum(f1);
@@ -3097,9 +3118,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         float alpha = 0.f;
         if (d0 < 0) {
           float c0 = 0.f;
-          for (int r = lane; r < nefc; r += kWave) {
-            float ja = jar[r], js = Js[r];
-            if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
+          if (reg_rows) {
+            if (rja < 0 || (rja == 0 && rjs < 0)) c0 += rD * rjs * rjs;
+          } else {
+            for (int r = lane; r < nefc; r += kWave) {
+              float ja = jar[r], js = Js[r];
+              if (ja < 0 || (ja == 0 && js < 0)) c0 += Dv[r] * js * js;
+            }
           }
           c0 = g2 + wave_sum(c0);
           float lo = 0.f, hi = -1.f, best = 0.f;
@@ -3130,7 +3155,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           S[L.x + i] += alpha * S[L.srch + i];
           S[L.Mx + i] += alpha * S[L.Ms + i];
         }
-        for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
+        if (reg_rows) {
+          if (lane < nefc) jar[lane] = rja + alpha * rjs;
+        } else {
+          for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
+        }
         sync();
         float old = cost;
         cost = cost_of(S + L.x, S + L.Mx);

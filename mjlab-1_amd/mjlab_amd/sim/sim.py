@@ -176,6 +176,11 @@ class SimulationCfg:
   """Constraint rows per world held in LDS."""
   ls_parallel: bool = True  # accepted for API compatibility; the line search is exact
   contact_sensor_maxmatch: int = 64
+  engine_capacity: tuple[int, int] | None = None
+  """(contacts, rows) per world the engine holds in LDS (this build's knob, not the
+  reference's).  None: 48 contacts and at most 160 rows, the fast carve for tasks whose
+  worlds stay far below it.  A task whose worlds reach it (tracking: 186 rows and 49
+  contacts at 4,096 random-action worlds) sets the reference's `njmax` here instead."""
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -189,11 +194,16 @@ def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   if os.environ.get("MJX355_WORLD_CAPACITY"):  # diagnostic: "ncon,rows"
     c, r = (int(v) for v in os.environ["MJX355_WORLD_CAPACITY"].split(","))
     return c, r
-  ncon = cfg.nconmax if cfg.nconmax is not None else 48
-  ncon = int(min(64, max(ncon, 48)))
-  rows = cfg.njmax if cfg.njmax is not None else 160
   nlim = int(np.sum(model.jnt_limited)) if model.njnt else 0
-  rows = int(max(1, min(rows, 4 * ncon + 2 * nlim, 160)))
+  if cfg.engine_capacity is not None:
+    ncon, cap = (int(v) for v in cfg.engine_capacity)
+    if not (1 <= ncon <= 64 and 1 <= cap <= 256):
+      raise ValueError(f"engine_capacity {cfg.engine_capacity}: contacts 1..64, rows 1..256")
+  else:
+    ncon = cfg.nconmax if cfg.nconmax is not None else 48
+    ncon, cap = int(min(64, max(ncon, 48))), 160
+  rows = cfg.njmax if cfg.njmax is not None else cap
+  rows = int(max(1, min(rows, 4 * ncon + 2 * nlim, cap)))
   return ncon, rows
 
 

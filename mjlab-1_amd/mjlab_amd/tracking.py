@@ -696,8 +696,10 @@ def make_tracking_env_cfg():
     scene=SceneCfg(scene_name="g1_tracking", num_envs=1), observations=observations,
     actions=actions, commands=commands, events=events, rewards=rewards,
     terminations=terminations,
-    sim=SimulationCfg(nconmax=35, njmax=250, mujoco=MujocoCfg(timestep=0.005, iterations=10,
-                                                               ls_iterations=20)),
+    # the reference's njmax (250 rows per world) held in full: random-action tracking worlds
+    # reach 186 rows and 49 contacts, past the default 48 / 160 carve
+    sim=SimulationCfg(nconmax=35, njmax=250, engine_capacity=(64, 256),
+                      mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)),
     decimation=4, episode_length_s=10.0)
 
 
