@@ -402,6 +402,19 @@ __device__ __forceinline__ int build_active(int* act, const float* jar, int nefc
   return base;
 }
 
+// build_active for nefc <= 64 with row `lane`'s jar in a register (lanes past nefc: 0)
+__device__ __forceinline__ int build_active1(int* act, float rja, int nefc, int lane,
+                                             unsigned long long (&sig)[4], bool* same,
+                                             int* nchg = nullptr) {
+  const bool f = lane < nefc && rja < 0.f;
+  const unsigned long long bal = __ballot(f);
+  if (f) act[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
+  *same = nefc <= 0 || bal == sig[0];
+  if (nchg) *nchg = nefc > 0 ? __popcll(bal ^ sig[0]) : 0;
+  if (nefc > 0) sig[0] = bal;
+  return __popcll(bal);
+}
+
 // --------------------------------------------------------------------------- register-row SPD
 // Lane i holds row i of an nvp x nvp SPD matrix in NR registers (NR = compile-time row
 // length >= nvp; rows/cols >= nvp are identity).  Cholesky and both triangular solves run
@@ -2932,19 +2945,48 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       stamp_acc[38] += 1;         // solves with rows
       stamp_acc[39] += !tree_h;   // of them with the dense factor (a contact across branches)
 #endif
+      // With at most one row per lane (every world of the bulk row class) the solver keeps
+      // its row's D, J x - aref (rja) and, in the line search, J s (rjs) in registers: the
+      // per-row loops below then read no LDS.  Lanes past nefc hold zeros (v = 0 is never
+      // active), so every sum is the loop form's, bit for bit; jar stays mirrored in LDS.
+      const bool reg_rows = nefc <= kWave;
+      const float rD = reg_rows && lane < nefc ? Dv[lane] : 0.f;
+      float rja = 0.f;
       // jar = J x - aref for every row (lane per row)
       auto set_jar = [&](const float* xv) {
         matvec_rows(jar, J, xv, nefc, nvp, lane);
         for (int r = lane; r < nefc; r += kWave) jar[r] -= S[L.efc_aref + r];
+        if (reg_rows) rja = lane < nefc ? jar[lane] : 0.f;
       };
       // total cost at (x, Mx, jar): Gauss term + active half-quadratics (wave-uniform)
       auto cost_of = [&](const float* xv, const float* Mxv) -> float {
         float g = 0.f;
         for (int i = lane; i < nv; i += kWave)
           g += 0.5f * (xv[i] - S[L.qacc_smooth + i]) * (Mxv[i] - S[L.qfrc_smooth + i]);
-        for (int r = lane; r < nefc; r += kWave) {
-          float v = jar[r];
-          if (v < 0.f) g += 0.5f * Dv[r] * v * v;
+        if (reg_rows) {
+          if (rja < 0.f) g += 0.5f * rD * rja * rja;
+        } else {
+          for (int r = lane; r < nefc; r += kWave) {
+            float v = jar[r];
+            if (v < 0.f) g += 0.5f * Dv[r] * v * v;
+          }
+        }
+        return wave_sum(g);
+      };
+      // lane i's dof values in registers for the iterations (nvp <= 64): x, M x (mirrored
+      // in LDS, which the J x products and the output copies read) and the constant
+      // qacc_smooth / qfrc_smooth; same per-lane arithmetic as the LDS loops
+      float rx = 0.f, rMx = 0.f, rqs = 0.f, rfs = 0.f;
+      auto cost_now = [&]() -> float {
+        float g = 0.f;
+        if (lane < nv) g += 0.5f * (rx - rqs) * (rMx - rfs);
+        if (reg_rows) {
+          if (rja < 0.f) g += 0.5f * rD * rja * rja;
+        } else {
+          for (int r = lane; r < nefc; r += kWave) {
+            float v = jar[r];
+            if (v < 0.f) g += 0.5f * Dv[r] * v * v;
+          }
         }
         return wave_sum(g);
       };
@@ -2972,13 +3014,20 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         cost = cost_ws;
       }
       sync();
+      if (lane < nvp) {
+        rx = S[L.x + lane];
+        rMx = S[L.Mx + lane];
+        rqs = S[L.qacc_smooth + lane];
+        rfs = S[L.qfrc_smooth + lane];
+      }
       SUBSTAMP(0);
       unsigned long long act_sig[4] = {~0ull, ~0ull, ~0ull, ~0ull};
       for (int iter = 0; iter < o.iterations; iter++) {
         // gradient = M x - qfrc_smooth + J_act^T (D jar)
         bool same_set;
         int nchg = 0;
-        const int nact = build_active(act, jar, nefc, lane, act_sig, &same_set, &nchg);
+        const int nact = reg_rows ? build_active1(act, rja, nefc, lane, act_sig, &same_set, &nchg)
+                                  : build_active(act, jar, nefc, lane, act_sig, &same_set, &nchg);
         // H depends on the active set only: unchanged set -> reuse the stored factor (exact)
         const bool refactor = iter == 0 || !same_set;
 #ifdef MJX_STAMPS
@@ -2989,12 +3038,17 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         stamp_acc[44] += iter == 0 ? nact : 0;
 #endif
         (void)nchg;
-        for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
+        if (reg_rows) {
+          if (lane < nefc) wv[lane] = rD * rja;
+        } else {
+          for (int r = lane; r < nefc; r += kWave) wv[r] = Dv[r] * jar[r];
+        }
         sync();
         jt_mul(S + L.srch, J, wv, act, nact, nvp, lane);
         float gn = 0.f, gr = 0.f;
-        for (int i = lane; i < nvp; i += kWave) {
-          const float jf = S[L.srch + i], mx = S[L.Mx + i], fs = S[L.qfrc_smooth + i];
+        if (lane < nvp) {
+          const int i = lane;
+          const float jf = S[L.srch + i], mx = rMx, fs = rfs;
           const float g = jf + mx - fs;  // gradient
           S[L.srch + i] = -g;
           gn += g * g;
@@ -3054,30 +3108,21 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         SUBSTAMP(4);
         matvec_rows(Js, J, S + L.srch, nefc, nvp, lane);
         tiles_symv(Mt, T, S + L.srch, S + L.Ms, nvp, lane);
-        float g1 = 0.f, sn = 0.f;
-        for (int i = lane; i < nv; i += kWave) {
-          float sv = S[L.srch + i];
-          g1 += sv * (S[L.Mx + i] - S[L.qfrc_smooth + i]);
+        float g1 = 0.f, sn = 0.f, sv = 0.f;
+        if (lane < nv) {
+          sv = S[L.srch + lane];
+          g1 += sv * (rMx - rfs);
           sn += sv * sv;
         }
         sync();
         float g2 = 0.f;
-        for (int i = lane; i < nv; i += kWave) g2 += S[L.srch + i] * S[L.Ms + i];
+        if (lane < nv) g2 += sv * S[L.Ms + lane];
         g1 = wave_sum(g1);
         g2 = wave_sum(g2);
         sn = sqrtf(wave_sum(sn));
         const float gtol = o.tolerance * o.ls_tolerance * sn / scale;
-        // With at most one row per lane (every world of the bulk row class) the line search
-        // holds its rows' J s, J x - aref and D in registers: they are constant across its
-        // evaluations, which otherwise re-read them from LDS each time.  Lanes past nefc hold
-        // zeros (v = 0 is never active), so every sum is the loop form's, bit for bit.
-        const bool reg_rows = nefc <= kWave;
-        float rjs = 0.f, rja = 0.f, rD = 0.f;
-        if (reg_rows && lane < nefc) {
-          rjs = Js[lane];
-          rja = jar[lane];
-          rD = Dv[lane];
-        }
+        // the line search's J s (constant across its evaluations) in a register too
+        const float rjs = reg_rows && lane < nefc ? Js[lane] : 0.f;
         SUBSTAMP(5);
         // exact line search on the piecewise-quadratic cost (same algorithm as the oracle)
         // The derivative is a sum of O(nefc) terms; once |der| is within its fp32
@@ -3151,18 +3196,21 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         niter = iter + 1;
         SUBSTAMP(6);
         if (alpha == 0.f) break;
-        for (int i = lane; i < nvp; i += kWave) {
-          S[L.x + i] += alpha * S[L.srch + i];
-          S[L.Mx + i] += alpha * S[L.Ms + i];
+        if (lane < nvp) {
+          rx = rx + alpha * S[L.srch + lane];
+          rMx = rMx + alpha * S[L.Ms + lane];
+          S[L.x + lane] = rx;
+          S[L.Mx + lane] = rMx;
         }
         if (reg_rows) {
-          if (lane < nefc) jar[lane] = rja + alpha * rjs;
+          rja = rja + alpha * rjs;  // lanes past nefc: 0 + alpha * 0
+          if (lane < nefc) jar[lane] = rja;
         } else {
           for (int r = lane; r < nefc; r += kWave) jar[r] += alpha * Js[r];
         }
         sync();
         float old = cost;
-        cost = cost_of(S + L.x, S + L.Mx);
+        cost = cost_now();
         SUBSTAMP(7);
         // MuJoCo's improvement test, with the fp32 resolution of the cost (a sum of
         // non-negative terms, so its rounding error is ~eps*|cost|) as the floor: below
@@ -3171,13 +3219,18 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       }
       // constraint forces and qfrc_constraint = J^T f over the active rows
       sync();
-      for (int r = lane; r < nefc; r += kWave) {
-        float ja = jar[r];
-        wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
+      if (reg_rows) {
+        if (lane < nefc) wv[lane] = rja < 0 ? -rD * rja : 0.f;
+      } else {
+        for (int r = lane; r < nefc; r += kWave) {
+          float ja = jar[r];
+          wv[r] = ja < 0 ? -Dv[r] * ja : 0.f;
+        }
       }
       unsigned long long sig_f[4] = {0, 0, 0, 0};
       bool same_f;
-      const int nact = build_active(act, jar, nefc, lane, sig_f, &same_f);
+      const int nact = reg_rows ? build_active1(act, rja, nefc, lane, sig_f, &same_f)
+                                : build_active(act, jar, nefc, lane, sig_f, &same_f);
       sync();
       jt_mul(S + L.qfrc_con, J, wv, act, nact, nvp, lane);
       SUBSTAMP(8);
