@@ -10,7 +10,7 @@ run() {
 }
 run Mjlab-Velocity-Flat-Unitree-G1 4096 200
 run Mjlab-Velocity-Flat-Unitree-Go1 8192 200 --no-cpu-baseline
-run Mjlab-Tracking-Flat-Unitree-G1 4096 100 "--no-cpu-baseline --allow-overflow"
+run Mjlab-Tracking-Flat-Unitree-G1 4096 100 --no-cpu-baseline
 run Mjlab-Jump-Flat-Unitree-G1 16384 60 --no-cpu-baseline
 run Mjlab-Jump-Hfield-Unitree-G1 16384 60 --no-cpu-baseline
 # SURVEY 8f row f3 (not BASELINE configs): the rough box-stair tasks
