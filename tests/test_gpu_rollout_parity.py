@@ -35,10 +35,12 @@ Checks per shadowed substep (fp32 engine vs fp64 oracle):
     qfrc_smooth (oracle_lib.step_given_qacc) against the engine's next state -- qvel per dof
     within QVEL_FLOOR + QVEL_EPS_MUL * eps32 * (v_i + |qvel_i|), v_i the fp32 error scale of
     the implicitfast update; qpos within QPOS_ABS + 4 fp32 ulps of the coordinate + h * that;
-  - sensordata against the oracle's own step within SENS_ABS + SENS_REL |s| (worlds inside
-    the solver model); contact-sensor entries, sums of constraint forces (the solver's dual
-    variables, sensitive where qacc is not), get SENS_FORCE_REL x the world's largest
-    constraint force on top;
+  - sensordata within SENS_ABS + SENS_REL |s| (worlds inside the solver model): contact-
+    sensor entries, sums of constraint forces (the solver's dual variables, sensitive where
+    qacc is not), against the oracle's own step with SENS_FORCE_REL x the world's largest
+    constraint force on top; the other sensors against the oracle's sensors at the engine's
+    own qacc (an acceleration-stage sensor is linear in qacc, so the solver's accepted fp32
+    error would otherwise reach it amplified in heavy worlds);
   - the env step's fused `decimation`-substep mjx_step equal, bit for bit, to that many
     single steps, over every world.
 The multipliers sit at about twice the largest ratio measured over the four configurations
@@ -240,20 +242,27 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
   # sensors against the oracle's own step (contact forces follow the solver's answer; a
   # world outside the sensitivity model is excused)
   s, s_ref = out["sensordata"][i], ref["sensordata"]
-  es = np.abs(s - s_ref)
-  sb = SENS_ABS + SENS_REL * np.abs(s_ref)
+  cs = _contact_sensor_mask(m)
+  # the other sensors against the oracle's sensors at the engine's own qacc (`gpu`, as the
+  # integration check (3)): an acceleration-stage sensor is linear in qacc, and in a heavy
+  # world (tracking, up to 190 rows) the fp32 solver error that check (1) accepts moves an
+  # accelerometer by more than SENS_ABS; the end-to-end difference stays a statistic
+  s_cmp = np.where(cs, s_ref, gpu["sensordata"])
+  stats["sens_e2e_abs"] = max(stats.get("sens_e2e_abs", 0.0),
+                              float(np.abs(s - s_ref)[~cs].max()) if (~cs).any() else 0.0)
+  es = np.abs(s - s_cmp)
+  sb = SENS_ABS + SENS_REL * np.abs(s_cmp)
   # contact-sensor values are sums of constraint forces -- the solver's dual variables,
   # sensitive where qacc is not (a friction row's force moves by D J dq): their slack
   # scales with the world's largest constraint force
   fmax = float(np.abs(ref["efc_force"]).max()) if ref["nefc"] else 0.0
-  cs = _contact_sensor_mask(m)
   if fmax > 0 and cs.any():
     stats["sens_force_rel"] = max(stats.get("sens_force_rel", 0.0), float(es[cs].max()) / fmax)
     sb = sb + np.where(cs, SENS_FORCE_REL * fmax, 0.0)
   if in_model:
     stats["sens_ratio"] = max(stats["sens_ratio"], float((es / sb).max()) if es.size else 0.0)
     _expect((es <= sb).all(), f"{where}: sensordata {int(np.argmax(es / sb))} err {es.max():.3e} "
-            f"(value {float(s_ref[int(np.argmax(es / sb))]):.3e})", stats)
+            f"(value {float(s_cmp[int(np.argmax(es / sb))]):.3e})", stats)
   # (3) end to end against the oracle's own step (statistics: includes both solvers'
   # stopping points)
   stats["e2e_qvel_abs"] = max(stats["e2e_qvel_abs"], float(np.abs(st1["qvel"][i] - ref["qvel"]).max()))
