@@ -162,6 +162,39 @@ def traffic_profile(task, num_envs, nv):
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md: Peak FP32 (matrix))
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md), at the 2.4 GHz peak engine clock
+N_SIMD, VALU_CYCLES_PER_INST, CLOCK_HZ = 1024, 2, 2.4e9
+
+
+def reduce_over_ranks(el: float, dropped, stats: torch.Tensor, device):
+  """The bench's cross-rank bookkeeping, no data-path collective:
+    - episode statistics: one packed fp32 all-gather on a side stream (StatsGather),
+      started first and collected last, so it overlaps the two reductions below;
+    - the timed region: MAX over ranks (the slowest rank sets the job's time);
+    - dropped-contact events: SUM over ranks, so every rank takes the same exit decision.
+  Returns (elapsed, dropped, gathered [world, len(stats)])."""
+  from mjlab_amd import distributed as mjdist
+  gather = mjdist.StatsGather(int(stats.numel()), torch.device(device))
+  gather.start(stats)
+  el = mjdist.max_over_ranks(el, device)
+  dropped = [int(v) for v in mjdist.sum_over_ranks(dropped, device)]
+  return el, dropped, gather.wait()
+
+
+def _launch_ranks(args_gpus: int) -> int:
+  """`bench.py --gpus N` started without a launcher: start the N ranks through
+  torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) before this process
+  touches the GPU, and return their exit status."""
+  import socket
+  import subprocess
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args_gpus}",
+         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+         *sys.argv[1:]]
+  return subprocess.call(cmd)
 
 
 def main():
@@ -182,6 +215,15 @@ def main():
 
   from mjlab_amd import distributed as mjdist
   world, rank, local = mjdist.world_info()
+  if args.gpus < 1:
+    print(f"bench.py: --gpus {args.gpus} must be >= 1", file=sys.stderr)
+    sys.exit(2)
+  if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    sys.exit(_launch_ranks(args.gpus))  # nothing has touched the GPU yet
+  if world != args.gpus:
+    print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+          "(torch.distributed.run --nproc-per-node N), or drop the launcher", file=sys.stderr)
+    sys.exit(2)
   dist = None
   torch.cuda.set_device(local)
   if world > 1:
@@ -256,9 +298,7 @@ def main():
   launch_ms = float(region_ms)
   st = sim.stats()
   if dist is not None:
-    el = mjdist.max_over_ranks(el, device)
-    # episode statistics: one packed all-gather over RCCL
-    mjdist.gather_stats(env.packed_episode_stats())
+    el, dropped, _ = reduce_over_ranks(el, dropped, env.packed_episode_stats(), device)
 
   total = args.steps * args.num_envs * world
   value = total / el
@@ -274,6 +314,8 @@ def main():
     mfma_flops = float(prof.get("mfma_flops_per_env_step", 0.0)) if prof else 0.0
     frac_hbm = max(achieved, traffic_gbps or 0.0) / HBM_PEAK_GBS
     frac_mfma = mfma_flops / launch_s / 1e12 / MFMA_F32_PEAK_TFLOPS
+    valu = float(prof["valu_insts_per_env_step"]) if prof and prof.get("valu_insts_per_env_step") else None
+    frac_valu = (valu * VALU_CYCLES_PER_INST / (N_SIMD * CLOCK_HZ * launch_s)) if valu else None
     bound = "hbm" if frac_hbm >= frac_mfma else "mfma"
     step_path = ("eager" if not graph_path else "sync-free, HIP-graph captured" +
                  (", fused HIP managers" if getattr(env, "_fused", None) is not None else ""))
@@ -301,6 +343,11 @@ def main():
                    "traffic_gbps": traffic_gbps, "traffic_profile": prof_path,
                    "frac_hbm_measured_traffic": (traffic_gbps / HBM_PEAK_GBS) if traffic_gbps else None,
                    "frac_mfma": frac_mfma, "mfma_flops_per_launch": mfma_flops,
+                   # the ceiling that applies to this latency/issue-bound path: VALU issue
+                   # slots used (SQ_INSTS_VALU of the committed SQ pass x 2 cycles over 1,024
+                   # SIMDs x 2.4 GHz x launch time) and each engine kernel's waiting share
+                   "frac_valu_issue": frac_valu, "valu_insts_per_launch": valu,
+                   "wait_share_per_kernel": (prof or {}).get("wait_share_per_kernel"),
                    # what actually bounds the step: per-world dependency latency and issue
                    # (SQ counters in the profile), DESIGN.md section 3
                    "limiter": (prof or {}).get("limiter", "latency/VALU issue (not HBM)")},
@@ -308,13 +355,14 @@ def main():
     }
     if not args.no_cpu_baseline and world == 1:
       out["cpu_baseline"] = cpu_baseline(env, dec)
-    print(json.dumps(out))
-    if any(dropped) and not args.allow_overflow:
-      print(f"bench.py: contacts were dropped in the timed steps (overflow events {dropped}); "
-            "the line above reports them", file=sys.stderr)
-      sys.exit(3)
+    print(json.dumps(out), flush=True)
   if dist is not None:
     dist.destroy_process_group()
+  if any(dropped) and not args.allow_overflow:
+    if rank == 0:
+      print(f"bench.py: contacts were dropped in the timed steps (overflow events {dropped}, "
+            "all ranks); the line above reports them", file=sys.stderr)
+    sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -46,6 +46,16 @@ def max_over_ranks(value: float, device: torch.device | str = "cpu") -> float:
   return float(t.item())
 
 
+def sum_over_ranks(values, device: torch.device | str = "cpu") -> list[float]:
+  """Element-wise sum of a short host vector over ranks (e.g. per-rank event counts)."""
+  vals = [float(v) for v in values]
+  if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    return vals
+  t = torch.tensor(vals, dtype=torch.float64, device=device)
+  dist.all_reduce(t, op=dist.ReduceOp.SUM)
+  return [float(v) for v in t.tolist()]
+
+
 def gather_stats(stats: torch.Tensor, capacity: int | None = None) -> torch.Tensor:
   """All-gather a packed fp32 statistics vector: [world_size, capacity] on every rank.
   Each rank's vector is zero-padded to `capacity` (default: its own length, which must then

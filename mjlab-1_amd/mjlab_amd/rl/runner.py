@@ -10,7 +10,8 @@ With several ranks, the rollout's statistics (finished-episode reward / length s
 counts, and the numeric extras["log"] entries) are packed into one fixed-size vector and
 all-gathered asynchronously on a side stream (distributed.StatsGather) while the PPO update
 runs; rank 0's record then carries the world-wide values under "world/..." (episode means
-over every rank's finished episodes, extras["log"] averaged over ranks).  rsl_rl logs rank
+over every rank's finished episodes, extras["log"] averaged over the ranks that report each
+key; the key set is the union over ranks, agreed on every iteration).  rsl_rl logs rank
 0's local statistics only (docs/api/distributed_training.md:68-100); those stay in the
 record as before.
 """
@@ -72,24 +73,36 @@ class OnPolicyRunner:
         out[k] = v
     return out
 
+  def _agree_keys(self, local: list[str]) -> list[str]:
+    """The union of every rank's extras["log"] keys (sorted), agreed on with one small host
+    all-gather per iteration: ranks can hold different key sets (a rank whose envs did not
+    reset yet, eager `_reset_idx` replacing the dict), and the packed all-gather needs one
+    layout on every rank."""
+    lists = [None] * self.world_size
+    dist.all_gather_object(lists, sorted(local))
+    return sorted(set().union(*[set(x) for x in lists]))
+
   def _start_gather(self, done_rew, done_len, done_cnt, log: dict) -> None:
-    """Pack [reward sum, length sum, episode count, extras["log"] values in a fixed key
-    order] and start the all-gather (no host sync).  The key order is fixed at the first
-    iteration (every rank runs the same task config, so the keys agree)."""
+    """Pack [reward sum, length sum, episode count, the agreed extras["log"] keys' values,
+    and per key a presence flag (1 where this rank has the key)] and start the all-gather (no
+    device sync).  The key list is re-agreed every iteration; the buffers are rebuilt only
+    when it changes (on every rank at once, since every rank sees the same union)."""
     num = self._numeric_log(log)
-    if self._log_keys is None:
-      self._log_keys = sorted(num)
-      self._gather = StatsGather(3 + len(self._log_keys), torch.device(self.device))
+    keys = self._agree_keys(list(num))
+    if keys != self._log_keys or self._gather is None:
+      self._log_keys = keys
+      self._gather = StatsGather(3 + 2 * len(keys), torch.device(self.device))
     dev = done_rew.device
     vals = [done_rew, done_len, done_cnt]
     for k in self._log_keys:
       v = num.get(k, 0.0)
       vals.append(v.to(dev, torch.float32) if isinstance(v, torch.Tensor)
                   else torch.tensor(float(v), device=dev))
+    vals += [torch.tensor(1.0 if k in num else 0.0, device=dev) for k in self._log_keys]
     self._gather.start(torch.stack([v.reshape(()).float() for v in vals]))
 
   def _finish_gather(self, rec: dict) -> None:
-    g = self._gather.wait()  # [world, 3 + nkeys]
+    g = self._gather.wait()  # [world, 3 + 2 nkeys]
     if self.rank != 0:
       return
     g = g.double().cpu()
@@ -97,8 +110,12 @@ class OnPolicyRunner:
     rec["world/episodes"] = cnt
     rec["world/mean_reward"] = float(g[:, 0].sum()) / cnt if cnt > 0 else None
     rec["world/mean_episode_length"] = float(g[:, 1].sum()) / cnt if cnt > 0 else None
+    nk = len(self._log_keys)
     for i, k in enumerate(self._log_keys):
-      rec[f"world/{k}"] = float(g[:, 3 + i].mean())
+      have = g[:, 3 + nk + i]
+      n = float(have.sum())
+      # mean over the ranks that reported the key (missing values are padding, not zeros)
+      rec[f"world/{k}"] = float((g[:, 3 + i] * have).sum()) / n if n > 0 else None
 
   def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False) -> list[dict]:
     env, alg = self.env, self.alg

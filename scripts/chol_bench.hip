@@ -11,7 +11,7 @@
 #include <cstdlib>
 #include <vector>
 #include "engine_impl.h"
-#include "chol_bench_old.h"
+#include "chol_bench_dense.h"
 
 using namespace mjx;
 constexpr int NR = 36;

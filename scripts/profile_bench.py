@@ -122,6 +122,15 @@ def main():
   mfma = sum(v for c, d in sq.items() if "MFMA" in c and "INSTS" in c for v in d.values())
   res["mfma_flops_per_env_step"] = mfma * MFMA_F32_FLOPS
   tot = {c: sum(d.values()) for c, d in sq.items()}
+  if tot.get("SQ_INSTS_VALU"):
+    # the VALU issue ceiling of the bench line (bench.py roofline.frac_valu_issue): wave64
+    # VALU instructions per env step, and per kernel the share of wave-cycles spent waiting
+    res["valu_insts_per_env_step"] = tot["SQ_INSTS_VALU"]
+    wc = sq.get("SQ_WAVE_CYCLES", {})
+    res["wait_share_per_kernel"] = {
+      k: {"wait_inst_any": sq.get("SQ_WAIT_INST_ANY", {}).get(k, 0.0) / c,
+          "wait_any": sq.get("SQ_WAIT_ANY", {}).get(k, 0.0) / c}
+      for k, c in sorted(wc.items(), key=lambda x: -x[1]) if c > 0 and k.startswith("mjx")}
   if tot.get("SQ_WAVE_CYCLES"):
     res["limiter"] = ("latency/issue: wait_any/wave_cycles = %.2f, VALU instructions per world "
                       "step %.0f, VMEM %.0f" % (tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"],

@@ -64,7 +64,8 @@ class _ToyEnv:
   """Vectorised one-step task (act = target), with an extras["log"] entry that differs per
   rank, for the runner's cross-rank statistics path."""
 
-  def __init__(self, n, rank):
+  def __init__(self, n, rank, ragged_keys=False):
+    self.ragged_keys = ragged_keys
     self.num_envs, self.num_actions, self.device = n, 2, torch.device("cpu")
     self.max_episode_length = 1
     self.episode_length_buf = torch.zeros(n, dtype=torch.long)
@@ -85,10 +86,18 @@ class _ToyEnv:
   def step(self, a):
     r = -((a - self.target) ** 2).sum(-1) + 10.0 * self.rank
     self._new()
+    self.calls = getattr(self, "calls", 0) + 1
+    if self.ragged_keys:
+      # the ranks' key sets differ: one key only rank 0 holds, and one that rank 1 starts
+      # reporting after the first iteration (4 env steps)
+      if self.rank == 0:
+        self.extras["log"]["Metrics/only_rank0"] = 3.0
+      elif self.calls > 4:
+        self.extras["log"]["Metrics/late_rank1"] = torch.tensor(7.0)
     return self.obs, r, torch.ones(self.num_envs, dtype=torch.long), {"time_outs": torch.zeros(self.num_envs)}
 
 
-def _runner_worker(rank, world, port, q):
+def _runner_worker(rank, world, port, q, ragged_keys=False):
   os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                     RANK=str(rank), LOCAL_RANK=str(rank))
   from mjlab_amd import distributed as d
@@ -99,9 +108,9 @@ def _runner_worker(rank, world, port, q):
     cfg = RslRlOnPolicyRunnerCfg(
       policy=RslRlPpoActorCriticCfg(actor_hidden_dims=(8,), critic_hidden_dims=(8,)),
       algorithm=RslRlPpoAlgorithmCfg(), num_steps_per_env=4)
-    env = _ToyEnv(32 * (rank + 1), rank)  # different env counts: episode-weighted means
+    env = _ToyEnv(32 * (rank + 1), rank, ragged_keys)  # different env counts: episode-weighted means
     runner = OnPolicyRunner(env, cfg, device="cpu")
-    hist = runner.learn(2)
+    hist = runner.learn(3 if ragged_keys else 2)
     q.put((rank, hist))
   finally:
     import torch.distributed as dist
@@ -131,3 +140,79 @@ def test_two_rank_runner_stats_gather():
     assert abs(r0["world/mean_reward"] - want) < 1e-4 * max(1.0, abs(want))
     assert r0["world/Episode_Termination/time_out"] == 1.5   # (1 + 2) / 2
     assert r0["world/Metrics/constant"] == 5.0
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_runner_ragged_log_keys():
+  """ranks whose extras["log"] key sets differ (and keys that first appear after
+  the first iteration) must still gather into one layout: the union of keys, agreed every
+  iteration, with per-key presence so a missing key is not averaged as zero."""
+  world, port = 2, _free_port()
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  procs = [ctx.Process(target=_runner_worker, args=(r, world, port, q, True)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = dict(q.get(timeout=150) for _ in range(world))
+  for p in procs:
+    p.join(timeout=30)
+    assert p.exitcode == 0
+  h0 = res[0]
+  assert len(h0) == 3
+  for it, r0 in enumerate(h0):
+    assert r0["world/Episode_Termination/time_out"] == 1.5
+    assert r0["world/Metrics/only_rank0"] == 3.0  # rank 0's value, not (3 + 0) / 2
+    if it == 0:
+      assert "world/Metrics/late_rank1" not in r0
+    else:
+      assert r0["world/Metrics/late_rank1"] == 7.0
+
+
+def _bench_worker(rank, world, port, q):
+  """bench.py's rank logic on a CPU stand-in (gloo): per-rank seed, MAX of the elapsed
+  time, SUM of the dropped-contact events, the packed episode-statistics all-gather."""
+  os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                    RANK=str(rank), LOCAL_RANK=str(rank))
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+  import bench
+  from mjlab_amd import distributed as d
+  d.init("gloo")
+  try:
+    seed = d.rank_seed(42, rank)
+    el, dropped, g = bench.reduce_over_ranks(1.0 + 0.5 * rank, [rank, 0, 2 * rank],
+                                             torch.tensor([float(seed), 1.0 + rank]), "cpu")
+    q.put((rank, seed, el, dropped, g.tolist()))
+  finally:
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_bench_reduction():
+  world, port = 2, _free_port()
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = sorted(q.get(timeout=90) for _ in range(world))
+  for p in procs:
+    p.join(timeout=30)
+    assert p.exitcode == 0
+  for rank, seed, el, dropped, g in res:
+    assert seed == 42 + rank
+    assert el == 1.5                      # the slowest rank's time
+    assert dropped == [1, 0, 2]           # summed: every rank exits the same way
+    assert g == [[42.0, 1.0], [43.0, 2.0]]
+
+
+def test_bench_refuses_gpus_world_mismatch():
+  """`--gpus N` must match the launcher's WORLD_SIZE (checked before any GPU call)."""
+  import subprocess
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+  r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1"], env=env,
+                     capture_output=True, text=True, timeout=120)
+  assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
