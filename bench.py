@@ -135,14 +135,39 @@ def cpu_baseline(env, dec, budget_s=12.0, config1_s=4.0):
   t0 = time.perf_counter()
   ol.rollout(m, q1, v1, w1, c1, t1, n1 * dec, nthreads=1, outputs=False)
   el1 = time.perf_counter() - t0
+  # config 1 full env: the task's ManagerBasedRlEnv on the host (torch managers on CPU
+  # tensors, the oracle behind the physics boundary, tests/oracle_sim.py), num_envs = 1,
+  # zero actions, measure_throughput.py's 50 warm-up + 200 timed env steps
+  from oracle_sim import make_cpu_env
+  task = getattr(env, "_bench_task", "Mjlab-Velocity-Flat-Unitree-G1")
+  torch_threads = torch.get_num_threads()
+  torch.set_num_threads(1)
+  try:
+    cenv = make_cpu_env(task, num_envs=1, seed=42)
+    cenv.reset()
+    za = torch.zeros(1, cenv.action_manager.total_action_dim)
+    for _ in range(50):
+      cenv.step(za)
+    t0 = time.perf_counter()
+    for _ in range(200):
+      cenv.step(za)
+    el_full = time.perf_counter() - t0
+  finally:
+    torch.set_num_threads(torch_threads)
   return {"value": nw * nsteps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+          "label": "CPU restatement of MuJoCo semantics (fp64 oracle, oracle/oracle.c), not MuJoCo-C",
           "sample": f"{nw} of the bench's worlds (states as the timed region left them) x "
                     f"{nsteps} env-steps ({dec} substeps each), new uniform[-1,1) actions per "
                     "env step through the action scale/offset, fp64 oracle, physics only",
           "host_cores_visible": aff, "cgroup_cpus": cgroup_cpus(),
           "config1": {"value": n1 / el1, "unit": "env-steps/s", "cores": 1, "num_envs": 1,
                       "sample": f"1 world x {n1} env-steps from the init keyframe, zero action "
-                                "(--agent zero), single thread, fp64 oracle, physics only"}}
+                                "(--agent zero), single thread, fp64 oracle, physics only",
+                      "full_env": {"value": 200 / el_full, "unit": "env-steps/s", "cores": 1,
+                                   "sample": f"{task} ManagerBasedRlEnv on the host, num_envs=1, "
+                                             "zero action, 50 warm-up + 200 timed env.step calls; "
+                                             "torch managers on CPU tensors (1 thread) + fp64 oracle "
+                                             "physics (tests/oracle_sim.py)"}}}
 
 
 def traffic_profile(task, num_envs, nv):
@@ -233,6 +258,7 @@ def main():
 
   from mjlab_amd.envs import make_env
   env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
+  env._bench_task = args.task
   sim = env.sim
   m = sim.mj_model
   dec = env.cfg.decimation

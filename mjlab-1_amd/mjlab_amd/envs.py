@@ -100,7 +100,7 @@ class ManagerBasedRlEnv:
     self.scene = Scene(model, cfg.scene.num_envs, device, cfg.scene.entities,
                        cfg.scene.contact_sensors, cfg.scene.env_spacing,
                        max_init_terrain_level=cfg.scene.max_init_terrain_level)
-    self.sim = Simulation(num_envs=cfg.scene.num_envs, cfg=cfg.sim, model=model, device=device)
+    self.sim = self._make_sim(model, device)
     self.scene.initialize(self.sim.mj_model, self.sim.model, self.sim.data)
     self.common_step_counter = 0
     self.episode_length_buf = torch.zeros(cfg.scene.num_envs, device=device, dtype=torch.long)
@@ -108,6 +108,11 @@ class ManagerBasedRlEnv:
     self.sync_free = False
     self._use_graph = False
     self.load_managers()
+
+  def _make_sim(self, model, device: str):
+    """The physics boundary (`envs/manager_based_rl_env.py:117-122`): the HIP engine.  There
+    is no CPU fallback; `Simulation` refuses a non-ROCm device."""
+    return Simulation(num_envs=self.cfg.scene.num_envs, cfg=self.cfg.sim, model=model, device=device)
 
   @property
   def num_envs(self) -> int:

@@ -92,19 +92,27 @@ def quat_from_euler_xyz(roll: torch.Tensor, pitch: torch.Tensor, yaw: torch.Tens
 
 
 def quat_from_matrix(m: torch.Tensor) -> torch.Tensor:
-  """Rotation matrix (..., 9) or (..., 3, 3) -> quaternion with w >= 0."""
+  """Rotation matrix (..., 9) or (..., 3, 3) -> quaternion (w, x, y, z), as
+  `utils/lab_api/math.py:318-372`: of the four quaternion components the largest in magnitude
+  is formed from the trace-like sum, the others from the matrix's off-diagonal sums and
+  differences divided by it (the best-conditioned candidate; that component comes out
+  positive)."""
   if m.shape[-1] == 9:
     m = m.reshape(m.shape[:-1] + (3, 3))
-  m00, m11, m22 = m[..., 0, 0], m[..., 1, 1], m[..., 2, 2]
-  w = torch.sqrt(torch.clamp(1 + m00 + m11 + m22, min=0)) * 0.5
-  x = torch.sqrt(torch.clamp(1 + m00 - m11 - m22, min=0)) * 0.5
-  y = torch.sqrt(torch.clamp(1 - m00 + m11 - m22, min=0)) * 0.5
-  z = torch.sqrt(torch.clamp(1 - m00 - m11 + m22, min=0)) * 0.5
-  x = torch.copysign(x, m[..., 2, 1] - m[..., 1, 2])
-  y = torch.copysign(y, m[..., 0, 2] - m[..., 2, 0])
-  z = torch.copysign(z, m[..., 1, 0] - m[..., 0, 1])
-  q = torch.stack([w, x, y, z], dim=-1)
-  return q / torch.linalg.norm(q, dim=-1, keepdim=True).clamp(min=1e-12)
+  m00, m01, m02 = m[..., 0, 0], m[..., 0, 1], m[..., 0, 2]
+  m10, m11, m12 = m[..., 1, 0], m[..., 1, 1], m[..., 1, 2]
+  m20, m21, m22 = m[..., 2, 0], m[..., 2, 1], m[..., 2, 2]
+  four = torch.stack([1 + m00 + m11 + m22, 1 + m00 - m11 - m22, 1 - m00 + m11 - m22,
+                      1 - m00 - m11 + m22], dim=-1)
+  mag = torch.sqrt(torch.clamp(four, min=0))  # 2 |q_i|
+  rows = torch.stack([
+    torch.stack([four[..., 0], m21 - m12, m02 - m20, m10 - m01], dim=-1),
+    torch.stack([m21 - m12, four[..., 1], m10 + m01, m02 + m20], dim=-1),
+    torch.stack([m02 - m20, m10 + m01, four[..., 2], m12 + m21], dim=-1),
+    torch.stack([m10 - m01, m20 + m02, m21 + m12, four[..., 3]], dim=-1)], dim=-2)
+  k = mag.argmax(dim=-1, keepdim=True)
+  best = torch.gather(rows, -2, k.unsqueeze(-1).expand(*k.shape[:-1], 1, 4)).squeeze(-2)
+  return best / (2.0 * torch.gather(mag, -1, k).clamp(min=0.1))
 
 
 def matrix_from_quat(q: torch.Tensor) -> torch.Tensor:

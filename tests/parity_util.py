@@ -43,13 +43,15 @@ def oracle_step(model, q, qv, qws, ctrl, step=True, nconmax=64, njmax=160):
 
 def expanded_fields(sim) -> list[str]:
   """Model fields the sim holds one copy of per world (Simulation.expand_model_fields)."""
+  from mjlab_amd._lib import lib
   out = []
   for name in sim.mj_model.arrays:
     try:
-      t = getattr(sim.model, name)
+      getattr(sim.model, name)
     except AttributeError:
       continue
-    if t.dim() > 0 and t.shape[0] == sim.num_envs and sim.num_envs > 1 and t.stride(0) != 0:
+    # the engine's own record (a one-world sim has no stride to tell an expanded field by)
+    if lib().mjx_field_is_expanded(sim._sim, name.encode()):
       out.append(name)
   return out
 
