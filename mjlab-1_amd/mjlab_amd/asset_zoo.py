@@ -9,7 +9,12 @@ damping = 2 * 2.0 * armature * (2*pi*10Hz), effort limits from the motor specs.
 
 from __future__ import annotations
 
+import json
+import os
+
 from .compiler.model import CollisionEdit, PositionActuatorGroup
+
+ROBOT_DIR = os.path.join(os.path.dirname(__file__), "assets", "robots")
 
 _NATURAL_FREQ = 10 * 2.0 * 3.1415926535
 _DAMPING_RATIO = 2.0
@@ -133,3 +138,51 @@ def action_scale(groups) -> dict[str, float]:
     for n in g.joint_names_expr:
       out[n] = 0.25 * g.effort_limit / g.stiffness
   return out
+
+
+# --------------------------------------------------------------------------- robot entities
+def robot_spec(name: str):
+  """The robot's MJCF as parsed data (`assets/robots/<name>.json`, written by
+  scripts/build_assets.py from the reference's `asset_zoo/robots/*/xmls/*.xml`; visual meshes
+  are frames only) as a fresh `Spec` -- the `spec_fn` of the robot's EntityCfg
+  (`g1_constants.py:33-36` `get_spec`)."""
+  from .compiler.mjcf import xmodel_from_dict
+  from .spec import Spec
+  path = os.path.join(ROBOT_DIR, f"{name}.json")
+  if not os.path.exists(path):
+    raise FileNotFoundError(f"robot description {path} missing; run scripts/build_assets.py")
+  with open(path) as fh:
+    return Spec(xmodel_from_dict(json.load(fh)))
+
+
+def get_g1_spec():
+  return robot_spec("unitree_g1")
+
+
+def get_go1_spec():
+  return robot_spec("unitree_go1")
+
+
+def _init_state(d):
+  from .entity import InitialStateCfg
+  return InitialStateCfg(pos=tuple(d["pos"]), joint_pos=dict(d["joint_pos"]),
+                         joint_vel={".*": 0.0})
+
+
+def get_g1_robot_cfg(init: dict | None = None):
+  """`g1_constants.py:260-285` (`get_g1_robot_cfg`): knees-bent init, full collision, the six
+  builtin position-actuator groups, soft joint limits at 90 %."""
+  from .entity import EntityArticulationInfoCfg, EntityCfg
+  return EntityCfg(init_state=_init_state(init or G1_KNEES_BENT), spec_fn=get_g1_spec,
+                   collisions=(G1_FULL_COLLISION,),
+                   articulation=EntityArticulationInfoCfg(actuators=g1_actuators(),
+                                                          soft_joint_pos_limit_factor=0.9))
+
+
+def get_go1_robot_cfg():
+  """`go1_constants.py:140-160` (`get_go1_robot_cfg`)."""
+  from .entity import EntityArticulationInfoCfg, EntityCfg
+  return EntityCfg(init_state=_init_state(GO1_INIT), spec_fn=get_go1_spec,
+                   collisions=(GO1_FULL_COLLISION,),
+                   articulation=EntityArticulationInfoCfg(actuators=go1_actuators(),
+                                                          soft_joint_pos_limit_factor=0.9))

@@ -305,3 +305,41 @@ def geom_frame(attrs: dict, angle_deg: bool, eulerseq: str):
   pos = np.asarray(attrs["pos"], dtype=np.float64)
   quat = _orientation(attrs, angle_deg, eulerseq)
   return pos, quat, np.array(size[:3], dtype=np.float64)
+
+
+# --------------------------------------------------------------------------- serialisation
+def _attrs_out(a: dict) -> dict:
+  return {k: (list(v) if isinstance(v, (tuple, np.ndarray)) else v) for k, v in a.items()}
+
+
+def _attrs_in(a: dict) -> dict:
+  return {k: (tuple(v) if isinstance(v, list) else v) for k, v in a.items()}
+
+
+def xmodel_to_dict(xm: XModel) -> dict:
+  """The parsed MJCF tree as plain JSON-able data (defaults already resolved), so a robot
+  description travels as data: `xmodel_from_dict` rebuilds the identical tree."""
+  def body(b: XBody) -> dict:
+    return dict(name=b.name, pos=[float(x) for x in b.pos], quat=[float(x) for x in b.quat],
+                inertial=_attrs_out(b.inertial) if b.inertial is not None else None,
+                mocap=bool(b.mocap),
+                joints=[dict(name=j.name, attrs=_attrs_out(j.attrs)) for j in b.joints],
+                geoms=[dict(name=g.name, attrs=_attrs_out(g.attrs)) for g in b.geoms],
+                sites=[dict(name=s.name, attrs=_attrs_out(s.attrs)) for s in b.sites],
+                children=[body(c) for c in b.children])
+  return dict(name=xm.name, world=body(xm.world), excludes=[list(e) for e in xm.excludes],
+              sensors=[[t, dict(a)] for t, a in xm.sensors], angle_deg=xm.angle_deg,
+              eulerseq=xm.eulerseq, inertiafromgeom=xm.inertiafromgeom)
+
+
+def xmodel_from_dict(d: dict) -> XModel:
+  def body(b: dict) -> XBody:
+    return XBody(name=b["name"], pos=np.array(b["pos"], float), quat=np.array(b["quat"], float),
+                 inertial=_attrs_in(b["inertial"]) if b["inertial"] is not None else None,
+                 joints=[XJoint(j["name"], _attrs_in(j["attrs"])) for j in b["joints"]],
+                 geoms=[XGeom(g["name"], _attrs_in(g["attrs"])) for g in b["geoms"]],
+                 sites=[XSite(s["name"], _attrs_in(s["attrs"])) for s in b["sites"]],
+                 children=[body(c) for c in b["children"]], mocap=bool(b["mocap"]))
+  return XModel(d["name"], body(d["world"]), [tuple(e) for e in d["excludes"]],
+                [(t, dict(a)) for t, a in d["sensors"]], bool(d["angle_deg"]), d["eulerseq"],
+                d.get("inertiafromgeom", "auto"))

@@ -139,6 +139,7 @@ class EntitySpec:
   init_pos: tuple = (0.0, 0.0, 0.0)
   init_rot: tuple = (1.0, 0.0, 0.0, 0.0)
   init_joint_pos: dict | None = None
+  key_qpos: np.ndarray | None = None  # the entity's own keyframe qpos (init joint_pos=None)
 
 
 @dataclass
@@ -824,6 +825,18 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
   key = qpos0.copy()
   for ent, jorder in keyframe_parts:
     prefix = f"{ent.name}/" if ent.name else ""
+    if ent.key_qpos is not None:
+      # the entity's own keyframe (entity.py:171-182), in its joint order
+      own = [k for k, j in enumerate(joints) if j["name"].startswith(prefix)]
+      width = sum(nqj[int(jtype[k])] for k in own)
+      if np.asarray(ent.key_qpos).size != width:
+        raise ValueError(f"entity '{ent.name}': keyframe qpos size {np.asarray(ent.key_qpos).size} != {width}")
+      off = 0
+      for k in own:
+        a, w = A["jnt_qposadr"][k], nqj[int(jtype[k])]
+        key[a:a + w] = np.asarray(ent.key_qpos, float)[off:off + w]
+        off += w
+      continue
     for k, j in enumerate(joints):
       if not j["name"].startswith(prefix):
         continue

@@ -24,20 +24,11 @@ from .managers import (ActionManager, CommandManager, CurriculumManager, Curricu
                        ObservationGroupCfg, ObservationManager, ObservationTermCfg,
                        RewardManager, RewardTermCfg, SceneEntityCfg, TerminationManager,
                        TerminationTermCfg, UniformNoiseCfg)
-from .scene import Scene
-from .scenes import load_scene
+from .entity import EntityCfg  # noqa: F401  (re-exported: the reference's mjlab.entity)
+from .scene import Scene, SceneCfg
+from .sensor import ContactMatch, ContactSensorCfg
 from .sim import MujocoCfg, Simulation, SimulationCfg
-
-
-@dataclass
-class SceneCfg:
-  scene_name: str = "g1_velocity"
-  num_envs: int = 1
-  env_spacing: float = 2.0
-  entities: dict = field(default_factory=lambda: {"robot": {"soft_joint_pos_limit_factor": 0.9}})
-  contact_sensors: dict = field(default_factory=dict)
-  # generator terrains (TerrainImporterCfg.max_init_terrain_level): highest initial level
-  max_init_terrain_level: int | None = None
+from .terrains import TerrainImporterCfg, rough_terrains_cfg
 
 
 @dataclass(kw_only=True)
@@ -96,10 +87,10 @@ class ManagerBasedRlEnv:
     self.extras: dict[str, Any] = {}
     self.obs_buf = {}
     self._fused = None
-    model = load_scene(cfg.scene.scene_name)
-    self.scene = Scene(model, cfg.scene.num_envs, device, cfg.scene.entities,
-                       cfg.scene.contact_sensors, cfg.scene.env_spacing,
-                       max_init_terrain_level=cfg.scene.max_init_terrain_level)
+    # the scene is assembled from cfg.scene (entities, terrain, sensors) and compiled here
+    # (`envs/manager_based_rl_env.py:115-122`)
+    self.scene = Scene(cfg.scene, device)
+    model = self.scene.compile()
     self.sim = self._make_sim(model, device)
     self.scene.initialize(self.sim.mj_model, self.sim.model, self.sim.data)
     self.common_step_counter = 0
@@ -380,8 +371,10 @@ class ManagerBasedRlEnv:
 
 
 # =========================================================================== task configs
-def make_velocity_env_cfg(scene_name: str) -> ManagerBasedRlEnvCfg:
-  """`tasks/velocity/velocity_env_cfg.py:33-354` (flat terrain variant)."""
+def make_velocity_env_cfg() -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/velocity_env_cfg.py:33-354`: the rough-terrain scene (ROUGH_TERRAINS_CFG,
+  `max_init_terrain_level` 5; the reference draws the generator seed at random, this build
+  fixes it at 0) with no entity yet; the robot configs add the robot and its sensors."""
   policy = {
     "base_lin_vel": ObservationTermCfg(func=mdp.builtin_sensor, params={"sensor_name": "robot/imu_lin_vel"},
                                        noise=UniformNoiseCfg(n_min=-0.5, n_max=0.5)),
@@ -468,8 +461,13 @@ def make_velocity_env_cfg(scene_name: str) -> ManagerBasedRlEnvCfg:
       {"step": 0, "lin_vel_x": (-1.0, 1.0), "ang_vel_z": (-0.5, 0.5)},
       {"step": 5000 * 24, "lin_vel_x": (-1.5, 2.0), "ang_vel_z": (-0.7, 0.7)},
       {"step": 10000 * 24, "lin_vel_x": (-2.0, 3.0)}]})}
+  curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
+                                                    params={"command_name": "twist"}),
+                **curriculum}
+  scene = SceneCfg(num_envs=1, terrain=TerrainImporterCfg(
+    terrain_type="generator", terrain_generator=rough_terrains_cfg(seed=0), max_init_terrain_level=5))
   return ManagerBasedRlEnvCfg(
-    scene=SceneCfg(scene_name=scene_name, num_envs=1), observations=observations,
+    scene=scene, observations=observations,
     actions=actions, commands=commands, events=events, rewards=rewards,
     terminations=terminations, curriculum=curriculum,
     sim=SimulationCfg(nconmax=35, njmax=300, mujoco=MujocoCfg(timestep=0.005, iterations=10,
@@ -477,40 +475,63 @@ def make_velocity_env_cfg(scene_name: str) -> ManagerBasedRlEnvCfg:
     decimation=4, episode_length_s=20.0)
 
 
+def _flat(cfg: ManagerBasedRlEnvCfg) -> ManagerBasedRlEnvCfg:
+  """`tasks/velocity/config/g1/env_cfgs.py:153-175`: plane terrain, no terrain curriculum."""
+  cfg.scene.terrain.terrain_type = "plane"
+  cfg.scene.terrain.terrain_generator = None
+  del cfg.curriculum["terrain_levels"]
+  return cfg
+
+
+def _rough(cfg: ManagerBasedRlEnvCfg, play: bool) -> ManagerBasedRlEnvCfg:
+  """Rough terrain in curriculum layout (`env_cfgs.py:51-52`); play mode
+  (`env_cfgs.py:131-148`): the random-layout 5 x 5 grid with a 10 m border and the
+  randomize_terrain reset event."""
+  if play:
+    cfg.scene.terrain.terrain_generator = rough_terrains_cfg(
+      seed=0, curriculum=False, num_rows=5, num_cols=5, border_width=10.0)
+    _rough_play_events(cfg)
+  else:
+    cfg.scene.terrain.terrain_generator.curriculum = True
+  return cfg
+
+
 def unitree_g1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/g1/env_cfgs.py:20-175` (flat)."""
-  return _g1_velocity_cfg("g1_velocity", play)
+  cfg = _g1_velocity_cfg(play)
+  if play:
+    t = cfg.commands["twist"]
+    t.ranges.lin_vel_x = (-1.5, 2.0)
+    t.ranges.ang_vel_z = (-0.7, 0.7)
+  return _flat(cfg)
 
 
 def unitree_g1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
-  """`tasks/velocity/config/g1/env_cfgs.py:20-148` (rough): the flat G1 task on the
-  box-stair terrain grid in curriculum layout (`velocity_env_cfg.py:318-324`,
-  max_init_terrain_level 5) with the terrain-level curriculum
-  (`velocity_env_cfg.py:296-300`).  Play mode: the random-layout 5 x 5 grid and the
-  randomize_terrain reset event (`tasks/velocity/config/g1/env_cfgs.py:131-148`)."""
-  cfg = _g1_velocity_cfg("g1_velocity_rough_play" if play else "g1_velocity_rough", play)
-  cfg.scene.max_init_terrain_level = 5
-  cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
-                                                        params={"command_name": "twist"}),
-                    **cfg.curriculum}
-  if play:
-    _rough_play_events(cfg)
-  return cfg
+  """`tasks/velocity/config/g1/env_cfgs.py:20-148` (rough): the G1 velocity task on the
+  box-stair terrain grid with the terrain-level curriculum (`velocity_env_cfg.py:296-300`)."""
+  return _rough(_g1_velocity_cfg(play), play)
 
 
 def _rough_play_events(cfg) -> None:
   """Play mode of the rough tasks (`tasks/velocity/config/{g1,go1}/env_cfgs.py`, play
-  overrides): every reset puts the env on a random sub-terrain (`randomize_terrain`); the
-  scene is the random-layout 5 x 5 grid with a 10 m border (scenes._rough_play_cfg)."""
+  overrides): every reset puts the env on a random sub-terrain (`randomize_terrain`)."""
   cfg.events["randomize_terrain"] = EventTermCfg(func=mdp.randomize_terrain, mode="reset", params={})
 
 
-def _g1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
-  cfg = make_velocity_env_cfg(scene_name)
-  cfg.scene.contact_sensors = {
-    "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
-    "self_collision": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
-  }
+def _g1_velocity_cfg(play: bool) -> ManagerBasedRlEnvCfg:
+  cfg = make_velocity_env_cfg()
+  cfg.scene.entities = {"robot": az.get_g1_robot_cfg()}
+  cfg.scene.sensors = (
+    ContactSensorCfg(name="feet_ground_contact",
+                     primary=ContactMatch(mode="subtree", entity="robot",
+                                          pattern=r"^(left_ankle_roll_link|right_ankle_roll_link)$"),
+                     secondary=ContactMatch(mode="body", pattern="terrain"),
+                     fields=("found", "force"), reduce="netforce", num_slots=1, track_air_time=True),
+    ContactSensorCfg(name="self_collision",
+                     primary=ContactMatch(mode="subtree", pattern="pelvis", entity="robot"),
+                     secondary=ContactMatch(mode="subtree", pattern="pelvis", entity="robot"),
+                     fields=("found",), reduce="none", num_slots=1),
+  )
   sites = ("left_foot", "right_foot")
   geoms = tuple(f"{s}_foot{i}_collision" for s in ("left", "right") for i in range(1, 8))
   cfg.actions["joint_pos"].scale = az.action_scale(az.g1_actuators())
@@ -541,38 +562,36 @@ def _g1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
     cfg.episode_length_s = int(1e9)
     cfg.observations["policy"].enable_corruption = False
     cfg.events.pop("push_robot", None)
-    t = cfg.commands["twist"]
-    t.ranges.lin_vel_x = (-1.5, 2.0)
-    t.ranges.ang_vel_z = (-0.7, 0.7)
   return cfg
 
 
 def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/go1/env_cfgs.py:15-127` (flat)."""
-  return _go1_velocity_cfg("go1_velocity", play)
+  return _flat(_go1_velocity_cfg(play))
 
 
 def unitree_go1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
-  """`tasks/velocity/config/go1/env_cfgs.py:15-112` (rough): the flat Go1 task on the
-  curriculum box-stair grid with the terrain-level curriculum (as unitree_g1_rough_env_cfg)."""
-  cfg = _go1_velocity_cfg("go1_velocity_rough_play" if play else "go1_velocity_rough", play)
-  cfg.scene.max_init_terrain_level = 5
-  cfg.curriculum = {"terrain_levels": CurriculumTermCfg(func=mdp.terrain_levels_vel,
-                                                        params={"command_name": "twist"}),
-                    **cfg.curriculum}
-  if play:
-    _rough_play_events(cfg)
-  return cfg
+  """`tasks/velocity/config/go1/env_cfgs.py:15-112` (rough): the Go1 task on the curriculum
+  box-stair grid with the terrain-level curriculum."""
+  return _rough(_go1_velocity_cfg(play), play)
 
 
-def _go1_velocity_cfg(scene_name: str, play: bool) -> ManagerBasedRlEnvCfg:
-  cfg = make_velocity_env_cfg(scene_name)
-  cfg.scene.contact_sensors = {
-    "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True},
-    "nonfoot_ground_touch": {"fields": ("found",), "num_slots": 1, "track_air_time": False},
-  }
+def _go1_velocity_cfg(play: bool) -> ManagerBasedRlEnvCfg:
+  cfg = make_velocity_env_cfg()
+  cfg.scene.entities = {"robot": az.get_go1_robot_cfg()}
   names = ("FR", "FL", "RR", "RL")
   geoms = tuple(f"{n}_foot_collision" for n in names)
+  cfg.scene.sensors = (
+    ContactSensorCfg(name="feet_ground_contact",
+                     primary=ContactMatch(mode="geom", pattern=geoms, entity="robot"),
+                     secondary=ContactMatch(mode="body", pattern="terrain"),
+                     fields=("found", "force"), reduce="netforce", num_slots=1, track_air_time=True),
+    ContactSensorCfg(name="nonfoot_ground_touch",
+                     primary=ContactMatch(mode="geom", entity="robot", pattern=r".*_collision\d*$",
+                                          exclude=geoms),
+                     secondary=ContactMatch(mode="body", pattern="terrain"),
+                     fields=("found",), reduce="none", num_slots=1),
+  )
   cfg.actions["joint_pos"].scale = az.action_scale(az.go1_actuators())
   cfg.observations["critic"].terms["foot_height"].params["asset_cfg"].site_names = names
   cfg.events["foot_friction"].params["asset_cfg"].geom_names = geoms

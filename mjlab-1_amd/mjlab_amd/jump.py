@@ -305,8 +305,14 @@ def make_jump_env_cfg(scene_name: str = "g1_jump"):
         {"step": 0, "weight": 1.0}, {"step": 15000 * 24, "weight": 2.5},
         {"step": 30000 * 24, "weight": 4.0}]}),
   }
+  from .terrains import TerrainImporterCfg, hf_rough_terrains_cfg
+  if scene_name == "g1_jump_hfield":
+    # config 5: the jump cfg re-terrained onto the seeded heightfield grid
+    terrain = TerrainImporterCfg(terrain_type="generator", terrain_generator=hf_rough_terrains_cfg(seed=0))
+  else:
+    terrain = TerrainImporterCfg(terrain_type="plane")
   return ManagerBasedRlEnvCfg(
-    scene=SceneCfg(scene_name=scene_name, num_envs=4096), observations=observations,
+    scene=SceneCfg(num_envs=4096, terrain=terrain), observations=observations,
     actions=actions, commands=commands, events=events, rewards=rewards,
     terminations=terminations, curriculum=curriculum,
     sim=SimulationCfg(nconmax=35, njmax=300, mujoco=MujocoCfg(timestep=0.002, iterations=10,
@@ -317,9 +323,15 @@ def make_jump_env_cfg(scene_name: str = "g1_jump"):
 def unitree_g1_jump_env_cfg(play: bool = False, scene_name: str = "g1_jump"):
   """`tasks/jump/config/g1/env_cfgs.py:49-112`."""
   from . import asset_zoo as az
+  from .sensor import ContactMatch, ContactSensorCfg
   cfg = make_jump_env_cfg(scene_name)
-  cfg.scene.contact_sensors = {
-    "feet_ground_contact": {"fields": ("found", "force"), "num_slots": 1, "track_air_time": True}}
+  cfg.scene.entities = {"robot": az.get_g1_robot_cfg(az.G1_JUMP_CROUCH)}
+  cfg.scene.sensors = (ContactSensorCfg(
+    name="feet_ground_contact",
+    primary=ContactMatch(mode="subtree", entity="robot",
+                         pattern=r"^(left_ankle_roll_link|right_ankle_roll_link)$"),
+    secondary=ContactMatch(mode="body", pattern="terrain"),
+    fields=("found", "force"), reduce="netforce", num_slots=1, track_air_time=True),)
   cfg.actions["joint_pos"].scale = az.action_scale(az.g1_actuators())
   cfg.observations["critic"].terms["foot_height"].params["asset_cfg"].site_names = (
     "left_foot", "right_foot")

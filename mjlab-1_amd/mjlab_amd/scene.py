@@ -3,15 +3,15 @@ engine's device fields.
 
 Mirrors `src/mjlab/entity/entity.py:390-825`, `src/mjlab/entity/data.py:20-533`,
 `src/mjlab/sensor/builtin_sensor.py`, `src/mjlab/sensor/contact_sensor.py:199-367` and
-`src/mjlab/scene/scene.py:120-198`.  The scene is compiled ahead of time
-(mjlab_amd/scenes.py), so `Scene` binds to the compiled model's name tables instead of
-editing an MjSpec.
+`src/mjlab/scene/scene.py:29-198`.  The scene is assembled at env construction
+from a `SceneCfg` (entities, terrain, sensors) by this build's MJCF compiler, and the runtime
+views bind to the compiled model's name tables.
 """
 
 from __future__ import annotations
 
 import re
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -651,61 +651,141 @@ class Terrain:
                                                      self.terrain_types[env_ids]]
 
 
-class Scene:
-  """Entities + sensors + env origins for a compiled scene (scene/scene.py)."""
+@dataclass(kw_only=True)
+class SceneCfg:
+  """`scene/scene.py:18-26`."""
+  num_envs: int = 1
+  env_spacing: float = 2.0
+  terrain: object | None = None        # terrains.TerrainImporterCfg
+  entities: dict = field(default_factory=dict)   # name -> entity.EntityCfg
+  sensors: tuple = field(default_factory=tuple)  # sensor.ContactSensorCfg, ...
+  extent: float | None = None
+  spec_fn: object | None = None
 
-  def __init__(self, mj_model, num_envs: int, device: str, entities: dict[str, dict],
-               contact_sensors: dict[str, dict], env_spacing: float = 2.0,
-               max_init_terrain_level: int | None = None):
-    self._m = mj_model
-    self.num_envs = num_envs
+
+class Scene:
+  """The scene of an env (`scene/scene.py:29-198`): built from a `SceneCfg` at env
+  construction -- terrain, each entity's spec attached under `<name>/`, the contact sensors
+  expanded over the entities, the merged keyframe -- and compiled by `compile()` into the
+  flat model the engine loads.  `initialize` then binds the runtime views (entities,
+  sensors, env origins) to the simulation's device fields."""
+
+  def __init__(self, scene_cfg: SceneCfg, device: str):
+    from .entity import EntityBuild
+    if scene_cfg.spec_fn is not None:
+      raise NotImplementedError("SceneCfg.spec_fn: scene-level MjSpec edits (edit the entity "
+                                "specs through EntityCfg.spec_fn instead)")
+    self._cfg = scene_cfg
+    self.num_envs = int(scene_cfg.num_envs)
     self.device = device
-    self._entities = {n: Entity(n, mj_model, **kw) for n, kw in entities.items()}
-    self._sensors: dict = {}
+    self._builds = {name: EntityBuild(name, ecfg) for name, ecfg in scene_cfg.entities.items()}
+    self._terrain_geoms, self._terrain_origins, self._terrain_size = None, None, None
+    t = scene_cfg.terrain
+    self._terrain_kind = "none"
+    if t is not None:
+      t.num_envs = self.num_envs
+      t.env_spacing = scene_cfg.env_spacing
+      if t.terrain_type == "plane":
+        self._terrain_kind = "plane"
+      elif t.terrain_type == "generator":
+        from .terrains import TerrainGenerator
+        if t.terrain_generator is None:
+          raise ValueError("terrain_type 'generator' needs a terrain_generator cfg")
+        self._terrain_kind = "generator"
+        geoms, origins = TerrainGenerator(t.terrain_generator).generate()
+        self._terrain_geoms, self._terrain_origins = geoms, origins
+        self._terrain_size = tuple(float(v) for v in t.terrain_generator.size)
+      else:
+        raise ValueError(f"unknown terrain_type {t.terrain_type!r}")
+    self._sensor_cfgs = {}
+    self._contact_specs = []
+    for sc in scene_cfg.sensors:
+      if not hasattr(sc, "expand"):
+        raise NotImplementedError(f"sensor cfg {type(sc).__name__}")
+      self._contact_specs.append(sc.expand(self._builds))
+      self._sensor_cfgs[sc.name] = sc
+    self._model = None
+
+  def compile(self):
+    """`MjSpec.compile()` of the assembled scene (scene/scene.py:47-48)."""
+    from .compiler.model import compile_scene
+    ents = [b.entity_spec() for b in self._builds.values()]
+    m = compile_scene(ents, terrain=self._terrain_kind, terrain_geoms=self._terrain_geoms,
+                      contact_sensors=self._contact_specs)
+    if self._terrain_origins is not None:
+      m.arrays["terrain_origins"] = np.asarray(self._terrain_origins, np.float64)
+      m.arrays["terrain_size"] = np.asarray(self._terrain_size, np.float64)
+    self._model = m
+    return m
+
+  @property
+  def cfg(self) -> SceneCfg:
+    return self._cfg
+
+  @property
+  def env_spacing(self) -> float:
+    return self._cfg.env_spacing
+
+  def _bind(self, mj_model) -> None:
+    """Runtime entities and sensors over the compiled model's name tables."""
+    self._m = mj_model
+    self._entities = {}
+    for name, b in self._builds.items():
+      art = b.cfg.articulation
+      init = b.cfg.init_state
+      self._entities[name] = Entity(
+        name, mj_model, soft_joint_pos_limit_factor=art.soft_joint_pos_limit_factor if art else 1.0,
+        init_lin_vel=init.lin_vel, init_ang_vel=init.ang_vel)
+    self._sensors = {}
     names = mj_model.names["sensor"]
-    adr = mj_model.sensor_adr
-    dim = mj_model.sensor_dim
+    adr, dim = mj_model.sensor_adr, mj_model.sensor_dim
     for i, n in enumerate(names):
       if mj_model.sensor_type[i] != 4:  # builtin
         self._sensors[n] = BuiltinSensor(n, int(adr[i]), int(dim[i]))
-    for cname, spec in contact_sensors.items():
+    for cname, sc in self._sensor_cfgs.items():
       slots = []
       for i, n in enumerate(names):
         if mj_model.sensor_type[i] == 4 and n.startswith(cname + "_"):
-          rest = n[len(cname) + 1:]
-          prim, fld = rest.rsplit("_", 1)
+          prim, fld = n[len(cname) + 1:].rsplit("_", 1)
           slots.append((prim, fld, int(adr[i]), int(dim[i])))
-      self._sensors[cname] = ContactSensor(cname, slots, spec["fields"], spec.get("num_slots", 1),
-                                           spec.get("track_air_time", False))
+      self._sensors[cname] = ContactSensor(cname, slots, sc.fields, sc.num_slots, sc.track_air_time)
     self.terrain = None
+    t = self._cfg.terrain
     if "terrain_origins" in mj_model.arrays:
       # generator terrain: curriculum origins over the sub-terrain spawn points
       # (terrain_importer.py:224-244), drawn from torch's global RNG like the reference
       size = tuple(float(v) for v in mj_model.arrays.get("terrain_size", (8.0, 8.0)))
-      self.terrain = Terrain(mj_model.arrays["terrain_origins"], size, num_envs, device,
-                             max_init_terrain_level)
+      self.terrain = Terrain(mj_model.arrays["terrain_origins"], size, self.num_envs, self.device,
+                             t.max_init_terrain_level if t is not None else None)
       self.env_origins = self.terrain.env_origins
       self.terrain_levels, self.terrain_types = self.terrain.terrain_levels, self.terrain.terrain_types
       return
-    # env origins on a grid (terrain_importer.py:246-261)
+    if t is None:
+      # no terrain: every env at the origin (scene/scene.py:128-130)
+      self.env_origins = torch.zeros(self.num_envs, 3, device=self.device)
+      return
+    # plane: env origins on a grid (terrain_importer.py:246-261)
+    num_envs, spacing = self.num_envs, float(self._cfg.env_spacing)
     rows = int(np.ceil(num_envs / int(np.sqrt(num_envs))))
     cols = int(np.ceil(num_envs / rows))
-    ii, jj = torch.meshgrid(torch.arange(rows, device=device), torch.arange(cols, device=device),
-                            indexing="ij")
-    o = torch.zeros(num_envs, 3, device=device)
-    o[:, 0] = -(ii.flatten()[:num_envs] - (rows - 1) / 2) * env_spacing
-    o[:, 1] = (jj.flatten()[:num_envs] - (cols - 1) / 2) * env_spacing
+    ii, jj = torch.meshgrid(torch.arange(rows, device=self.device),
+                            torch.arange(cols, device=self.device), indexing="ij")
+    o = torch.zeros(num_envs, 3, device=self.device)
+    o[:, 0] = -(ii.flatten()[:num_envs] - (rows - 1) / 2) * spacing
+    o[:, 1] = (jj.flatten()[:num_envs] - (cols - 1) / 2) * spacing
     self.env_origins = o
 
   def __getitem__(self, key):
-    if key in self._entities:
-      return self._entities[key]
+    if key == "terrain":
+      if self.terrain is None:
+        raise KeyError("No terrain configured in this scene.")
+      return self.terrain
     if key in self._sensors:
       return self._sensors[key]
-    if key.startswith("robot/") and key in self._sensors:
-      return self._sensors[key]
-    raise KeyError(f"'{key}' not found in scene (entities {list(self._entities)}, "
-                   f"sensors {list(self._sensors)})")
+    if key in self._entities:
+      return self._entities[key]
+    available = list(self._entities) + list(self._sensors)
+    raise KeyError(f"Scene element '{key}' not found. Available: {available}")
 
   @property
   def entities(self):
@@ -716,6 +796,7 @@ class Scene:
     return self._sensors
 
   def initialize(self, mj_model, model, data):
+    self._bind(mj_model)
     for e in self._entities.values():
       e.initialize(mj_model, model, data, self.device)
     for s in self._sensors.values():

@@ -136,6 +136,39 @@ class SpecBody:
   quat = property(lambda self: np.array(self._x.quat, float))
   mocap = property(lambda self: bool(self._x.mocap))
 
+  # MjsBody.mass / ipos / inertia: the body's <inertial> (bodies whose inertia comes from their
+  # geoms have none to edit; give them one first)
+  def _inertial(self) -> dict:
+    if self._x.inertial is None:
+      raise NotImplementedError(f"body '{self.name}': no explicit <inertial> to edit")
+    return self._x.inertial
+
+  @property
+  def mass(self) -> float:
+    return float(self._x.inertial.get("mass", 0.0)) if self._x.inertial is not None else 0.0
+
+  @mass.setter
+  def mass(self, v: float) -> None:
+    self._inertial()["mass"] = float(v)
+
+  @property
+  def ipos(self) -> np.ndarray:
+    return np.array(self._inertial().get("pos", (0.0, 0.0, 0.0)), float)
+
+  @ipos.setter
+  def ipos(self, v) -> None:
+    self._inertial()["pos"] = _vec(v, 3)
+
+  @property
+  def inertia(self) -> np.ndarray:
+    return np.array(self._inertial().get("diaginertia", (0.0, 0.0, 0.0)), float)
+
+  @inertia.setter
+  def inertia(self, v) -> None:
+    inr = self._inertial()
+    inr.pop("fullinertia", None)
+    inr["diaginertia"] = _vec(v, 3)
+
   def add_body(self, name: str = "", pos=(0, 0, 0), quat=(1, 0, 0, 0), mocap: bool = False,
                mass: float | None = None, ipos=(0, 0, 0), inertia=None) -> "SpecBody":
     xb = XBody(name, np.array(_vec(pos, 3)), quat_normalize(_vec(quat, 4)), None, mocap=mocap)

@@ -300,6 +300,18 @@ class TerrainGeneratorCfg:
   difficulty_range: tuple[float, float] = (0.0, 1.0)
 
 
+@dataclass
+class TerrainImporterCfg:
+  """`terrains/terrain_importer.py:30-60`: a plane (env origins on a grid of `env_spacing`)
+  or a generated terrain (`terrain_generator`, env origins from its sub-terrain spawn points
+  with the curriculum's initial levels up to `max_init_terrain_level`)."""
+  terrain_type: str = "plane"
+  terrain_generator: TerrainGeneratorCfg | None = None
+  env_spacing: float | None = 2.0
+  max_init_terrain_level: int | None = None
+  num_envs: int = 1
+
+
 class TerrainGenerator:
   """`terrain_generator.py:62-249`: patch grid centred at the origin; random layout
   (per-patch proportion draw + uniform difficulty) or curriculum layout (type per column,

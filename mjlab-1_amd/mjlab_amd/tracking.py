@@ -607,6 +607,7 @@ def make_tracking_env_cfg():
   """`tasks/tracking/tracking_env_cfg.py:44-317`."""
   from .envs import ManagerBasedRlEnvCfg, SceneCfg
   from .sim import MujocoCfg, SimulationCfg
+  from .terrains import TerrainImporterCfg
   U = UniformNoiseCfg
   policy = {
     "command": ObservationTermCfg(func=mdp.generated_commands, params={"command_name": "motion"}),
@@ -693,7 +694,8 @@ def make_tracking_env_cfg():
       **m, "threshold": 0.25, "body_names": ()}),
   }
   return ManagerBasedRlEnvCfg(
-    scene=SceneCfg(scene_name="g1_tracking", num_envs=1), observations=observations,
+    scene=SceneCfg(num_envs=1, terrain=TerrainImporterCfg(terrain_type="plane")),
+    observations=observations,
     actions=actions, commands=commands, events=events, rewards=rewards,
     terminations=terminations,
     # the reference's njmax (250 rows per world) held in full: random-action tracking worlds
@@ -707,9 +709,13 @@ def unitree_g1_flat_tracking_env_cfg(has_state_estimation: bool = True, play: bo
                                      motion_file: str = SYNTHETIC_G1_MOTION):
   """`tasks/tracking/config/g1/env_cfgs.py:15-100`."""
   from . import asset_zoo as az
+  from .sensor import ContactMatch, ContactSensorCfg
   cfg = make_tracking_env_cfg()
-  cfg.scene.contact_sensors = {
-    "self_collision": {"fields": ("found",), "num_slots": 1, "track_air_time": False}}
+  cfg.scene.entities = {"robot": az.get_g1_robot_cfg()}
+  cfg.scene.sensors = (ContactSensorCfg(
+    name="self_collision", primary=ContactMatch(mode="subtree", pattern="pelvis", entity="robot"),
+    secondary=ContactMatch(mode="subtree", pattern="pelvis", entity="robot"),
+    fields=("found",), reduce="none", num_slots=1),)
   cfg.actions["joint_pos"].scale = az.action_scale(az.g1_actuators())
   mc = cfg.commands["motion"]
   mc.motion_file = motion_file

@@ -14,16 +14,18 @@ from mjlab_amd.scenes import load_scene
 
 
 def test_play_configs():
-  for task, scene in (("Mjlab-Velocity-Rough-Unitree-G1", "g1_velocity_rough_play"),
-                      ("Mjlab-Velocity-Rough-Unitree-Go1", "go1_velocity_rough_play")):
+  for task in ("Mjlab-Velocity-Rough-Unitree-G1", "Mjlab-Velocity-Rough-Unitree-Go1"):
     cfg = load_env_cfg(task, play=True)
-    assert cfg.scene.scene_name == scene
+    tg = cfg.scene.terrain.terrain_generator
+    assert (tg.num_rows, tg.num_cols, tg.border_width, tg.curriculum) == (5, 5, 10.0, False)
     ev = cfg.events["randomize_terrain"]
     assert ev.func is mdp.randomize_terrain and ev.mode == "reset" and ev.params == {}
     assert "push_robot" not in cfg.events and not cfg.observations["policy"].enable_corruption
     assert cfg.episode_length_s == int(1e9)
     train = load_env_cfg(task, play=False)
-    assert "randomize_terrain" not in train.events and not train.scene.scene_name.endswith("_play")
+    assert "randomize_terrain" not in train.events
+    tg = train.scene.terrain.terrain_generator
+    assert (tg.num_rows, tg.num_cols, tg.border_width, tg.curriculum) == (10, 20, 20.0, True)
 
 
 def test_play_grid_is_random_layout():

@@ -1,0 +1,76 @@
+"""`Scene(scene_cfg, device)` as the env's construction path (`src/mjlab/scene/scene.py:29-48`,
+`entity/entity.py:127-207`): every shipped task's SceneCfg (robot entity
+from the shipped robot description, collision edits, actuator groups, init keyframe,
+terrain, contact-sensor expansion) compiles to exactly the model of its compiled scene
+asset (`mjlab_amd/assets/<scene>.npz`, built by scripts/build_assets.py from the reference
+MJCF), and a cfg edit reaches the compiled model."""
+
+import numpy as np
+import pytest
+
+from mjlab_amd.envs import load_env_cfg
+from mjlab_amd.scene import Scene
+from mjlab_amd.scenes import load_scene
+
+TASKS = [("Mjlab-Velocity-Flat-Unitree-G1", False, "g1_velocity"),
+         ("Mjlab-Velocity-Flat-Unitree-Go1", False, "go1_velocity"),
+         ("Mjlab-Velocity-Rough-Unitree-G1", False, "g1_velocity_rough"),
+         ("Mjlab-Velocity-Rough-Unitree-Go1", False, "go1_velocity_rough"),
+         ("Mjlab-Velocity-Rough-Unitree-G1", True, "g1_velocity_rough_play"),
+         ("Mjlab-Velocity-Rough-Unitree-Go1", True, "go1_velocity_rough_play"),
+         ("Mjlab-Tracking-Flat-Unitree-G1", False, "g1_tracking"),
+         ("Mjlab-Jump-Flat-Unitree-G1", False, "g1_jump"),
+         ("Mjlab-Jump-Hfield-Unitree-G1", False, "g1_jump_hfield")]
+
+
+def _same(a, b):
+  assert (a.nq, a.nv, a.nu, a.nbody, a.ngeom, a.nsite, a.nsensor, a.nsensordata, a.npair) == \
+         (b.nq, b.nv, b.nu, b.nbody, b.ngeom, b.nsite, b.nsensor, b.nsensordata, b.npair)
+  assert a.names == b.names
+  assert set(a.arrays) == set(b.arrays), set(a.arrays) ^ set(b.arrays)
+  for k in a.arrays:
+    x, y = np.asarray(a.arrays[k]), np.asarray(b.arrays[k])
+    assert x.shape == y.shape and np.array_equal(x, y), k
+  assert a.meaninertia == b.meaninertia
+
+
+@pytest.mark.parametrize("task,play,asset", TASKS)
+def test_task_scene_compiles_to_its_asset(task, play, asset):
+  cfg = load_env_cfg(task, play)
+  m = Scene(cfg.scene, "cpu").compile()
+  _same(m, load_scene(asset))
+
+
+def test_scene_cfg_edits_reach_the_model():
+  """A contact sensor added, a foot geom's friction and a body mass changed in cfg.scene."""
+  from mjlab_amd.sensor import ContactMatch, ContactSensorCfg
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  robot = cfg.scene.entities["robot"]
+  base_fn = robot.spec_fn
+
+  def heavier_torso():
+    spec = base_fn()
+    spec.body("torso_link").mass = spec.body("torso_link").mass + 2.5
+    return spec
+
+  robot.spec_fn = heavier_torso
+  robot.collisions[0].friction[r"^(left|right)_foot[1-7]_collision$"] = (0.9,)
+  cfg.scene.sensors = cfg.scene.sensors + (ContactSensorCfg(
+    name="hands", primary=ContactMatch(mode="body", entity="robot",
+                                       pattern=r"^(left|right)_wrist_yaw_link$"),
+    secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "force"),
+    reduce="netforce"),)
+  m = Scene(cfg.scene, "cpu").compile()
+  base = load_scene("g1_velocity")
+  tb = base.names["body"].index("robot/torso_link")
+  assert m.body_mass[tb] == pytest.approx(base.body_mass[tb] + 2.5)
+  feet = [i for i, n in enumerate(m.names["geom"]) if "foot" in n and n.endswith("_collision")]
+  assert len(feet) == 14 and np.all(m.geom_friction[feet, 0] == 0.9)
+  assert np.all(base.geom_friction[feet, 0] == 0.6)
+  new = [n for n in m.names["sensor"] if n.startswith("hands_")]
+  assert new == ["hands_left_wrist_yaw_link_found", "hands_left_wrist_yaw_link_force",
+                 "hands_right_wrist_yaw_link_found", "hands_right_wrist_yaw_link_force"]
+  assert m.nsensordata == base.nsensordata + 8
+  # the mass change reaches the engine's constants (subtree mass, invweight)
+  pel = base.names["body"].index("robot/pelvis")
+  assert m.body_subtreemass[pel] == pytest.approx(base.body_subtreemass[pel] + 2.5)
