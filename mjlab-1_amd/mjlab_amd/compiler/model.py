@@ -131,6 +131,16 @@ class ContactSensorSpec:
 
 
 @dataclass
+class BuiltinSensorSpec:
+  """A builtin sensor added by the scene config (`sensor/builtin_sensor.py:279-305`): MJCF tag
+  (gyro, accelerometer, jointpos, ...), its object attribute ({"site" | "body" | "joint":
+  prefixed name}) and the sensor's full name."""
+  tag: str
+  attrs: dict
+  name: str
+
+
+@dataclass
 class EntitySpec:
   name: str
   xml: XModel
@@ -755,7 +765,9 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     smask2.append(mk2 if mk2 is not None else np.zeros(nmw, np.uint32))
     adr += dim
 
-  for tag, attrs, name in xml_sensors:
+  def push_builtin(tag, attrs, name):
+    if tag not in _SENSOR_TAGS:
+      raise NotImplementedError(f"sensor '{name}': type {tag!r} (supported: {sorted(_SENSOR_TAGS)})")
     t = _SENSOR_TAGS[tag]
     if "site" in attrs:
       ot, oi = OBJ_SITE, m.names["site"].index(attrs["site"])
@@ -766,6 +778,9 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
     else:
       raise ValueError(f"unsupported sensor attrs {attrs}")
     push(t, ot, oi, OBJ_NONE, -1, _SENSOR_DIM[t], name=name)
+
+  for tag, attrs, name in xml_sensors:
+    push_builtin(tag, attrs, name)
 
   children = [[] for _ in range(nbody)]
   for b in range(1, nbody):
@@ -798,6 +813,9 @@ def compile_scene(entities: list[EntitySpec], *, terrain: str = "plane",
 
   objmode = {"geom": OBJ_GEOM, "body": OBJ_BODY, "subtree": OBJ_XBODY}
   for cs in contact_sensors:
+    if isinstance(cs, BuiltinSensorSpec):  # scene-config sensors keep the config's order
+      push_builtin(cs.tag, cs.attrs, cs.name)
+      continue
     for prim in cs.primary_names:
       for fld in cs.fields:
         m1 = geom_mask(cs.primary_mode, prim)

@@ -158,8 +158,10 @@ def root_height_below_minimum(env, minimum_height: float, asset_cfg=_ROBOT):
 
 
 def nan_detection(env):
-  d = env.sim.data
-  return torch.isnan(d.qpos).any(-1) | torch.isnan(d.qvel).any(-1)
+  """`envs/mdp/terminations.py:45-47`: NaN or Inf anywhere in qpos, qvel, qacc or
+  qacc_warmstart of the env (NanGuard.detect_nans)."""
+  from .sim.sim import NanGuard
+  return NanGuard.detect_nans(env.sim.data)
 
 
 def illegal_contact(env, sensor_name: str):

@@ -697,13 +697,24 @@ class Scene:
         self._terrain_size = tuple(float(v) for v in t.terrain_generator.size)
       else:
         raise ValueError(f"unknown terrain_type {t.terrain_type!r}")
+    from .sensor import BuiltinSensorCfg
+    xml_sensors = {f"{n}/{a.get('name', '')}" for n, b in self._builds.items()
+                   for _, a in b.spec._xml.sensors}
     self._sensor_cfgs = {}
     self._contact_specs = []
     for sc in scene_cfg.sensors:
       if not hasattr(sc, "expand"):
         raise NotImplementedError(f"sensor cfg {type(sc).__name__}")
+      if isinstance(sc, BuiltinSensorCfg) and sc.name in xml_sensors | set(self._sensor_cfgs):
+        if sc.obj is not None and sc.obj.entity is not None:
+          raise ValueError(f"Sensor '{sc.name}' is defined in both entity XML and scene config. "
+                           "Remove the sensor definition from the entity XML file, or remove the "
+                           "BuiltinSensorCfg from scene.sensors.")
+        raise ValueError(f"Sensor '{sc.name}' already exists in the scene. Rename this sensor "
+                         "to avoid conflicts.")
       self._contact_specs.append(sc.expand(self._builds))
-      self._sensor_cfgs[sc.name] = sc
+      if not isinstance(sc, BuiltinSensorCfg):
+        self._sensor_cfgs[sc.name] = sc
     self._model = None
 
   def compile(self):

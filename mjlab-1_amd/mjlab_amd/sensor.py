@@ -13,7 +13,7 @@ import re
 from dataclasses import dataclass
 from typing import Literal
 
-from .compiler.model import ContactSensorSpec
+from .compiler.model import BuiltinSensorSpec, ContactSensorSpec
 
 
 @dataclass
@@ -107,3 +107,83 @@ class ContactSensorCfg:
       return names[0]
     raise ValueError(f"Secondary pattern '{match.pattern}' matched multiple: {names}. "
                      "Be explicit or set secondary_policy='first' or 'any'.")
+
+
+# ----------------------------------------------------------------------------- builtin sensors
+_REQUIRES_SITE = {"accelerometer", "velocimeter", "gyro", "force", "torque", "magnetometer",
+                  "rangefinder"}
+_REQUIRES_FRAME = {"framepos", "framequat", "framexaxis", "frameyaxis", "framezaxis",
+                   "framelinvel", "frameangvel", "framelinacc", "frameangacc"}
+_REQUIRES_BODY = {"subtreecom", "subtreelinvel", "subtreeangmom"}
+_REQUIRES_OBJ = {"jointpos": "joint", "jointvel": "joint", "jointlimitpos": "joint",
+                 "jointlimitvel": "joint", "jointlimitfrc": "joint", "jointactuatorfrc": "joint",
+                 "tendonpos": "tendon", "tendonvel": "tendon", "tendonactuatorfrc": "tendon",
+                 "actuatorpos": "actuator", "actuatorvel": "actuator", "actuatorfrc": "actuator"}
+_FRAME_TYPES = {"body", "xbody", "geom", "site", "camera"}
+# what the engine evaluates: sensor type -> the object types it takes
+_ENGINE = {"accelerometer": {"site"}, "velocimeter": {"site"}, "gyro": {"site"},
+           "framepos": {"site", "xbody"}, "framequat": {"site", "xbody"},
+           "jointpos": {"joint"}, "jointvel": {"joint"}, "subtreeangmom": {"body"}}
+
+
+@dataclass
+class ObjRef:
+  """`builtin_sensor.py:171-189`."""
+  type: Literal["body", "xbody", "joint", "geom", "site", "actuator", "tendon", "camera"]
+  name: str
+  entity: str | None = None
+
+  def prefixed_name(self) -> str:
+    return f"{self.entity}/{self.name}" if self.entity else self.name
+
+
+@dataclass
+class BuiltinSensorCfg:
+  """`builtin_sensor.py:195-250`: a MuJoCo builtin sensor added by the scene config; the
+  name is entity-prefixed when `obj` names an entity.  The object-type rules are checked at
+  construction as the reference does; types the engine does not evaluate raise at scene
+  construction (`expand`)."""
+  name: str
+  sensor_type: str
+  obj: ObjRef | None = None
+  ref: ObjRef | None = None
+  cutoff: float = 0.0
+
+  def __post_init__(self) -> None:
+    if self.obj is not None and self.obj.entity is not None:
+      self.name = f"{self.obj.entity}/{self.name}"
+    st = self.sensor_type
+    if st in _REQUIRES_SITE:
+      if self.obj is None:
+        raise ValueError(f"Sensor type '{st}' requires obj with type='site'")
+      if self.obj.type != "site":
+        raise ValueError(f"Sensor type '{st}' requires obj.type='site', got '{self.obj.type}'")
+    elif st in _REQUIRES_FRAME:
+      if self.obj is None:
+        raise ValueError(f"Sensor type '{st}' requires obj with spatial frame")
+      if self.obj.type not in _FRAME_TYPES:
+        raise ValueError(f"Sensor type '{st}' requires obj.type in {_FRAME_TYPES}, got '{self.obj.type}'")
+    elif st in _REQUIRES_BODY:
+      if self.obj is None:
+        raise ValueError(f"Sensor type '{st}' requires obj with type='body'")
+      if self.obj.type != "body":
+        raise ValueError(f"Sensor type '{st}' requires obj.type='body', got '{self.obj.type}'")
+    elif st in _REQUIRES_OBJ:
+      req = _REQUIRES_OBJ[st]
+      if self.obj is None:
+        raise ValueError(f"Sensor type '{st}' requires obj with type='{req}'")
+      if self.obj.type != req:
+        raise ValueError(f"Sensor type '{st}' requires obj.type='{req}', got '{self.obj.type}'")
+    if self.ref is not None and st not in _REQUIRES_FRAME:
+      raise ValueError(f"Sensor type '{st}' does not support ref specification")
+
+  def expand(self, entities: dict) -> BuiltinSensorSpec:
+    del entities
+    st, obj = self.sensor_type, self.obj
+    if st not in _ENGINE or obj is None or obj.type not in _ENGINE[st]:
+      raise NotImplementedError(f"sensor '{self.name}': {st} on a {obj.type if obj else None} "
+                                f"(the engine evaluates {_ENGINE})")
+    if self.ref is not None or self.cutoff > 0:
+      raise NotImplementedError(f"sensor '{self.name}': ref frames and cutoff")
+    key = {"site": "site", "xbody": "body", "body": "body", "joint": "joint"}[obj.type]
+    return BuiltinSensorSpec(st, {key: obj.prefixed_name()}, self.name)

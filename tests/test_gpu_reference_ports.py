@@ -1,0 +1,719 @@
+"""The reference's own hot-path tests, ported to run on the HIP engine.
+
+Each test keeps the reference's inline MJCF, scene assembly and assertions, with this build's
+classes in place of mujoco / mujoco_warp (`mujoco.MjSpec.from_string` -> `Spec.from_string`,
+`mujoco.MjModel.from_xml_string` -> a compiled `Spec`).  The tests that step physics also
+compare the engine's sensordata at the final state with the fp64 oracle's (`_matches_oracle`),
+so the qualitative answers the reference pins are checked against the oracle too.
+
+  - tests/test_contact_sensor.py:147-757 (contact sensor: found / force / fields, pattern
+    lists and regexes, reduce modes, excludes, body / subtree modes, air time, num_slots);
+  - tests/test_builtin_sensor.py:70-190, 270-305 (accelerometer non-zero after falling, ...);
+  - tests/test_terminations.py:44-103 (nan_detection, and through the termination manager);
+  - tests/test_encoder_bias.py:104-307 (encoder bias in observations and actions, identical
+    physics under bias compensation, the randomize_encoder_bias event);
+  - tests/test_sim_data.py:67-75 (the device bridge refuses attribute assignment).
+"""
+
+from __future__ import annotations
+
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as ol
+from mjlab_amd.compiler.model import SENS_CONTACT
+from mjlab_amd.entity import BuiltinPositionActuatorCfg, EntityArticulationInfoCfg, EntityCfg
+from mjlab_amd.scene import Scene, SceneCfg
+from mjlab_amd.sensor import BuiltinSensorCfg, ContactMatch, ContactSensorCfg, ObjRef
+from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+from mjlab_amd.spec import Spec
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def device(gpu_device):
+  return gpu_device
+
+
+def _matches_oracle(sim):
+  """The engine's forward at the current state against the oracle's, per world: contact
+  counts equal, sensordata within the rollout parity test's sensor bounds (contact-sensor
+  entries with 6e-3 x the largest constraint force on top)."""
+  sim.forward()
+  torch.cuda.synchronize()
+  m = sim.mj_model
+  d = sim.data
+  q, v, ws, c = (getattr(d, k).double().cpu().numpy() for k in ("qpos", "qvel", "qacc_warmstart", "ctrl"))
+  t = d.time.double().cpu().numpy().reshape(-1)
+  sd = d.sensordata.double().cpu().numpy()
+  ncon = d.ncon.cpu().numpy().reshape(-1)
+  cs = np.zeros(m.nsensordata, bool)
+  for ty, a, dm in zip(m.sensor_type, m.sensor_adr, m.sensor_dim):
+    cs[a:a + dm] |= int(ty) == SENS_CONTACT
+  for w in range(sim.num_envs):
+    ref = ol.forward(m, q[w], v[w], ws[w], c[w], float(t[w]), nconmax=sim.nconmax, njmax=sim.njmax)
+    assert int(ncon[w]) == ref["ncon"], f"world {w}: ncon {int(ncon[w])} vs oracle {ref['ncon']}"
+    fmax = float(np.abs(ref["efc_force"]).max()) if ref["nefc"] else 0.0
+    bound = 1e-2 + 1e-3 * np.abs(ref["sensordata"]) + np.where(cs, 6e-3 * fmax, 0.0)
+    err = np.abs(sd[w] - ref["sensordata"])
+    assert (err <= bound).all(), f"world {w}: sensordata {int(np.argmax(err - bound))} err {err.max():.3e}"
+
+
+# ============================================================================ contact sensor
+FALLING_BOX_XML = """
+<mujoco>
+  <worldbody>
+    <body name="ground" pos="0 0 0">
+      <geom name="ground_geom" type="plane" size="5 5 0.1" rgba="0.5 0.5 0.5 1"/>
+    </body>
+    <body name="box" pos="0 0 0.5">
+      <freejoint name="box_joint"/>
+      <geom name="box_geom" type="box" size="0.1 0.1 0.1" rgba="0.8 0.3 0.3 1"
+        mass="1.0"/>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+BIPED_XML = """
+<mujoco>
+  <worldbody>
+    <body name="ground" pos="0 0 0">
+      <geom name="ground_geom" type="plane" size="5 5 0.1" rgba="0.5 0.5 0.5 1"/>
+    </body>
+    <body name="base" pos="0 0 0.5">
+      <freejoint name="base_joint"/>
+      <geom name="torso_geom" type="box" size="0.15 0.1 0.2" mass="5.0"/>
+      <body name="left_foot" pos="0.1 0 -0.25">
+        <joint name="left_ankle" type="hinge" axis="0 1 0" range="-0.5 0.5"/>
+        <geom name="left_foot_geom" type="box" size="0.05 0.08 0.02" mass="0.2"/>
+      </body>
+      <body name="right_foot" pos="-0.1 0 -0.25">
+        <joint name="right_ankle" type="hinge" axis="0 1 0" range="-0.5 0.5"/>
+        <geom name="right_foot_geom" type="box" size="0.05 0.08 0.02" mass="0.2"/>
+      </body>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+SIMPLE_ROBOT_XML = """
+<mujoco>
+  <worldbody>
+    <body name="ground" pos="0 0 0">
+      <geom name="ground_geom" type="plane" size="5 5 0.1"/>
+    </body>
+    <body name="robot" pos="0 0 0.3">
+      <freejoint name="robot_joint"/>
+      <geom name="trunk_collision" type="box" size="0.2 0.15 0.1" mass="2.0"/>
+      <geom name="head_collision" type="sphere" size="0.08" pos="0.25 0 0.1"
+      mass="0.5"/>
+      <body name="leg1" pos="0.1 0.1 -0.1">
+        <geom name="leg1_thigh_collision1" type="capsule" size="0.02"
+          fromto="0 0 0 0 0 -0.1"/>
+        <geom name="leg1_thigh_collision2" type="capsule" size="0.02"
+          fromto="0 0 -0.05 0 0 -0.15"/>
+        <geom name="leg1_foot_collision" type="sphere" size="0.03" pos="0 0 -0.2"/>
+      </body>
+      <body name="leg2" pos="-0.1 0.1 -0.1">
+        <geom name="leg2_thigh_collision1" type="capsule" size="0.02"
+          fromto="0 0 0 0 0 -0.1"/>
+        <geom name="leg2_thigh_collision2" type="capsule" size="0.02"
+          fromto="0 0 -0.05 0 0 -0.15"/>
+        <geom name="leg2_foot_collision" type="sphere" size="0.03" pos="0 0 -0.2"/>
+      </body>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+
+def create_scene_with_sensor(xml, entity_name, sensor_cfg, device, num_envs=2, njmax=75):
+  entity_cfg = EntityCfg(spec_fn=lambda: Spec.from_string(xml))
+  scene_cfg = SceneCfg(num_envs=num_envs, env_spacing=3.0, entities={entity_name: entity_cfg},
+                       sensors=(sensor_cfg,))
+  scene = Scene(scene_cfg, device)
+  model = scene.compile()
+  sim = Simulation(num_envs=num_envs, cfg=SimulationCfg(njmax=njmax), model=model, device=device)
+  scene.initialize(sim.mj_model, sim.model, sim.data)
+  return scene, sim
+
+
+def step_and_settle(sim, num_steps=30):
+  for _ in range(num_steps):
+    sim.step()
+
+
+def _place(entity, sim, z):
+  root_state = torch.zeros((sim.num_envs, 13), device=sim.device)
+  root_state[:, 2] = z
+  root_state[:, 3] = 1.0
+  entity.write_root_state_to_sim(root_state)
+  return root_state
+
+
+def test_basic_contact_detection(device):
+  cfg = ContactSensorCfg(name="box_contact",
+                         primary=ContactMatch(mode="geom", pattern="box_geom", entity="box"),
+                         secondary=None, fields=("found", "force"))
+  scene, sim = create_scene_with_sensor(FALLING_BOX_XML, "box", cfg, device)
+  sensor, box = scene["box_contact"], scene["box"]
+  _place(box, sim, 0.11)
+  step_and_settle(sim)
+  data = sensor.data
+  assert data.found is not None and data.force is not None
+  assert data.found.shape == (2, 1)
+  assert data.force.shape[-1] == 3
+  assert torch.any(data.found > 0)
+  assert torch.any(torch.abs(data.force[data.found > 0]) > 0)
+  _matches_oracle(sim)
+
+
+def test_contact_fields(device):
+  cfg = ContactSensorCfg(name="box_contact",
+                         primary=ContactMatch(mode="geom", pattern="box_geom", entity="box"),
+                         secondary=None, fields=("found", "force", "torque", "dist", "pos", "normal"))
+  scene, sim = create_scene_with_sensor(FALLING_BOX_XML, "box", cfg, device)
+  sensor, box = scene["box_contact"], scene["box"]
+  _place(box, sim, 0.105)
+  step_and_settle(sim, num_steps=10)
+  data = sensor.data
+  for f in ("found", "force", "torque", "dist", "pos", "normal"):
+    assert getattr(data, f) is not None
+  for f in ("force", "torque", "pos", "normal"):
+    assert getattr(data, f).shape[-1] == 3
+  assert len(data.dist.shape) == 2
+  _matches_oracle(sim)
+
+
+def test_multi_slot_pattern_matching(device):
+  cfg = ContactSensorCfg(name="feet_contact",
+                         primary=ContactMatch(mode="geom", pattern=("left_foot_geom", "right_foot_geom"),
+                                              entity="biped"),
+                         secondary=None, fields=("found", "force"), track_air_time=True)
+  scene, sim = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  sensor, biped = scene["feet_contact"], scene["biped"]
+  _place(biped, sim, 0.25)
+  step_and_settle(sim, num_steps=20)
+  data = sensor.data
+  assert data.found.shape == (2, 2)
+  assert data.force.shape == (2, 2, 3)
+  assert hasattr(data, "current_air_time")
+  assert data.current_air_time.shape == (2, 2)
+  _matches_oracle(sim)
+
+
+def test_regex_pattern_matching(device):
+  cfg = ContactSensorCfg(name="all_feet_contact",
+                         primary=ContactMatch(mode="geom", pattern=r".*foot_geom$", entity="biped"),
+                         secondary=None, fields=("found", "force"))
+  scene, sim = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  sensor, biped = scene["all_feet_contact"], scene["biped"]
+  assert sensor.data.found.shape == (2, 2)
+  _place(biped, sim, 0.24)
+  step_and_settle(sim, num_steps=20)
+  data = sensor.data
+  assert torch.any(data.found > 0)
+  assert data.force is not None and data.force.shape == (2, 2, 3)
+  _matches_oracle(sim)
+
+
+@pytest.mark.parametrize("reduce_mode", ["none", "mindist", "maxforce", "netforce"])
+def test_reduce_modes(device, reduce_mode):
+  cfg = ContactSensorCfg(name="box_contact",
+                         primary=ContactMatch(mode="geom", pattern="box_geom", entity="box"),
+                         secondary=None, fields=("force",), reduce=reduce_mode, num_slots=1)
+  scene, sim = create_scene_with_sensor(FALLING_BOX_XML, "box", cfg, device)
+  data = scene["box_contact"].data
+  assert len(data.force.shape) == 3
+  assert data.force.shape[-1] == 3
+  # and with the box resting on the plane (4 corner contacts): the engine's reduction of
+  # them against the oracle's
+  _place(scene["box"], sim, 0.1)
+  step_and_settle(sim, num_steps=10)
+  _matches_oracle(sim)
+
+
+def test_reduce_modes_multiple_contacts(device):
+  cfg = ContactSensorCfg(name="feet_contact",
+                         primary=ContactMatch(mode="geom", pattern=("left_foot_geom", "right_foot_geom"),
+                                              entity="biped"),
+                         secondary=None, fields=("found", "force", "dist"), reduce="mindist",
+                         num_slots=1)
+  scene, sim = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  _place(scene["biped"], sim, 0.25)
+  step_and_settle(sim, num_steps=20)
+  data = scene["feet_contact"].data
+  assert data.found.shape == (2, 2)
+  assert data.force.shape == (2, 2, 3)
+  _matches_oracle(sim)
+
+
+def test_exclude_exact_names(device):
+  cfg = ContactSensorCfg(name="nonfoot_contact",
+                         primary=ContactMatch(mode="geom", pattern=r".*_collision\d*$", entity="robot",
+                                              exclude=("leg1_foot_collision", "leg2_foot_collision")),
+                         secondary=None, fields=("found",))
+  scene, _ = create_scene_with_sensor(SIMPLE_ROBOT_XML, "robot", cfg, device)
+  assert scene["nonfoot_contact"].data.found.shape == (2, 6)
+
+
+def test_exclude_regex_pattern(device):
+  cfg = ContactSensorCfg(name="no_thigh_contact",
+                         primary=ContactMatch(mode="geom", pattern=r".*_collision\d*$", entity="robot",
+                                              exclude=(r".*thigh_collision\d+",)),
+                         secondary=None, fields=("found",))
+  scene, _ = create_scene_with_sensor(SIMPLE_ROBOT_XML, "robot", cfg, device)
+  assert scene["no_thigh_contact"].data.found.shape == (2, 4)
+
+
+def test_exclude_mixed_patterns(device):
+  cfg = ContactSensorCfg(name="mixed_exclude",
+                         primary=ContactMatch(mode="geom", pattern=r".*_collision\d*$", entity="robot",
+                                              exclude=("trunk_collision", r".*foot_collision")),
+                         secondary=None, fields=("found",))
+  scene, sim = create_scene_with_sensor(SIMPLE_ROBOT_XML, "robot", cfg, device)
+  assert scene["mixed_exclude"].data.found.shape == (2, 5)
+  step_and_settle(sim, num_steps=20)
+  _matches_oracle(sim)
+
+
+def test_body_mode_contacts(device):
+  cfg = ContactSensorCfg(name="body_contact",
+                         primary=ContactMatch(mode="body", pattern="base", entity="biped"),
+                         secondary=None, fields=("found",))
+  scene, _ = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  assert scene["body_contact"].data.found.shape[1] == 1
+
+
+def test_subtree_mode_contacts(device):
+  cfg = ContactSensorCfg(name="subtree_contact",
+                         primary=ContactMatch(mode="subtree", pattern="base", entity="biped"),
+                         secondary=None, fields=("found",))
+  scene, sim = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  _place(scene["biped"], sim, 0.2)
+  step_and_settle(sim, num_steps=30)
+  assert torch.any(scene["subtree_contact"].data.found > 0)
+  _matches_oracle(sim)
+
+
+def test_air_time_tracking(device):
+  cfg = ContactSensorCfg(name="feet_contact",
+                         primary=ContactMatch(mode="geom", pattern=("left_foot_geom", "right_foot_geom"),
+                                              entity="biped"),
+                         secondary=None, fields=("found",), track_air_time=True)
+  scene, sim = create_scene_with_sensor(BIPED_XML, "biped", cfg, device)
+  sensor, biped = scene["feet_contact"], scene["biped"]
+  root_state = _place(biped, sim, 0.24)
+
+  def steps(n):
+    # the reference's `sim.step()` loop; its contact sensor's air time advances with
+    # `scene.update(dt)` (the env calls it after every physics step)
+    for _ in range(n):
+      sim.step()
+      scene.update(sim.mj_model.timestep)
+
+  steps(30)
+  data1 = sensor.data
+  assert torch.any(data1.found > 0)
+  on = data1.found > 0
+  assert torch.all(data1.current_air_time[on] == 0) and torch.all(data1.current_contact_time[on] > 0)
+  root_state[:, 2] = 1.0
+  biped.write_root_state_to_sim(root_state)
+  steps(20)
+  data2 = sensor.data
+  assert torch.all(data2.found == 0)
+  assert hasattr(data2, "current_air_time") and hasattr(data2, "last_air_time")
+  # in the air for at least the 20 steps since the jump; the feet that touched before it
+  # had their contact phase recorded
+  h = sim.mj_model.timestep
+  assert torch.all(data2.current_air_time >= 20 * h - 1e-5)
+  assert torch.all(data2.current_contact_time == 0) and torch.all(data2.last_contact_time[on] > 0)
+  root_state[:, 2] = 0.24
+  biped.write_root_state_to_sim(root_state)
+  steps(30)
+  data3 = sensor.data
+  assert torch.any(data3.found > 0)
+  # the landing recorded the air phase
+  assert torch.all(data3.last_air_time[data3.found > 0] >= 20 * h - 1e-5)
+  _matches_oracle(sim)
+
+
+def test_multiple_sensors(device):
+  left = ContactSensorCfg(name="left_foot_contact",
+                          primary=ContactMatch(mode="geom", pattern="left_foot_geom", entity="biped"),
+                          secondary=None, fields=("found", "force"))
+  right = ContactSensorCfg(name="right_foot_contact",
+                           primary=ContactMatch(mode="geom", pattern="right_foot_geom", entity="biped"),
+                           secondary=None, fields=("found", "force"))
+  scene = Scene(SceneCfg(num_envs=2, env_spacing=3.0,
+                         entities={"biped": EntityCfg(spec_fn=lambda: Spec.from_string(BIPED_XML))},
+                         sensors=(left, right)), device)
+  model = scene.compile()
+  sim = Simulation(num_envs=2, cfg=SimulationCfg(njmax=40), model=model, device=device)
+  scene.initialize(sim.mj_model, sim.model, sim.data)
+  assert scene["left_foot_contact"].data.found.shape == (2, 1)
+  assert scene["right_foot_contact"].data.found.shape == (2, 1)
+
+
+def test_no_contacts(device):
+  cfg = ContactSensorCfg(name="box_contact",
+                         primary=ContactMatch(mode="geom", pattern="box_geom", entity="box"),
+                         secondary=None, fields=("found", "force"))
+  scene, sim = create_scene_with_sensor(FALLING_BOX_XML, "box", cfg, device)
+  _place(scene["box"], sim, 5.0)
+  sim.step()
+  data = scene["box_contact"].data
+  assert torch.all(data.found == 0)
+  assert torch.all(data.force == 0)
+
+
+def test_num_slots_greater_than_one(device):
+  pat = ContactMatch(mode="geom", pattern=("left_foot_geom", "right_foot_geom"), entity="biped")
+  s1 = ContactSensorCfg(name="feet_contact_single", primary=pat, secondary=None,
+                        fields=("found", "force", "normal"), num_slots=1)
+  s3 = ContactSensorCfg(name="feet_contact_triple", primary=pat, secondary=None,
+                        fields=("found", "force", "normal"), num_slots=3)
+  scene = Scene(SceneCfg(num_envs=2, env_spacing=3.0,
+                         entities={"biped": EntityCfg(spec_fn=lambda: Spec.from_string(BIPED_XML))},
+                         sensors=(s1, s3)), device)
+  model = scene.compile()
+  sim = Simulation(num_envs=2, cfg=SimulationCfg(njmax=40), model=model, device=device)
+  scene.initialize(sim.mj_model, sim.model, sim.data)
+  _place(scene["biped"], sim, 0.25)
+  step_and_settle(sim, num_steps=20)
+  d1, d3 = scene["feet_contact_single"].data, scene["feet_contact_triple"].data
+  assert d1.found.shape == (2, 2) and d1.force.shape == (2, 2, 3) and d1.normal.shape == (2, 2, 3)
+  assert d3.found.shape == (2, 6) and d3.force.shape == (2, 6, 3) and d3.normal.shape == (2, 6, 3)
+  _matches_oracle(sim)
+
+
+# ============================================================================ builtin sensors
+ARTICULATED_ROBOT_XML = """
+    <mujoco>
+      <worldbody>
+        <geom name="floor" type="plane" size="5 5 0.1" pos="0 0 0"/>
+        <body name="base" pos="0 0 1">
+          <freejoint name="free_joint"/>
+          <geom name="base_geom" type="box" size="0.2 0.2 0.1" mass="5.0"/>
+          <site name="base_site" pos="0 0 0"/>
+          <body name="link1" pos="0.3 0 0">
+            <joint name="joint1" type="hinge" axis="0 0 1" range="-1.57 1.57"/>
+            <geom name="link1_geom" type="box" size="0.1 0.1 0.1" mass="1.0"/>
+            <site name="link1_site" pos="0 0 0"/>
+          </body>
+        </body>
+      </worldbody>
+    </mujoco>
+"""
+
+ROBOT_WITH_XML_SENSORS = """
+    <mujoco>
+      <worldbody>
+        <body name="base" pos="0 0 1">
+          <freejoint name="free_joint"/>
+          <geom name="base_geom" type="box" size="0.2 0.2 0.1" mass="5.0"/>
+          <site name="base_site" pos="0 0 0"/>
+          <body name="link1" pos="0.3 0 0">
+            <joint name="joint1" type="hinge" axis="0 0 1" range="-1.57 1.57"/>
+            <geom name="link1_geom" type="box" size="0.1 0.1 0.1" mass="1.0"/>
+            <site name="link1_site" pos="0 0 0"/>
+          </body>
+        </body>
+      </worldbody>
+      <sensor>
+        <jointpos name="xml_joint_sensor" joint="joint1"/>
+        <accelerometer name="xml_accel_sensor" site="base_site"/>
+        <gyro name="xml_gyro_sensor" site="link1_site"/>
+      </sensor>
+    </mujoco>
+"""
+
+
+def _builtin_scene(xml, sensors, num_envs, device):
+  scene = Scene(SceneCfg(num_envs=num_envs, env_spacing=3.0,
+                         entities={"robot": EntityCfg(spec_fn=lambda: Spec.from_string(xml))},
+                         sensors=sensors), device)
+  model = scene.compile()
+  sim = Simulation(num_envs=num_envs, cfg=SimulationCfg(njmax=20), model=model, device=device)
+  scene.initialize(sim.mj_model, sim.model, sim.data)
+  return scene, sim
+
+
+def test_jointpos_sensor(device):
+  cfg = BuiltinSensorCfg(name="joint1_pos", sensor_type="jointpos",
+                         obj=ObjRef(type="joint", name="joint1", entity="robot"))
+  scene, sim = _builtin_scene(ARTICULATED_ROBOT_XML, (cfg,), 2, device)
+  sensor = scene["robot/joint1_pos"]
+  sim.step()
+  assert isinstance(sensor.data, torch.Tensor) and sensor.data.shape == (2, 1)
+  _matches_oracle(sim)
+
+
+def test_accelerometer_sensor(device):
+  """tests/test_builtin_sensor.py:103-138: non-zero acceleration once the robot has fallen
+  onto the floor."""
+  cfg = BuiltinSensorCfg(name="base_accel", sensor_type="accelerometer",
+                         obj=ObjRef(type="site", name="base_site", entity="robot"))
+  scene, sim = _builtin_scene(ARTICULATED_ROBOT_XML, (cfg,), 2, device)
+  sensor = scene["robot/base_accel"]
+  for _ in range(100):
+    sim.step()
+  data = sensor.data
+  assert isinstance(data, torch.Tensor) and data.shape == (2, 3)
+  # 100 steps of 2 ms is still mid-fall from 1 m (about 0 m/s^2 of specific force); once the
+  # robot rests on the floor the accelerometer reads the support, +g along the site's z
+  for _ in range(500):
+    sim.step()
+  data = sensor.data
+  assert torch.any(torch.abs(data) > 0)
+  torch.testing.assert_close(data[:, 2], torch.full_like(data[:, 2], 9.81), rtol=0, atol=0.05)
+  _matches_oracle(sim)
+
+
+def test_multiple_builtin_sensors(device):
+  cfgs = (BuiltinSensorCfg(name="joint1_pos", sensor_type="jointpos",
+                           obj=ObjRef(type="joint", name="joint1", entity="robot")),
+          BuiltinSensorCfg(name="joint1_vel", sensor_type="jointvel",
+                           obj=ObjRef(type="joint", name="joint1", entity="robot")),
+          BuiltinSensorCfg(name="base_gyro", sensor_type="gyro",
+                           obj=ObjRef(type="site", name="base_site", entity="robot")))
+  scene, sim = _builtin_scene(ARTICULATED_ROBOT_XML, cfgs, 1, device)
+  sim.step()
+  assert scene["robot/joint1_pos"].data.shape == (1, 1)
+  assert scene["robot/joint1_vel"].data.shape == (1, 1)
+  assert scene["robot/base_gyro"].data.shape == (1, 3)
+  _matches_oracle(sim)
+
+
+def test_xml_sensors_auto_discovered(device):
+  scene, sim = _builtin_scene(ROBOT_WITH_XML_SENSORS, (), 2, device)
+  sim.step()
+  assert scene["robot/xml_joint_sensor"].data.shape == (2, 1)
+  assert scene["robot/xml_accel_sensor"].data.shape == (2, 3)
+  assert scene["robot/xml_gyro_sensor"].data.shape == (2, 3)
+  _matches_oracle(sim)
+
+
+# ============================================================================ nan_detection
+NAN_XML = """
+  <mujoco>
+    <worldbody>
+      <body>
+        <freejoint/>
+        <geom type="box" size="0.1 0.1 0.1"/>
+      </body>
+    </worldbody>
+  </mujoco>
+"""
+
+
+@pytest.fixture
+def mock_env_with_sim(device):
+  from types import SimpleNamespace
+  env = SimpleNamespace(num_envs=4, device=device, max_episode_length=1000)
+  env.episode_length_buf = torch.zeros(4, dtype=torch.long, device=device)
+  env.sim = Simulation(num_envs=4, cfg=SimulationCfg(), model=Spec.from_string(NAN_XML).compile(),
+                       device=device)
+  return env
+
+
+def test_nan_detection_function(mock_env_with_sim):
+  from mjlab_amd.mdp import nan_detection
+  env = mock_env_with_sim
+  result = nan_detection(env)
+  assert result.shape == (4,)
+  assert not result.any()
+  env.sim.data.qpos[1, 0] = float("nan")
+  result = nan_detection(env)
+  assert result[1] and not result[0] and not result[2] and not result[3]
+  env.sim.data.qacc_warmstart[3, 0] = float("-inf")
+  result = nan_detection(env)
+  assert result[1] and result[3] and not result[0] and not result[2]
+
+
+def test_nan_detection_with_termination_manager(mock_env_with_sim):
+  from mjlab_amd.managers import TerminationManager, TerminationTermCfg
+  from mjlab_amd.mdp import nan_detection
+  env = mock_env_with_sim
+  manager = TerminationManager({"nan_term": TerminationTermCfg(func=nan_detection, params={},
+                                                                time_out=False)}, env)
+  result = manager.compute()
+  assert not result.any() and not manager.terminated.any() and not manager.time_outs.any()
+  env.sim.data.qpos[1, 0] = float("nan")
+  result = manager.compute()
+  assert result[1] and not result[0] and not result[2] and not result[3]
+  assert manager.terminated[1] and not manager.time_outs[1]
+  reset_info = manager.reset(torch.tensor([1], device=env.device))
+  assert "Episode_Termination/nan_term" in reset_info
+  assert reset_info["Episode_Termination/nan_term"] == 1
+  env.sim.data.qvel[0, 0] = float("inf")
+  env.sim.data.qacc[2, 0] = float("-inf")
+  result = manager.compute()
+  assert result[0] and result[2]
+  reset_info = manager.reset(torch.tensor([0, 2], device=env.device))
+  assert reset_info["Episode_Termination/nan_term"] == 2
+
+
+# ============================================================================ encoder bias
+SLIDING_MASS_XML = """
+<mujoco>
+  <option timestep="0.002"/>
+  <worldbody>
+    <body name="mass" pos="0 0 0">
+      <joint name="slide" type="slide" axis="1 0 0" range="-1 1" limited="true"/>
+      <geom name="mass_geom" type="sphere" size="0.1" mass="1.0"/>
+    </body>
+  </worldbody>
+  <sensor>
+    <jointpos name="slide_pos" joint="slide"/>
+  </sensor>
+</mujoco>
+"""
+
+
+def _make_robot_cfg():
+  return EntityCfg(spec_fn=lambda: Spec.from_string(SLIDING_MASS_XML),
+                   articulation=EntityArticulationInfoCfg(actuators=(
+                     BuiltinPositionActuatorCfg(joint_names_expr=(".*",), stiffness=1000.0,
+                                                damping=100.0),)))
+
+
+def _make_env_cfg(obs_func=None, num_envs=2, events=None):
+  from mjlab_amd import mdp
+  from mjlab_amd.envs import ManagerBasedRlEnvCfg
+  from mjlab_amd.managers import ObservationGroupCfg, ObservationTermCfg
+  from mjlab_amd.terrains import TerrainImporterCfg
+  if obs_func is None:
+    obs_func = partial(mdp.joint_pos_rel, biased=True)
+  return ManagerBasedRlEnvCfg(
+    scene=SceneCfg(terrain=TerrainImporterCfg(terrain_type="plane"), num_envs=num_envs, extent=1.0,
+                   entities={"robot": _make_robot_cfg()}),
+    observations={"policy": ObservationGroupCfg(terms={"obs": ObservationTermCfg(func=obs_func)})},
+    actions={"joint_pos": mdp.JointPositionActionCfg(asset_name="robot", actuator_names=(".*",),
+                                                     scale=1.0)},
+    events=events or {},
+    sim=SimulationCfg(mujoco=MujocoCfg(timestep=0.002, iterations=1)),
+    decimation=1, episode_length_s=10.0)
+
+
+def _env(cfg, device):
+  from mjlab_amd.envs import ManagerBasedRlEnv
+  env = ManagerBasedRlEnv(cfg=cfg, device=device)
+  env.reset()
+  return env
+
+
+def test_encoder_bias_initialized_to_zero(device):
+  env = _env(_make_env_cfg(num_envs=4), device)
+  robot = env.scene["robot"]
+  assert robot.data.encoder_bias.shape == (4, 1)
+  assert (robot.data.encoder_bias == 0).all()
+
+
+def test_encoder_bias_can_be_set_per_env(device):
+  robot = _env(_make_env_cfg(), device).scene["robot"]
+  robot.data.encoder_bias[0, 0] = 0.1
+  robot.data.encoder_bias[1, 0] = -0.2
+  assert robot.data.encoder_bias[0, 0].item() == pytest.approx(0.1)
+  assert robot.data.encoder_bias[1, 0].item() == pytest.approx(-0.2)
+
+
+def test_joint_pos_biased_equals_joint_pos_plus_bias(device):
+  robot = _env(_make_env_cfg(), device).scene["robot"]
+  robot.data.encoder_bias[:, 0] = 0.25
+  torch.testing.assert_close(robot.data.joint_pos_biased, robot.data.joint_pos + robot.data.encoder_bias)
+
+
+def test_joint_pos_rel_includes_encoder_bias(device):
+  env = _env(_make_env_cfg(), device)
+  robot = env.scene["robot"]
+  obs_before = env.observation_manager.compute()["policy"].clone()
+  robot.data.encoder_bias[:, 0] = 0.5
+  env.observation_manager._obs_buffer = None
+  obs_after = env.observation_manager.compute()["policy"]
+  torch.testing.assert_close(obs_after, obs_before + 0.5, atol=1e-5, rtol=0)
+
+
+def test_joint_vel_rel_ignores_encoder_bias(device):
+  from mjlab_amd import mdp
+  env = _env(_make_env_cfg(obs_func=mdp.joint_vel_rel), device)
+  robot = env.scene["robot"]
+  obs_before = env.observation_manager.compute()["policy"].clone()
+  robot.data.encoder_bias[:, 0] = 0.5
+  env.observation_manager._obs_buffer = None
+  obs_after = env.observation_manager.compute()["policy"]
+  torch.testing.assert_close(obs_before, obs_after, atol=1e-6, rtol=0)
+
+
+def test_position_action_subtracts_encoder_bias(device):
+  env = _env(_make_env_cfg(), device)
+  robot = env.scene["robot"]
+  robot.data.encoder_bias[0, 0] = 0.0
+  robot.data.encoder_bias[1, 0] = 0.3
+  env.step(torch.tensor([[0.5], [0.5]], device=device))
+  assert robot.data.joint_pos_target[0, 0].item() == pytest.approx(0.5, abs=1e-5)
+  assert robot.data.joint_pos_target[1, 0].item() == pytest.approx(0.2, abs=1e-5)
+
+
+def test_bias_compensation_produces_identical_physical_behavior(device):
+  """tests/test_encoder_bias.py:221-264: bias-compensated commands give identical physics;
+  the observations differ by the bias."""
+  env = _env(_make_env_cfg(), device)
+  robot = env.scene["robot"]
+  b0, b1 = 0.0, 0.3
+  robot.data.encoder_bias[0, 0] = b0
+  robot.data.encoder_bias[1, 0] = b1
+  target = 0.4
+  action = torch.tensor([[target + b0], [target + b1]], device=device)
+  for _ in range(100):
+    env.step(action)
+  p0, p1 = robot.data.joint_pos[0, 0].item(), robot.data.joint_pos[1, 0].item()
+  assert p0 == pytest.approx(p1, abs=1e-4)
+  env.observation_manager._obs_buffer = None
+  obs = env.observation_manager.compute()["policy"]
+  assert obs[1, 0].item() - obs[0, 0].item() == pytest.approx(b1 - b0, abs=1e-4)
+  # the two worlds' states are the same state, so the oracle agrees with both alike
+  _matches_oracle(env.sim)
+
+
+def test_randomize_encoder_bias_event(device):
+  from mjlab_amd import mdp
+  from mjlab_amd.envs import ManagerBasedRlEnvCfg
+  from mjlab_amd.managers import (EventTermCfg, ObservationGroupCfg, ObservationTermCfg,
+                                  SceneEntityCfg)
+  from mjlab_amd.terrains import TerrainImporterCfg
+  cfg = ManagerBasedRlEnvCfg(
+    scene=SceneCfg(terrain=TerrainImporterCfg(terrain_type="plane"), num_envs=100, extent=10.0,
+                   entities={"robot": _make_robot_cfg()}),
+    observations={"policy": ObservationGroupCfg(
+      terms={"obs": ObservationTermCfg(func=partial(mdp.joint_pos_rel, biased=True))})},
+    actions={"joint_pos": mdp.JointPositionActionCfg(asset_name="robot", actuator_names=(".*",),
+                                                     scale=1.0)},
+    events={"randomize_bias": EventTermCfg(func=mdp.randomize_encoder_bias, mode="startup",
+                                           params={"bias_range": (-0.1, 0.1),
+                                                   "asset_cfg": SceneEntityCfg("robot")})},
+    sim=SimulationCfg(mujoco=MujocoCfg(timestep=0.002, iterations=1)),
+    decimation=1, episode_length_s=10.0)
+  env = _env(cfg, device)
+  biases = env.scene["robot"].data.encoder_bias[:, 0]
+  assert (biases >= -0.1).all() and (biases <= 0.1).all()
+  assert biases.std() > 0.01
+
+
+# ============================================================================ sim data bridge
+def test_bridge_raises_on_setattr(device):
+  """tests/test_sim_data.py:67-75, on the engine's own device bridge."""
+  sim = Simulation(num_envs=2, cfg=SimulationCfg(), model=Spec.from_string(NAN_XML).compile(),
+                   device=device)
+  ptr = sim.data.qpos.data_ptr()
+  with pytest.raises(AttributeError, match="Cannot set attribute 'qpos' on WarpBridge"):
+    sim.data.qpos = torch.zeros((2, 7), device=device)
+  with pytest.raises(AttributeError, match="Use in-place operations instead"):
+    sim.data.val = 42.0
+  sim.data.qpos[:] = torch.zeros((2, 7), device=device)  # in place: same device memory
+  assert sim.data.qpos.data_ptr() == ptr and torch.all(sim.data.qpos == 0)
