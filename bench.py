@@ -22,7 +22,10 @@ separate rocprofv3 passes over bench.py itself, scripts/profile_round.sh) when o
 taken on this task / num_envs / nv, else null.  `bound` is the larger of the HBM and MFMA
 fractions.
 overflow: contact/row overflow events counted by the engine over the timed steps (dropped
-contact work); non-zero makes the run exit 3 after printing the line (--allow-overflow).
+contact work past the max capacity); non-zero makes the run exit 3 after printing the line
+(--allow-overflow).  resolved_events: world-substeps that overflowed the fast LDS carve and
+were re-solved at the max capacity inside the same step (nothing dropped; their cost is in
+the timing).
 cpu_baseline: the fp64 CPU oracle (oracle/liboracle.so, "port") on the allotted host cores
 over the bench's own worlds with random actions, plus config 1 (num_envs=1, zero action,
 one thread).
@@ -284,7 +287,7 @@ def main():
 
   for _ in range(args.warmup):
     one_step(draw())
-  ev_before = sim.overflow_events().clone()
+  ev_before = sim.event_counts().clone()
   sim.marker(1)  # kernel-trace bracket (outside the timing: it completes before t0)
   torch.cuda.synchronize()
   if dist is not None:
@@ -304,9 +307,10 @@ def main():
     dist.barrier()
   el = time.perf_counter() - t0
   sim.marker(2)
-  # contacts dropped in the timed steps (a world whose contacts or rows overflow its LDS
-  # capacity drops whole contacts; the engine counts the events every substep)
-  dropped = (sim.overflow_events() - ev_before).cpu().tolist()
+  # contacts dropped in the timed steps (a world whose contacts or rows overflow the max
+  # capacity drops whole contacts; the engine counts the events every substep) and the
+  # re-solves of worlds that overflowed the fast carve
+  events = (sim.event_counts() - ev_before).cpu().tolist()
   region_ms = r0.elapsed_time(r1) / args.steps
   # and, for reference, HIP events around each of `launch_reps` further single steps on the
   # stream they are launched on (torch's current stream; graph replays and the engine's
@@ -324,7 +328,8 @@ def main():
   launch_ms = float(region_ms)
   st = sim.stats()
   if dist is not None:
-    el, dropped, _ = reduce_over_ranks(el, dropped, env.packed_episode_stats(), device)
+    el, events, _ = reduce_over_ranks(el, events, env.packed_episode_stats(), device)
+  dropped, resolved = events[:3], int(events[3])
 
   total = args.steps * args.num_envs * world
   value = total / el
@@ -357,6 +362,9 @@ def main():
                               "asked": {"nconmax": env.cfg.sim.nconmax, "njmax": env.cfg.sim.njmax}}},
       "overflow": {"timed_steps": args.steps, "contact_overflow_events": int(dropped[0]),
                    "row_overflow_events": int(dropped[1]), "unsupported_pair_events": int(dropped[2]),
+                   "resolved_events": resolved,
+                   "fast_capacity": {"contacts_per_world": sim.fast_capacity[0],
+                                     "rows_per_world": sim.fast_capacity[1]},
                    "max_contacts_seen": st["max_ncon"], "max_rows_seen": st["max_nefc"]},
       "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -119,6 +119,15 @@ int mjx_model_destroy(mjxModel* model);
  * reference's per-world budget, sim/sim.py:82-92); njmax: constraint rows per world.
  * Data starts at qpos0 (mj_resetData semantics). */
 int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mjxSim** out);
+/* The same with a max capacity (nconmax <= nconmax_max <= 64, njmax <= njmax_max): the step
+ * runs at (nconmax, njmax) per world -- the fast LDS carve -- and a world whose contacts or
+ * rows overflow it in a substep is re-solved at (nconmax_max, njmax_max) instead of
+ * truncated (the reference's budget semantics: its nconmax is pooled, sim/sim.py:82-92; its
+ * njmax, 300 rows for the velocity tasks, bounds each world).  Only what overflows the max
+ * capacity is dropped (counted by mjx_sim_stats).  The contact output arrays hold
+ * nconmax_max slots per world; a masked forward runs at the max capacity throughout. */
+int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax, int nconmax_max,
+                      int njmax_max, mjxSim** out);
 int mjx_sim_destroy(mjxSim* sim);
 
 /* One mj_step (forward + implicitfast/Euler integration) for every world, repeated
@@ -154,9 +163,16 @@ int mjx_sim_track_air_time(mjxSim* sim, int n, const int32_t* found_adr, float* 
                            float* last_air, float* cur_contact, float* last_contact,
                            float* last_time, void* stream);
 
-/* Diagnostics: per-sim counters (max contacts/rows seen, overflow events) as
- * int32[8] written to host `out`; synchronises the stream. */
+/* Diagnostics: per-sim counters as int32[8] written to host `out` ([0] max contacts, [1] max
+ * rows seen, [2] contact-overflow, [3] row-overflow, [4] unsupported-pair events -- dropped
+ * work --, [5] max Newton iterations, [6] worlds re-solved at the max capacity); synchronises
+ * the stream. */
 int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);
+/* The sim's capacities and kernels as int32[8]: [0] nconmax, [1] njmax (the fast carve),
+ * [2] nconmax_max, [3] njmax_max, [4] spec of the fast carve's kernels, [5] spec of the max
+ * capacity's kernels (csrc/specs.inc entry, 0 = generic), [6] re-solve list capacity per
+ * substep, [7] Newton row classes. */
+int mjx_sim_info(const mjxSim* sim, int32_t* out);
 /* Diagnostics: per-stage cycle sums uint64[48] (non-zero only in the -DMJX_STAMPS build). */
 int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
 /* Which step kernels the sim launches: k > 0 = kernels compiled for entry k of

@@ -102,12 +102,29 @@ struct mjxSim_ {
       if (side.split_join[p]) (void)hipEventDestroy(side.split_join[p]);
     }
     if (side.split_fork) (void)hipEventDestroy(side.split_fork);
+    for (int p = 0; p < mjx::kMaxSplit; p++) {
+      if (side.ovf[p]) (void)hipStreamDestroy(side.ovf[p]);
+      if (side.ovf_fork[p]) (void)hipEventDestroy(side.ovf_fork[p]);
+      if (side.ovf_join[p]) (void)hipEventDestroy(side.ovf_join[p]);
+    }
   }
   int gC = 0, gF = 0, gstride = 0;
   float* gscr = nullptr;
   int* wl = nullptr;  // Newton work lists: [nworld] world ids + [kMaxSplit][2 * (kRowClasses + 1)] segments
   void* arena = nullptr;
   mjx::Params* dparams = nullptr;  // device copy of the launch parameters
+  // overflow re-solve (mjx_sim_create_ex with a max capacity above the fast carve): the
+  // max-capacity dims / carves / kernels / scratch, and the lists phase A fills
+  bool big = false;
+  mjx::Dims dbig{};
+  mjx::Lds lds_big[3]{};
+  int spec_big = 0;
+  int gC_big = 0, gF_big = 0, gstride_big = 0;
+  float* gscr_big = nullptr;
+  int* ovf = nullptr;  // [kMaxSplit][2][ovf_cap] lists, [kMaxSplit][2] counts, [nworld] flags
+  int ovf_cap = 0;
+  int con_stride = 0;  // contact slots per world in the contact output arrays
+  mjx::Params* dparams_big = nullptr;
   std::vector<void*> expanded_allocs;
   std::map<std::string, FieldInfo> fields;
   std::vector<std::string> names;
@@ -139,15 +156,44 @@ static mjx::Params host_params(const mjxSim_* s) {
     return e ? atoi(e) : 0;
   }();
   p.stamp_minrows = minrows;
+  p.ovf_resolve = s->big ? 1 : 0;
+  p.ovf_cap = s->ovf_cap;
+  p.ovf_list = s->ovf;
+  p.ovf_n = s->ovf ? s->ovf + (size_t)mjx::kMaxSplit * 2 * s->ovf_cap : nullptr;
+  p.ovf_flag = s->ovf ? p.ovf_n + mjx::kMaxSplit * 2 : nullptr;
+  p.con_stride = s->con_stride;
+  return p;
+}
+
+// The max-capacity launch parameters of the overflow re-solve: same model, data, lists and
+// air-time buffers; the max dims, carves, kernels and scratch; no row classes (its worlds run
+// the latency Newton kernel); overflow past it drops contacts.
+static mjx::Params host_params_big(const mjxSim_* s) {
+  mjx::Params p = host_params(s);
+  p.d = s->dbig;
+  for (int i = 0; i < 3; i++) p.LP[i] = s->lds_big[i];
+  for (int k = 0; k < mjx::kRowClasses; k++) p.LP[3 + k] = s->lds_big[1];
+  p.nrowclass = 0;
+  p.gscr = s->gscr_big;
+  p.gC = s->gC_big;
+  p.gF = s->gF_big;
+  p.gstride = s->gstride_big;
+  p.spec = s->spec_big;
+  p.ovf_resolve = 0;
   return p;
 }
 
 // Upload the launch parameters (stream-ordered, so later launches see the new copy).
 static int sync_params(mjxSim_* s, void* stream) {
-  static thread_local mjx::Params staging;
+  static thread_local mjx::Params staging, staging_big;
   staging = host_params(s);
   HIPCHK(hipMemcpyAsync(s->dparams, &staging, sizeof(mjx::Params), hipMemcpyHostToDevice,
                         (hipStream_t)stream));
+  if (s->big) {
+    staging_big = host_params_big(s);
+    HIPCHK(hipMemcpyAsync(s->dparams_big, &staging_big, sizeof(mjx::Params), hipMemcpyHostToDevice,
+                          (hipStream_t)stream));
+  }
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }
@@ -454,11 +500,18 @@ int mjx_model_destroy(mjxModel* m) {
 }
 
 int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mjxSim** out) {
+  return mjx_sim_create_ex(model, nworld, nconmax, njmax, nconmax, njmax, out);
+}
+
+int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
+                      int nconmax_max, int njmax_max, mjxSim** out) {
   if (!model || !out) return fail("null argument");
   if (nworld <= 0) return fail("nworld must be positive");
   if (nconmax <= 0 || nconmax > mjx::kWave)
     return fail("nconmax (contacts held per world) must be in [1, 64]");
   if (njmax <= 0) return fail("njmax must be positive");
+  if (nconmax_max < nconmax || nconmax_max > mjx::kWave || njmax_max < njmax)
+    return fail("max capacity: nconmax <= nconmax_max <= 64 and njmax <= njmax_max");
   HIPCHK(hipSetDevice(model->device));
   auto* s = new mjxSim_();
   s->model = model;
@@ -473,6 +526,26 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
       delete s;
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
+  }
+  s->big = nconmax_max > nconmax || njmax_max > njmax;
+  s->con_stride = s->big ? nconmax_max : nconmax;
+  if (s->big) {
+    s->dbig = s->d;
+    s->dbig.nconmax = nconmax_max;
+    s->dbig.njmax = njmax_max;
+    for (int i = 0; i < 3; i++) {
+      s->lds_big[i] = mjx::make_lds(s->dbig, i);
+      if ((size_t)s->lds_big[i].total * 4 > 160 * 1024) {
+        delete s;
+        return fail("max-capacity LDS footprint exceeds 160 KiB; lower njmax_max/nconmax_max");
+      }
+    }
+    s->spec_big = mjx::find_spec(s->dbig, model->dof_parentid.data());
+    s->gC_big = (s->lds_big[1].pack_len + 63) & ~63;
+    s->gF_big = s->gC_big + ((s->lds_big[2].pack_len + 63) & ~63);
+    s->gstride_big = s->gF_big + ((mjx::ltr_size((s->d.nv + 3) & ~3) + 63) & ~63);
+    // re-solve list capacity per split and substep parity: every world may be listed
+    s->ovf_cap = nworld;
   }
   s->spec = mjx::find_spec(s->d, model->dof_parentid.data());
   s->nrowclass = mjx::choose_row_classes(s->d, s->spec, s->row_cap);
@@ -504,6 +577,11 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
         if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.join[p][k], hipEventDisableTiming);
       }
     }
+    for (int p = 0; p < s->side.nsplit && s->big && e == hipSuccess; p++) {
+      e = hipStreamCreateWithFlags(&s->side.ovf[p], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.ovf_fork[p], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&s->side.ovf_join[p], hipEventDisableTiming);
+    }
     if (e != hipSuccess) { delete s; return fail(std::string("side streams: ") + hipGetErrorString(e)); }
   }
   s->gC = (s->lds_ph[1].pack_len + 63) & ~63;
@@ -512,7 +590,10 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
     const int nvp = (s->d.nv + 3) & ~3;
     s->gstride = s->gF + ((mjx::ltr_size(nvp) + 63) & ~63);  // implicit factor, LTR form
   }
-  const mjx::Dims& d = s->d;
+  // the contact output arrays hold the max capacity's contacts
+  mjx::Dims dout = s->d;
+  dout.nconmax = s->con_stride;
+  const mjx::Dims& d = dout;
   // data arena: one allocation, 256-B aligned sub-buffers
   size_t off = 0;
   std::vector<std::pair<std::string, size_t>> offs;
@@ -539,6 +620,16 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc work lists: ") + hipGetErrorString(e)); }
   e = hipMemset(s->wl, 0, sizeof(int) * ((size_t)nworld + 2 * (mjx::kRowClasses + 1) * mjx::kMaxSplit));
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
+  if (s->big) {
+    const size_t gb = sizeof(float) * (size_t)nworld * s->gstride_big;
+    e = hipMalloc((void**)&s->gscr_big, gb);
+    if (e == hipSuccess) e = hipMemset(s->gscr_big, 0, gb);
+    const size_t ob = sizeof(int) * ((size_t)mjx::kMaxSplit * 2 * (s->ovf_cap + 1) + nworld);
+    if (e == hipSuccess) e = hipMalloc((void**)&s->ovf, ob);
+    if (e == hipSuccess) e = hipMemset(s->ovf, 0, ob);
+    if (e == hipSuccess) e = hipMalloc((void**)&s->dparams_big, sizeof(mjx::Params));
+    if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc re-solve buffers: ") + hipGetErrorString(e)); }
+  }
   e = hipMalloc(&s->arena, off);
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc data: ") + hipGetErrorString(e)); }
   e = hipMemset(s->arena, 0, off);
@@ -590,6 +681,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
   if (e != hipSuccess) { delete s; return fail(std::string("hipMalloc params: ") + hipGetErrorString(e)); }
   if (sync_params(s, nullptr)) { delete s; return -1; }
   e = mjx::prepare_step(host_params(s));
+  if (e == hipSuccess && s->big) e = mjx::prepare_step(host_params_big(s));
   if (e != hipSuccess) { delete s; return fail(std::string("prepare: ") + hipGetErrorString(e)); }
   // heightfield geom frames are static: write them once for every world
   for (size_t k = 0; k < model->static_geoms.size(); k++) {
@@ -623,6 +715,9 @@ int mjx_sim_destroy(mjxSim* s) {
   if (s->gscr) (void)hipFree(s->gscr);
   if (s->wl) (void)hipFree(s->wl);
   if (s->dparams) (void)hipFree(s->dparams);
+  if (s->gscr_big) (void)hipFree(s->gscr_big);
+  if (s->ovf) (void)hipFree(s->ovf);
+  if (s->dparams_big) (void)hipFree(s->dparams_big);
   for (void* p : s->expanded_allocs) (void)hipFree(p);
   delete s;
   return 0;
@@ -631,8 +726,10 @@ int mjx_sim_destroy(mjxSim* s) {
 int mjx_step(mjxSim* s, int nsubstep, void* stream) {
   if (!s) return fail("null sim");
   if (nsubstep < 1) return fail("nsubstep must be >= 1");
+  const mjx::Params hb = s->big ? host_params_big(s) : mjx::Params{};
   hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, nsubstep, 1, nullptr,
-                                  (hipStream_t)stream, &s->side);
+                                  (hipStream_t)stream, &s->side, s->big ? &hb : nullptr,
+                                  s->dparams_big);
   if (e != hipSuccess) return fail(std::string("step launch: ") + hipGetErrorString(e));
   return 0;
 }
@@ -641,8 +738,10 @@ int mjx_forward(mjxSim* s, void* stream) { return mjx_forward_masked(s, nullptr,
 
 int mjx_forward_masked(mjxSim* s, const uint8_t* mask, void* stream) {
   if (!s) return fail("null sim");
+  const mjx::Params hb = s->big ? host_params_big(s) : mjx::Params{};
   hipError_t e = mjx::launch_step(host_params(s), s->dparams, s->nworld, 1, 0, mask,
-                                  (hipStream_t)stream, &s->side);
+                                  (hipStream_t)stream, &s->side, s->big ? &hb : nullptr,
+                                  s->dparams_big);
   if (e != hipSuccess) return fail(std::string("forward launch: ") + hipGetErrorString(e));
   return 0;
 }
@@ -774,6 +873,15 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
 
 int mjx_sim_spec(const mjxSim* s) { return s ? s->spec : -1; }
 
+int mjx_sim_info(const mjxSim* s, int32_t* out) {
+  if (!s || !out) return fail("null argument");
+  const int32_t v[8] = {s->d.nconmax, s->d.njmax, s->big ? s->dbig.nconmax : s->d.nconmax,
+                        s->big ? s->dbig.njmax : s->d.njmax, s->spec, s->spec_big, s->ovf_cap,
+                        s->nrowclass};
+  for (int i = 0; i < 8; i++) out[i] = v[i];
+  return 0;
+}
+
 int mjx_marker(int tag, void* stream) {
   hipError_t e = mjx::launch_marker(tag, (hipStream_t)stream);
   if (e != hipSuccess) return fail(std::string("marker launch: ") + hipGetErrorString(e));
@@ -794,6 +902,10 @@ int mjx_sim_stats(mjxSim* s, int32_t* out, void* stream) {
     r[0] = std::max(r[0], x[0]); r[1] = std::max(r[1], x[1]); r[5] = std::max(r[5], x[5]);
     r[2] += x[2]; r[3] += x[3]; r[4] += x[4];
   }
+  // [6] overflow re-solves (worlds re-solved at the max capacity) over all worlds
+  HIPCHK(hipMemcpyAsync(&r[6], s->dd.evtotal + 3, sizeof(int32_t), hipMemcpyDeviceToHost,
+                        (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   for (int i = 0; i < 8; i++) out[i] = r[i];
   return 0;
 }

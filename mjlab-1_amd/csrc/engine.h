@@ -167,7 +167,29 @@ struct Params {
   int air_found[kMaxAirSlots];
   float *air_cur, *air_last, *air_cc, *air_lc, *air_time;
   int stamp_minrows;  // diagnostic stamps build: count worlds with at least this many rows
+  // Overflow re-solve ("Contact budget"): with ovf_resolve set, a world
+  // whose contacts or constraint rows overflow this carve is not truncated -- phase A lists
+  // it (ovf_list / ovf_n, one list per batch split and substep parity, ovf_cap entries each)
+  // and flags it (ovf_flag[w], rewritten by the world's every phase A), skips the rest of
+  // its substep in this carve, and the "max" launch set (a second Params at the sim's full
+  // capacity) re-solves its substep from its state.  The max Params have ovf_resolve = 0:
+  // what overflows them is dropped and counted.
+  int ovf_resolve;
+  int ovf_cap;
+  int* ovf_list;   // [kMaxSplit][2][ovf_cap]
+  int* ovf_n;      // [kMaxSplit][2]
+  int* ovf_flag;   // [nworld]
+  int con_stride;  // contact slots per world of the contact output arrays (the max capacity)
 };
+
+// `sel` launch argument of the step kernels: bits 0-7 batch split, 8-15 row class + 1 (the
+// piped C / next-A launches of a class), kSelOvf: the world is the blockIdx-th entry of the
+// overflow list of parity kSelRPar, kSelAPar: the parity of the substep phase A computes
+// (the list it appends overflowing worlds to).
+constexpr int kOvfGrid = 256;  // workgroups of a re-solve launch (each loops over listed worlds)
+constexpr int kSelOvf = 1 << 16;
+constexpr int kSelAPar = 1 << 17;
+constexpr int kSelRPar = 1 << 18;
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.
@@ -185,10 +207,17 @@ struct SideStream {
   int nsplit;                        // batch splits in use (1 = one launch set per phase)
   hipStream_t split[kMaxSplit];      // [0] unused: split 0 runs on the launch stream
   hipEvent_t split_fork, split_join[kMaxSplit];
+  // overflow re-solve chain of each split (forked after phase A / classify, joined before the
+  // next substep's classify)
+  hipStream_t ovf[kMaxSplit];
+  hipEvent_t ovf_fork[kMaxSplit], ovf_join[kMaxSplit];
 };
+// `hbig` / `dbig`: the max-capacity Params (host copy for the launch geometry, device copy
+// for the kernels) of the overflow re-solve, or null (overflow drops contacts).
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,
-                       const SideStream* side);
+                       const SideStream* side, const Params* hbig = nullptr,
+                       const Params* dbig = nullptr);
 // Newton row classes (capacities ascending into caps[]); returns how many are used.
 int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,

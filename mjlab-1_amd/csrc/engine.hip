@@ -53,8 +53,11 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
   for (int i = t; i < nb; i += kClassifyThreads) bin[i] = 0;
   __syncthreads();
   const int* nefc = P->D.nefc;
+  // worlds listed for the overflow re-solve this substep are not classed (the max launch set
+  // solves them)
+  const int* oflag = P->ovf_resolve ? P->ovf_flag : nullptr;
   for (int w = w0 + t; w < w1; w += kClassifyThreads)
-    if (!mask || mask[w]) atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1);
+    if ((!mask || mask[w]) && !(oflag && oflag[w])) atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1);
   __syncthreads();
   // exclusive scan of the bins in descending row count: bin[r] <- #listed worlds with more
   // than r rows.  Thread t owns a contiguous chunk of the reversed bin order.
@@ -103,8 +106,14 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
   }
   __syncthreads();  // the segments read the bins before the scatter advances them
   for (int w = w0 + t; w < w1; w += kClassifyThreads)
-    if (!mask || mask[w]) P->wl_list[w0 + atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1)] = w;
+    if ((!mask || mask[w]) && !(oflag && oflag[w]))
+      P->wl_list[w0 + atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1)] = w;
 }
+
+// The overflow list of one split and substep parity is emptied by the last launch of the
+// re-solve chain that consumed it (before the substep two ahead, or the next step call,
+// appends to it again).
+__global__ void ovf_clear_kernel(int* n) { *n = 0; }
 
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
 template <int NR>
@@ -292,14 +301,51 @@ static hipError_t launch_split_classes(const Params& host, const Params* dev, in
   return hipGetLastError();
 }
 
+// Overflow re-solve chain of split k at substep `sub` (parity sub & 1), on the split's
+// re-solve stream: the listed worlds' substep at full capacity (max A, latency Newton, C),
+// then -- when the class pipelines carry the next substep's phase A -- that phase A in the
+// normal carve, and the list is emptied.  The grid is fixed (kOvfGrid workgroups, each
+// looping over listed worlds); workgroups past the listed count exit at once.
+static void ovf_chain(const Params& host, const Params* dev, const Params& hbig, const Params* dbig,
+                      hipStream_t cs, int k, int w0, int w1, int sub, int nsubstep, int integrate,
+                      bool next_a) {
+  const int last = sub == nsubstep - 1;
+  const int par = sub & 1;
+  const int g = std::min(hbig.ovf_cap, kOvfGrid);
+  const int sel = k | kSelOvf | (par ? kSelRPar : 0);
+  hipLaunchKernelGGL(step_fn(hbig, 0), dim3(g), dim3(kWave), lds_bytes(hbig, 0), cs, dbig, w0, w1,
+                     sel, last, integrate, nullptr);
+  hipLaunchKernelGGL(step_fn(hbig, 3), dim3(g), dim3(kWave), lds_bytes(hbig, 1), cs, dbig, w0, w1,
+                     sel, last, -1, nullptr);
+  hipLaunchKernelGGL(step_fn(hbig, 2), dim3(g), dim3(kWave), lds_bytes(hbig, 2), cs, dbig, w0, w1,
+                     sel, last, integrate, nullptr);
+  if (next_a && !last)
+    hipLaunchKernelGGL(step_fn(host, 0), dim3(g), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
+                       sel | ((sub + 1) & 1 ? kSelAPar : 0), sub + 1 == nsubstep - 1, integrate,
+                       nullptr);
+  hipLaunchKernelGGL(ovf_clear_kernel, dim3(1), dim3(1), 0, cs, host.ovf_n + 2 * k + par);
+}
+
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,
-                       const SideStream* side) {
+                       const SideStream* side, const Params* hbig, const Params* dbig) {
   if (nworld <= 0) return hipSuccess;
+  if (mask && hbig) {
+    // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve
+    const StepFn fA = step_fn(*hbig, 0), fBL = step_fn(*hbig, 3), fC = step_fn(*hbig, 2);
+    hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(*hbig, 0), stream, dbig, 0, nworld, 0,
+                       1, integrate, mask);
+    hipLaunchKernelGGL(fBL, dim3(nworld), dim3(kWave), lds_bytes(*hbig, 1), stream, dbig, 0, nworld, 0,
+                       1, -1, mask);
+    hipLaunchKernelGGL(fC, dim3(nworld), dim3(kWave), lds_bytes(*hbig, 2), stream, dbig, 0, nworld, 0,
+                       1, integrate, mask);
+    return hipGetLastError();
+  }
   const StepFn fA = step_fn(host, 0), fB = step_fn(host, 1), fC = step_fn(host, 2);
   const StepFn fBL = newton_lat() ? step_fn(host, 3) : fB;
   const int nc = host.nrowclass;
   if (nc > 0 && !side) return hipErrorInvalidValue;
+  const bool ovf = hbig && side && host.ovf_resolve;
   // Batch split: the worlds in nsplit contiguous ranges, each range's A -> B -> C chain on
   // its own stream.  The ranges are independent, so one range's launches fill the tail of
   // the other's (the last, partly filled round of workgroups per CU) and the launch gaps.
@@ -311,8 +357,11 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     const char* e = getenv("MJX355_CLASS_PIPE");
     return !e || atoi(e) != 0;
   }();
-  if (nsplit > 1 && nc > 0)
+  if (nsplit > 1 && nc > 0) {
+    // (diagnostic topology; the overflow re-solve is not wired into it)
+    if (ovf) return hipErrorNotSupported;
     return launch_split_classes(host, dev, nworld, nsubstep, integrate, stream, side, nsplit, pipe);
+  }
   hipStream_t sst[kMaxSplit];
   int wb[kMaxSplit + 1];
   for (int k = 0; k <= nsplit; k++) wb[k] = (int)(((long long)nworld * k) / nsplit);
@@ -333,14 +382,32 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   // after the join (diagnostic).
   for (int sub = 0; sub < nsubstep; sub++) {
     const int last = sub == nsubstep - 1;
+    const int apar = (sub & 1) ? kSelAPar : 0;  // phase A of this substep lists into parity sub & 1
     for (int k = 0; k < nsplit; k++) {
       const int w0 = wb[k], w1 = wb[k + 1], n = w1 - w0;
       if (n <= 0) continue;
       hipStream_t st = sst[k];
       const bool piped = nc > 0 && !mask && pipe;
       if (!piped || sub == 0)
-        hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), st, dev, w0, w1, k,
+        hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), st, dev, w0, w1, k | apar,
                            last, integrate, mask);
+      // the re-solve chain: forked after this substep's phase A (and classify), joined at the
+      // end of the substep -- the empty chain overlaps the class launches
+      auto fork_ovf = [&]() {
+        if (!ovf) return hipSuccess;
+        hipError_t e2 = hipEventRecord(side->ovf_fork[k], st);
+        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(side->ovf[k], side->ovf_fork[k], 0);
+        if (e2 == hipSuccess)
+          ovf_chain(host, dev, *hbig, dbig, side->ovf[k], k, w0, w1, sub, nsubstep, integrate,
+                    piped);
+        return e2;
+      };
+      auto join_ovf = [&]() {
+        if (!ovf) return hipSuccess;
+        hipError_t e2 = hipEventRecord(side->ovf_join[k], side->ovf[k]);
+        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(st, side->ovf_join[k], 0);
+        return e2;
+      };
       if (nc > 0 && mask) {
         // masked forward (a few reset worlds): one Newton launch at full capacity over the
         // masked worlds -- no classify launch, no fork/join latency on this short critical path
@@ -349,6 +416,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       } else if (nc > 0) {
         hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, st, dev, w0, w1,
                            k, mask);
+        if ((e = fork_ovf()) != hipSuccess) return e;
         // Newton by row class, concurrently: the full-capacity class (few worlds, long
         // per-world latency) first on a side stream so its blocks dispatch first, the middle
         // classes on further side streams, the smallest (most worlds) on the launch stream.
@@ -365,7 +433,8 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                              k | (cls + 1) << 8, last, integrate, mask);
           if (!last)
             hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
-                               k | (cls + 1) << 8, sub + 1 == nsubstep - 1, integrate, mask);
+                               k | (cls + 1) << 8 | (((sub + 1) & 1) ? kSelAPar : 0),
+                               sub + 1 == nsubstep - 1, integrate, mask);
         };
         for (int c = 0; c < nc; c++) {
           const int cls = c == 0 ? 0 : nc + 1 - c;  // 0, then nc, nc-1, ..., 2
@@ -379,13 +448,18 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[k][c], 0);
           if (e != hipSuccess) return e;
         }
-        if (piped) continue;
+        if (piped) {
+          if ((e = join_ovf()) != hipSuccess) return e;
+          continue;
+        }
       } else {
+        if ((e = fork_ovf()) != hipSuccess) return e;
         hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
                            0, mask);
       }
       hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), st, dev, w0, w1, k, last,
                          integrate, mask);
+      if ((e = join_ovf()) != hipSuccess) return e;
     }
   }
   for (int k = 1; k < nsplit; k++) {

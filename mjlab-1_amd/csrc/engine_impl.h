@@ -1600,7 +1600,7 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 template <int NR, int PH, int SP, bool LAT>
 __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* __restrict__ P, int w0,
                                           int w1, int sel, int last, int integrate,
-                                          const uint8_t* __restrict__ mask) {
+                                          const uint8_t* __restrict__ mask, const int bid) {
   const auto& d = dims_of<SP>(P);
   const Opt& o = P->o;
   const DModel& m = P->m;
@@ -1609,28 +1609,41 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate] : lds_of<SP, PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
-  int w = w0 + (int)blockIdx.x;
+  int w = w0 + bid;
+  const int sel_arg = sel;  // (phase C's contact-sensor code has a local `sel`)
+  (void)sel_arg;
   const int split = sel & 0xff;
-  if constexpr (PH == 1) {
-    // Newton by row class: workgroup i takes the i-th world of its class's list
-    // (classify_kernel: rows descending, masked worlds only)
-    if (P->nrowclass > 0 && integrate >= 0) {  // integrate < 0: every world, full carve
-      const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + integrate);
-      if ((int)blockIdx.x >= seg[1]) return;
-      w = P->wl_list[seg[0] + blockIdx.x];
+  const int cls1 = (sel >> 8) & 0xff;
+  if (sel & kSelOvf) {
+    // overflow re-solve: workgroup i takes the i-th world phase A listed (parity kSelRPar)
+    const int li = 2 * split + ((sel & kSelRPar) ? 1 : 0);
+    if (bid >= min(P->ovf_n[li], P->ovf_cap)) return;
+    w = P->ovf_list[(size_t)li * P->ovf_cap + bid];
+  } else {
+    if constexpr (PH == 1) {
+      // Newton by row class: workgroup i takes the i-th world of its class's list
+      // (classify_kernel: rows descending, masked worlds only)
+      if (P->nrowclass > 0 && integrate >= 0) {  // integrate < 0: every world, full carve
+        const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + integrate);
+        if (bid >= seg[1]) return;
+        w = P->wl_list[seg[0] + bid];
+      }
     }
-  }
-  if constexpr (PH == 0 || PH == 2) {
-    // phase C of one row class right behind that class's Newton launch, and phase A of the
-    // next substep for the same worlds (the class lists stay valid until the next classify)
-    if (sel >> 8) {
-      const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + (sel >> 8) - 1);
-      if ((int)blockIdx.x >= seg[1]) return;
-      w = P->wl_list[seg[0] + blockIdx.x];
+    if constexpr (PH == 0 || PH == 2) {
+      // phase C of one row class right behind that class's Newton launch, and phase A of the
+      // next substep for the same worlds (the class lists stay valid until the next classify)
+      if (cls1) {
+        const int* seg = P->wl_seg + 2 * ((kRowClasses + 1) * split + cls1 - 1);
+        if (bid >= seg[1]) return;
+        w = P->wl_list[seg[0] + bid];
+      }
     }
   }
   if (w >= w1) return;
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
+  // a world listed for the overflow re-solve this substep skips this carve's B and C (the
+  // class lists already leave it out; the all-world launches check)
+  if (PH != 0 && P->ovf_resolve && !(sel & kSelOvf) && P->ovf_flag[w]) return;
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
   float* gc = gw + P->gC;
   float* gf = gw + P->gF;  // implicit-integration factor (phase A writes, phase C reads)
@@ -2536,6 +2549,25 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if (lane < ncon && cdim != 1 && cdim != 3) atomicOr(&ints[3], 4);
       int con_total, con_off = wave_excl_scan(crow, lane, &con_total);
       int nefc = lim_total + con_total;
+      if (P->ovf_resolve) {
+        // contacts or rows past this carve: list the world for the re-solve at full capacity
+        // (the max launch set) instead of dropping whole contacts; a full list falls back to
+        // dropping (counted below)
+        const bool over = ints[0] > d.nconmax || nefc > d.njmax;
+        int slot = -1;
+        if (over && lane == 0) {
+          const int li = 2 * split + ((sel_arg & kSelAPar) ? 1 : 0);
+          slot = atomicAdd(P->ovf_n + li, 1);
+          if (slot < P->ovf_cap) {
+            P->ovf_list[(size_t)li * P->ovf_cap + slot] = w;
+            atomicAdd(D.evtotal + 3, 1);
+          }
+        }
+        slot = __shfl(slot, 0);
+        const bool listed = over && slot < P->ovf_cap;
+        if (lane == 0) P->ovf_flag[w] = listed ? 1 : 0;
+        if (listed) return;
+      }
       if (nefc > d.njmax) {
         if (lane == 0) atomicOr(&ints[3], 2);
       }
@@ -2844,8 +2876,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
       }
       for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
-      size_t wc = (size_t)w * d.nconmax;
-      for (int c = lane; c < d.nconmax; c += kWave) {
+      size_t wc = (size_t)w * P->con_stride;
+      for (int c = lane; c < P->con_stride; c += kWave) {
         bool v = c < ncon;
         D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
         D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
@@ -3401,8 +3433,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     if (last) {
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
-      size_t wc = (size_t)w * d.nconmax;
-      for (int c = lane; c < d.nconmax; c += kWave) {
+      size_t wc = (size_t)w * P->con_stride;
+      for (int c = lane; c < P->con_stride; c += kWave) {
         V3 f = {0, 0, 0};
         if (c < ncon && nefc > 0) {
           int r0 = Si[L.con_efc + c];
@@ -3510,12 +3542,27 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
 #endif
 }
 
+// An overflow re-solve launch has a fixed grid (kOvfGrid, captured in graphs); each
+// workgroup takes listed worlds bid, bid + grid, ... until the list's count.  Every other
+// launch runs one world per workgroup.
+__device__ __forceinline__ bool ovf_more(const Params* __restrict__ P, int sel, int bid) {
+  if (!(sel & kSelOvf)) return false;
+  const int li = 2 * (sel & 0xff) + ((sel & kSelRPar) ? 1 : 0);
+  if (bid >= min(P->ovf_n[li], P->ovf_cap)) return false;
+  __syncthreads();  // the wave's LDS carve is reused by the next world
+  return true;
+}
+
 template <int NR, int PH, int SP>
 __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params* __restrict__ P, int w0, int w1,
                                                     int sel, int last, int integrate,
                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
-  step_body<NR, PH, SP, false>(S, P, w0, w1, sel, last, integrate, mask);
+  int bid = (int)blockIdx.x;
+  do {
+    step_body<NR, PH, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
+    bid += (int)gridDim.x;
+  } while (ovf_more(P, sel, bid));
 }
 // Phase B for the full-capacity row class (the heavy worlds: more constraint rows than the
 // class capacity) and the masked forward.  That launch holds a few hundred worlds on 256 CUs,
@@ -3527,7 +3574,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
-  step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask);
+  int bid = (int)blockIdx.x;
+  do {
+    step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask, bid);
+    bid += (int)gridDim.x;
+  } while (ovf_more(P, sel, bid));
 }
 
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);

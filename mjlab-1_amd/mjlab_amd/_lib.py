@@ -19,7 +19,8 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            "mjx_model_destroy", "mjx_sim_create", "mjx_sim_destroy", "mjx_step", "mjx_forward",
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
            "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile", "mjx_sim_spec",
-           "mjx_forward_masked", "mjx_sim_track_air_time", "mjx_marker",
+           "mjx_forward_masked", "mjx_sim_track_air_time", "mjx_marker", "mjx_sim_create_ex",
+           "mjx_sim_info",
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
@@ -50,6 +51,9 @@ def lib() -> ctypes.CDLL:
   L.mjx_model_create.argtypes = [ctypes.POINTER(ModelDesc), ci, ctypes.POINTER(vp)]
   L.mjx_model_destroy.argtypes = [vp]
   L.mjx_sim_create.argtypes = [vp, ci, ci, ci, ctypes.POINTER(vp)]
+  if hasattr(L, "mjx_sim_create_ex"):
+    L.mjx_sim_create_ex.argtypes = [vp, ci, ci, ci, ci, ci, ctypes.POINTER(vp)]
+    L.mjx_sim_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
   L.mjx_sim_destroy.argtypes = [vp]
   L.mjx_step.argtypes = [vp, ci, vp]
   L.mjx_forward.argtypes = [vp, vp]

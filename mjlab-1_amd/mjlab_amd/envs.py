@@ -347,14 +347,16 @@ class ManagerBasedRlEnv:
 
   def _log_sim_counters(self, log: dict) -> None:
     """Engine overflow counters (contacts dropped because a world's contacts or rows
-    exceeded its LDS capacity, and unsupported geom pairs), cumulative over all worlds,
-    as device scalars: no host sync."""
+    exceeded its max capacity, and unsupported geom pairs) and the world-substeps re-solved
+    at the max capacity after overflowing the fast carve, cumulative over all worlds, as
+    device scalars: no host sync."""
     ev = getattr(self, "_sim_events", None)
     if ev is None:
-      ev = self._sim_events = self.sim.overflow_events()
+      ev = self._sim_events = self.sim.event_counts()
     log["Sim/contact_overflow"] = ev[0]
     log["Sim/row_overflow"] = ev[1]
     log["Sim/unsupported_pairs"] = ev[2]
+    log["Sim/resolved_overflow"] = ev[3]
 
   def packed_episode_stats(self) -> torch.Tensor:
     """Episode statistics of the last reset, packed into one fp32 vector (for the

@@ -190,7 +190,7 @@ def _stream_handle(device: torch.device) -> int:
 
 
 def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
-  """Per-world contact/row capacities held in LDS."""
+  """Per-world contact/row capacities of the fast LDS carve."""
   if os.environ.get("MJX355_WORLD_CAPACITY"):  # diagnostic: "ncon,rows"
     c, r = (int(v) for v in os.environ["MJX355_WORLD_CAPACITY"].split(","))
     return c, r
@@ -207,11 +207,30 @@ def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   return ncon, rows
 
 
+def max_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
+  """Per-world contacts / rows a world may reach before anything is dropped: a world that
+  overflows the fast carve in a substep is re-solved at this capacity (mjx_sim_create_ex).
+  The reference pools contacts over worlds ("one world may have more than nconmax",
+  sim/sim.py:82-86) and bounds each world's rows by njmax (:87-91): here every world may
+  hold the engine's 64 contacts (one wave lane each) and njmax rows -- or, with njmax unset,
+  as many rows as 64 pyramidal contacts and every joint limit make.  MJX355_RESOLVE=0: no
+  re-solve (overflow drops contacts; diagnostic)."""
+  ncon, rows = world_capacity(cfg, model)
+  if os.environ.get("MJX355_RESOLVE", "1") == "0" or os.environ.get("MJX355_WORLD_CAPACITY"):
+    return ncon, rows
+  nlim = int(np.sum(model.jnt_limited)) if model.njnt else 0
+  cmax = 64
+  rmax = 4 * cmax + 2 * nlim
+  if cfg.njmax is not None:
+    rmax = min(rmax, int(cfg.njmax))
+  return max(ncon, cmax), max(rows, rmax)
+
+
 _capacity_warned: set = set()
 
 
 def _warn_capacity(cfg: SimulationCfg, ncon: int, rows: int) -> None:
-  """Warn once per distinct clamp: a world whose contacts or rows overflow the LDS
+  """Warn once per distinct clamp: a world whose contacts or rows overflow the max
   capacity drops whole contacts (counted in `engine_counters`, `stats()` and the env's
   extras["log"]["Sim/..."] entries)."""
   asked = (cfg.nconmax, cfg.njmax)
@@ -247,11 +266,16 @@ class Simulation:
     check(L.mjx_model_create(ctypes.byref(desc), self._torch_device.index,
                              ctypes.byref(self._model_ptr)))
     del keep
-    self.nconmax, self.njmax = world_capacity(cfg, model)
+    # the fast carve every substep runs in, and the capacity an overflowing world is
+    # re-solved at; nconmax / njmax report the latter (what a world may hold before a
+    # contact is dropped)
+    self.fast_capacity = world_capacity(cfg, model)
+    self.nconmax, self.njmax = max_capacity(cfg, model)
     _warn_capacity(cfg, self.nconmax, self.njmax)
     self._sim = ctypes.c_void_p()
-    check(L.mjx_sim_create(self._model_ptr, self.num_envs, self.nconmax, self.njmax,
-                           ctypes.byref(self._sim)))
+    check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
+                              self.fast_capacity[1], self.nconmax, self.njmax,
+                              ctypes.byref(self._sim)))
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
                          for i in range(L.mjx_field_count(self._sim))}
     self._data_bridge = DeviceBridge(self, "", None)
@@ -388,17 +412,32 @@ class Simulation:
 
   def overflow_events(self) -> torch.Tensor:
     """Device [3] int32 view: total contact-overflow, row-overflow and unsupported-pair
-    events over all worlds since creation (kept by the engine; no kernel, no host sync)."""
+    events over all worlds since creation -- work dropped past the max capacity (kept by the
+    engine; no kernel, no host sync)."""
     if "engine_events" not in self._field_names:  # an older engine build (scripts/ab.sh)
       return self.engine_counters[:, 2:5].sum(dim=0)
     return self.field("engine_events")[0, :3]
 
+  def event_counts(self) -> torch.Tensor:
+    """Device [4] int32 view: overflow_events() followed by the re-solve count --
+    world-substeps that overflowed the fast carve and were re-solved at the max capacity
+    (nothing dropped)."""
+    return self.field("engine_events")[0, :4]
+
   def stats(self) -> dict:
-    """Engine counters: max contacts/rows seen, overflow and unsupported-pair events."""
+    """Engine counters: max contacts/rows seen, overflow and unsupported-pair events,
+    re-solves."""
     out = (ctypes.c_int32 * 8)()
     check(lib().mjx_sim_stats(self._sim, out, _stream_handle(self._torch_device)))
     return dict(max_ncon=out[0], max_nefc=out[1], con_overflow=out[2], row_overflow=out[3],
-                unsupported=out[4], max_niter=out[5])
+                unsupported=out[4], max_niter=out[5], resolved=out[6])
+
+  def info(self) -> dict:
+    """Capacities and kernels (mjx_sim_info)."""
+    out = (ctypes.c_int32 * 8)()
+    check(lib().mjx_sim_info(self._sim, out))
+    return dict(nconmax=out[0], njmax=out[1], nconmax_max=out[2], njmax_max=out[3], spec=out[4],
+                spec_max=out[5], resolve_list=out[6], row_classes=out[7])
 
   def profile(self) -> list[int]:
     """Per-stage cycle sums (diagnostic MJX_STAMPS build only)."""

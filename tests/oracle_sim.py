@@ -154,13 +154,14 @@ class OracleSimulation:
   oracle model on the next call)."""
 
   def __init__(self, num_envs: int, cfg, model, device: str = "cpu"):
-    from mjlab_amd.sim.sim import world_capacity
+    from mjlab_amd.sim.sim import max_capacity
     self.cfg = cfg
     cfg.mujoco.apply(model)
     self._mj_model = model
     self.num_envs = int(num_envs)
     self.device = device
-    self.nconmax, self.njmax = world_capacity(cfg, model)
+    # the engine's max capacity: what a world holds before a contact is dropped
+    self.nconmax, self.njmax = max_capacity(cfg, model)
     self._worlds = [OracleData(model, self.nconmax, self.njmax) for _ in range(self.num_envs)]
     w0 = self._worlds[0]
     n = self.num_envs
@@ -210,10 +211,13 @@ class OracleSimulation:
   def overflow_events(self) -> torch.Tensor:
     return self._events
 
+  def event_counts(self) -> torch.Tensor:
+    return torch.cat([self._events, torch.zeros(1, dtype=torch.int32)])
+
   def stats(self) -> dict:
     return dict(max_ncon=int(self.data.ncon.max()), max_nefc=int(self.data.nefc.max()),
                 con_overflow=int(self._events[0]), row_overflow=int(self._events[1]),
-                unsupported=int(self._events[2]), max_niter=0)
+                unsupported=int(self._events[2]), max_niter=0, resolved=0)
 
   def marker(self, tag: int) -> None:
     pass

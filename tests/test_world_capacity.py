@@ -9,7 +9,7 @@ import re
 import pytest
 
 from mjlab_amd.scenes import load_scene
-from mjlab_amd.sim.sim import SimulationCfg, world_capacity
+from mjlab_amd.sim.sim import SimulationCfg, max_capacity, world_capacity
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -36,9 +36,28 @@ def test_engine_capacity_bounds():
     world_capacity(SimulationCfg(engine_capacity=(48, 300)), m)
 
 
+def test_max_capacity_is_the_resolve_carve(monkeypatch):
+  """An overflowing world is re-solved at 64 contacts and njmax rows (bounded by what 64
+  pyramidal contacts and every joint limit make); MJX355_RESOLVE=0 turns that off."""
+  g1, go1 = load_scene("g1_velocity"), load_scene("go1_velocity")
+  cfg = SimulationCfg(nconmax=35, njmax=300)
+  assert max_capacity(cfg, g1) == (64, 300)
+  assert max_capacity(cfg, go1) == (64, 4 * 64 + 2 * 12)
+  assert max_capacity(SimulationCfg(), g1) == (64, 4 * 64 + 2 * 29)
+  assert max_capacity(SimulationCfg(njmax=100), g1) == (64, 100)
+  from mjlab_amd.tracking import make_tracking_env_cfg
+  assert max_capacity(make_tracking_env_cfg().sim, load_scene("g1_tracking")) == (64, 250)
+  monkeypatch.setenv("MJX355_RESOLVE", "0")
+  assert max_capacity(cfg, g1) == (48, 160)
+
+
 def test_specs_carry_the_task_capacities():
   text = open(os.path.join(ROOT, "mjlab-1_amd", "csrc", "specs.inc")).read()
-  caps = {mm.group(1): (int(mm.group(2)), int(mm.group(3))) for mm in
-          re.finditer(r"^MJX_SPEC\(\d+, (\w+),.*, (\d+), (\d+)\)$", text, re.M)}
-  assert caps["g1_tracking"] == (64, 250)
-  assert caps["g1_velocity"] == caps["go1_velocity"] == caps["g1_jump"] == (48, 160)
+  caps = {}
+  for mm in re.finditer(r"^MJX_SPEC\(\d+, (\w+),.*, (\d+), (\d+)\)$", text, re.M):
+    caps.setdefault(mm.group(1), []).append((int(mm.group(2)), int(mm.group(3))))
+  assert caps["g1_tracking"] == [(64, 250)]
+  for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
+    assert caps[name] == [(48, 160), (64, 300)], name
+  for name in ("go1_velocity", "go1_velocity_rough"):
+    assert caps[name] == [(48, 160), (64, 280)], name
