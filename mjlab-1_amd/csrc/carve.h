@@ -52,7 +52,9 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::xaxis, 3 * d.njnt, A}, {&Lds::stmass, nb, 0}, {&Lds::subtree_com, 3 * nb, A | Cp},
     {&Lds::cinert, 10 * nb, A}, {&Lds::crb, 10 * nb, A}, {&Lds::cvel, 6 * nb, A | Cp},
     {&Lds::cacc, 6 * nb, A | Cp}, {&Lds::stlin, 3 * nb, A}, {&Lds::stang, 3 * nb, A},
-    {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, A | Cp},
+    // cdofdot: phase A only, in the crb slot (below); phase C gets the velocity-product
+    // acceleration cacc_v(b) = -gravity + sum cdofdot * qvel (6 per body) that A's RNE forms
+    {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, 0}, {&Lds::cacc_v, 6 * nb, Cp},
     {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
     {&Lds::M, nv * nv, A | B}, {&Lds::H, nv * nv, A | B},
@@ -78,7 +80,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
                                      &Lds::efc_aref, &Lds::efc_D, &Lds::efc_J};
   int Lds::* const packC[] = {
-      &Lds::cdof, &Lds::cdofdot, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
+      &Lds::cdof, &Lds::cacc_v, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
       &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
       &Lds::con_n, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
       // written by phase B:
@@ -141,6 +143,10 @@ constexpr Lds make_lds(const Dims& d, int ph) {
       L.stlin = L.cinert;
       L.stang = L.cinert + nb3;
     }
+    // cdofdot lives from comVel to RNE's acceleration sum, in the crb slot: M is assembled
+    // (crb dead) and RNE's body forces are written there only after that sum
+    if (10 * nb >= 6 * nv) L.cdofdot = L.crb;
+    else take(&Lds::cdofdot);
     const int gp = (3 * d.ngeom_lds + 3) & ~3;
     if (g2.second >= gp + 9 * d.ngeom_lds) {
       L.gxpos = g2.first;

@@ -110,7 +110,7 @@ struct Lds {
   int qpos, qvel, ctrl, qacc_ws, qfrc_applied, xfrc;
   int xpos, xquat, xmat, xipos, ximat, xanchor, xaxis;
   int stmass, subtree_com, cinert, crb, cvel, cacc, stlin, stang;
-  int cdof, cdofdot, gxpos, gxmat, sxpos, sxmat;
+  int cdof, cdofdot, cacc_v, gxpos, gxmat, sxpos, sxmat;
   int M, H;
   int qfrc_bias, qfrc_passive, qfrc_act, qfrc_smooth, qacc_smooth, x, Mx, grad, srch, Ms,
       qfrc_con, vtmp, act_force, act_len, act_vel;

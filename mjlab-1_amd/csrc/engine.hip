@@ -118,8 +118,7 @@ __global__ void ovf_clear_kernel(int* n) { *n = 0; }
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
 template <int NR>
 static StepFn phase_fn_nr(int ph) {
-  return ph == 0 ? step_phase<NR, 0, 0> : ph == 1 ? step_phase<NR, 1, 0>
-       : ph == 2 ? step_phase<NR, 2, 0> : step_newton_lat<NR, 0>;
+  return phase_kernel<NR, 0>(ph);
 }
 static StepFn generic_fn(int nv, int ph) {
   // exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36), multiples of 8 otherwise
@@ -206,11 +205,11 @@ static size_t lds_bytes(const Params& host, int ph) {
 hipError_t prepare_step(const Params& host) {
   size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
   for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
-  for (int ph = 0; ph < 4; ph++) {
-    if (shmem[ph == 3 ? 1 : ph] > 64 * 1024) {
+  for (int ph = 0; ph < 7; ph++) {  // phase codes of phase_kernel: 3 and 5 are phase B
+    const int c = ph == 3 || ph == 5 ? 1 : ph == 4 ? 0 : ph == 6 ? 2 : ph;
+    if (shmem[c] > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)step_fn(host, ph),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)shmem[ph == 3 ? 1 : ph]);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem[c]);
       if (e != hipSuccess) return e;
     }
   }
@@ -313,14 +312,14 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
   const int par = sub & 1;
   const int g = std::min(hbig.ovf_cap, kOvfGrid);
   const int sel = k | kSelOvf | (par ? kSelRPar : 0);
-  hipLaunchKernelGGL(step_fn(hbig, 0), dim3(g), dim3(kWave), lds_bytes(hbig, 0), cs, dbig, w0, w1,
+  hipLaunchKernelGGL(step_fn(hbig, 4), dim3(g), dim3(kWave), lds_bytes(hbig, 0), cs, dbig, w0, w1,
                      sel, last, integrate, nullptr);
-  hipLaunchKernelGGL(step_fn(hbig, 3), dim3(g), dim3(kWave), lds_bytes(hbig, 1), cs, dbig, w0, w1,
+  hipLaunchKernelGGL(step_fn(hbig, 5), dim3(g), dim3(kWave), lds_bytes(hbig, 1), cs, dbig, w0, w1,
                      sel, last, -1, nullptr);
-  hipLaunchKernelGGL(step_fn(hbig, 2), dim3(g), dim3(kWave), lds_bytes(hbig, 2), cs, dbig, w0, w1,
+  hipLaunchKernelGGL(step_fn(hbig, 6), dim3(g), dim3(kWave), lds_bytes(hbig, 2), cs, dbig, w0, w1,
                      sel, last, integrate, nullptr);
   if (next_a && !last)
-    hipLaunchKernelGGL(step_fn(host, 0), dim3(g), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
+    hipLaunchKernelGGL(step_fn(host, 4), dim3(g), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
                        sel | ((sub + 1) & 1 ? kSelAPar : 0), sub + 1 == nsubstep - 1, integrate,
                        nullptr);
   hipLaunchKernelGGL(ovf_clear_kernel, dim3(1), dim3(1), 0, cs, host.ovf_n + 2 * k + par);

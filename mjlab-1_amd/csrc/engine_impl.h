@@ -2038,7 +2038,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     }
     sync();
     // RNE (flg_acc = 0): cacc(b) = -gravity + sum over the dofs moving b of cdofdot * qvel
-    // (broadcast loop), body forces f(b) into the crb slot (dead after M), then
+    // (broadcast loop; handed to phase C as cacc_v), body forces f(b) into the crb slot (dead
+    // after M; cdofdot's slot, read by every lane before the barrier), then
     // cfrc(b) = f summed over the subtree into the cacc slot (dead after RNE in phase A)
     {
       float a[6] = {0.f, 0.f, 0.f, -o.gravity[0], -o.gravity[1], -o.gravity[2]};
@@ -2053,8 +2054,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           a[t + 1] = fmaf(f, c2.y, a[t + 1]);
         }
       }
+      sync();  // cdofdot (crb slot) read by every lane before the body forces land there
       if (bl) {
         const int b = B.b;
+#pragma unroll
+        for (int t = 0; t < 6; t++) gc[LC.cacc_v + 6 * b + t] = a[t];
         float f1[6], iv[6], f2[6];
         inert_mul(f1, S + L.cinert + 10 * b, a);
         inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
@@ -2900,7 +2904,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
     cp4(gw + LB.efc_D, S + L.efc_D, nr4, lane);
     cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
-    cp4(gc + LC.cdofdot, S + L.cdofdot, 6 * nvp, lane);
     cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
     cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
     cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
@@ -3302,18 +3305,22 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     const int niter_last = ints[5];
     STAMP(15);
     // =========================================================== post-constraint acc
-    // cacc(b) = -gravity + sum over the dofs moving b of cdofdot * qvel + cdof * qacc
-    // (broadcast loop over the dofs, no level syncs)
+    // cacc(b) = cacc_v(b) + sum over the dofs moving b of cdof * qacc, cacc_v(b) = -gravity
+    // + sum cdofdot * qvel from phase A's RNE (broadcast loop over the dofs, no level syncs)
     {
-      float a[6] = {0.f, 0.f, 0.f, -o.gravity[0], -o.gravity[1], -o.gravity[2]};
+      float a[6];
+#pragma unroll
+      for (int t = 0; t < 6; t++) a[t] = S[L.cacc_v + 6 * B.b + t];
 #pragma unroll 4
       for (int j = 0; j < nv; j++) {
-        const bool in = (B.dofs >> j) & 1ull;
-        const float fv = in ? S[L.qvel + j] : 0.f, fa = in ? S[L.x + j] : 0.f;
-        const float* cdd = S + L.cdofdot + 6 * j;
+        const float fa = (B.dofs >> j) & 1ull ? S[L.x + j] : 0.f;
         const float* cd = S + L.cdof + 6 * j;
 #pragma unroll
-        for (int t = 0; t < 6; t++) a[t] = fmaf(fv, cdd[t], fmaf(fa, cd[t], a[t]));
+        for (int t = 0; t < 6; t += 2) {
+          const float2 c2 = *reinterpret_cast<const float2*>(cd + t);
+          a[t] = fmaf(fa, c2.x, a[t]);
+          a[t + 1] = fmaf(fa, c2.y, a[t + 1]);
+        }
       }
       if (bl) {
 #pragma unroll
@@ -3542,9 +3549,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
 #endif
 }
 
-// An overflow re-solve launch has a fixed grid (kOvfGrid, captured in graphs); each
-// workgroup takes listed worlds bid, bid + grid, ... until the list's count.  Every other
-// launch runs one world per workgroup.
+// An overflow re-solve launch (step_ovf) has a fixed grid (kOvfGrid, captured in graphs);
+// each workgroup takes listed worlds bid, bid + grid, ... until the list's count.  Every
+// other launch runs one world per workgroup.
 __device__ __forceinline__ bool ovf_more(const Params* __restrict__ P, int sel, int bid) {
   if (!(sel & kSelOvf)) return false;
   const int li = 2 * (sel & 0xff) + ((sel & kSelRPar) ? 1 : 0);
@@ -3558,11 +3565,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
                                                     int sel, int last, int integrate,
                                                     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
-  int bid = (int)blockIdx.x;
-  do {
-    step_body<NR, PH, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
-    bid += (int)gridDim.x;
-  } while (ovf_more(P, sel, bid));
+  step_body<NR, PH, SP, false>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
 }
 // Phase B for the full-capacity row class (the heavy worlds: more constraint rows than the
 // class capacity) and the masked forward.  That launch holds a few hundred worlds on 256 CUs,
@@ -3574,13 +3577,39 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
-  int bid = (int)blockIdx.x;
-  do {
-    step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask, bid);
-    bid += (int)gridDim.x;
-  } while (ovf_more(P, sel, bid));
+  step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
+}
+
+// The overflow re-solve launches (sel & kSelOvf; ovf_chain): a fixed grid of kOvfGrid
+// workgroups, each looping over the listed worlds.  A separate entry, so that the loop's
+// live ranges stay out of the bulk kernels (inlined into step_phase the loop cost phase A 74
+// VGPRs and phase C 64); its few worlds need no residency.
+template <int NR, int PH, int SP, bool LAT>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_ovf(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  for (int bid = (int)blockIdx.x;; bid += (int)gridDim.x) {
+    step_body<NR, PH, SP, LAT>(S, P, w0, w1, sel, last, integrate, mask, bid);
+    if (!ovf_more(P, sel, bid + (int)gridDim.x)) break;
+  }
 }
 
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
+
+// kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4 / 5 / 6: A / B latency / C
+// of the overflow re-solve
+template <int NR, int SP>
+StepFn phase_kernel(int ph) {
+  switch (ph) {
+    case 0: return step_phase<NR, 0, SP>;
+    case 1: return step_phase<NR, 1, SP>;
+    case 2: return step_phase<NR, 2, SP>;
+    case 3: return step_newton_lat<NR, SP>;
+    case 4: return step_ovf<NR, 0, SP, false>;
+    case 5: return step_ovf<NR, 1, SP, true>;
+    default: return step_ovf<NR, 2, SP, false>;
+  }
+}
 
 }  // namespace mjx

@@ -14,11 +14,9 @@ namespace mjx {
 StepFn MJX_CAT(spec_fn_, MJX_SPEC_ID)(int ph) {
   constexpr int NR = spec_nr<MJX_SPEC_ID>();
   static_assert(ModelSpec<MJX_SPEC_ID>::on, "unknown specialisation");
-  // ph 3: the latency form of phase B (full-capacity row class, masked forward)
-  return ph == 0 ? step_phase<NR, 0, MJX_SPEC_ID>
-       : ph == 1 ? step_phase<NR, 1, MJX_SPEC_ID>
-       : ph == 2 ? step_phase<NR, 2, MJX_SPEC_ID>
-                 : step_newton_lat<NR, MJX_SPEC_ID>;
+  // ph 3: the latency form of phase B (full-capacity row class, masked forward); 4-6: the
+  // overflow re-solve's A / B / C (phase_kernel)
+  return phase_kernel<NR, MJX_SPEC_ID>(ph);
 }
 
 }  // namespace mjx

@@ -171,16 +171,19 @@ def load_nan_dump(path: str) -> tuple[dict, dict]:
 @dataclass(kw_only=True)
 class SimulationCfg:
   nconmax: int | None = None
-  """Contacts per world (engine holds at most 64 per world in LDS)."""
+  """Contacts per world (the engine holds at most 64 per world in LDS; the reference's is a
+  per-world average of a pooled budget, so a world overflowing the fast carve is re-solved
+  at 64, `max_capacity`)."""
   njmax: int | None = None
-  """Constraint rows per world held in LDS."""
+  """Constraint rows per world: the max capacity a world is re-solved at."""
   ls_parallel: bool = True  # accepted for API compatibility; the line search is exact
   contact_sensor_maxmatch: int = 64
   engine_capacity: tuple[int, int] | None = None
-  """(contacts, rows) per world the engine holds in LDS (this build's knob, not the
-  reference's).  None: 48 contacts and at most 160 rows, the fast carve for tasks whose
-  worlds stay far below it.  A task whose worlds reach it (tracking: 186 rows and 49
-  contacts at 4,096 random-action worlds) sets the reference's `njmax` here instead."""
+  """(contacts, rows) per world of the fast LDS carve every substep runs in (this build's
+  knob, not the reference's).  None: 48 contacts and at most 160 rows, far above what the
+  velocity and jump worlds reach; the rare world past it is re-solved at the max capacity
+  (`max_capacity`: 64 contacts, `njmax` rows) within the same substep.  A task whose worlds
+  reach it often may hold the reference's `njmax` here instead (tracking: (64, 256))."""
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -273,9 +276,14 @@ class Simulation:
     self.nconmax, self.njmax = max_capacity(cfg, model)
     _warn_capacity(cfg, self.nconmax, self.njmax)
     self._sim = ctypes.c_void_p()
-    check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
-                              self.fast_capacity[1], self.nconmax, self.njmax,
-                              ctypes.byref(self._sim)))
+    if not hasattr(L, "mjx_sim_create_ex"):  # an older engine build (MJX355_LIB, scripts/lib_ab.sh)
+      self.nconmax, self.njmax = self.fast_capacity
+      check(L.mjx_sim_create(self._model_ptr, self.num_envs, self.nconmax, self.njmax,
+                             ctypes.byref(self._sim)))
+    else:
+      check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
+                                self.fast_capacity[1], self.nconmax, self.njmax,
+                                ctypes.byref(self._sim)))
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
                          for i in range(L.mjx_field_count(self._sim))}
     self._data_bridge = DeviceBridge(self, "", None)
