@@ -237,6 +237,9 @@ def main():
   ap.add_argument("--eager", action="store_true", help="reference-style eager env.step (host syncs)")
   ap.add_argument("--launch-reps", type=int, default=20,
                   help="env steps timed one by one with HIP events after the timed region")
+  ap.add_argument("--engine-capacity", default=None,
+                  help="diagnostic: 'C,R' or 'none' overrides the task's SimulationCfg.engine_capacity "
+                       "(the fast LDS carve; worlds past it are re-solved at the max capacity)")
   ap.add_argument("--allow-overflow", action="store_true",
                   help="exit 0 even if contacts were dropped in the timed steps")
   args = ap.parse_args()
@@ -260,7 +263,15 @@ def main():
   device = f"cuda:{local}"
 
   from mjlab_amd.envs import make_env
-  env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
+  if args.engine_capacity is None:
+    env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
+  else:
+    from mjlab_amd.envs import ManagerBasedRlEnv, load_env_cfg
+    cfg = load_env_cfg(args.task)
+    cfg.scene.num_envs, cfg.seed = args.num_envs, mjdist.rank_seed(42, rank)
+    cap = args.engine_capacity
+    cfg.sim.engine_capacity = None if cap == "none" else tuple(int(v) for v in cap.split(","))
+    env = ManagerBasedRlEnv(cfg, device=device)
   env._bench_task = args.task
   sim = env.sim
   m = sim.mj_model

@@ -40,7 +40,9 @@ Checks per shadowed substep (fp32 engine vs fp64 oracle):
     qacc is not), against the oracle's own step with SENS_FORCE_REL x the world's largest
     constraint force on top; the other sensors against the oracle's sensors at the engine's
     own qacc (an acceleration-stage sensor is linear in qacc, so the solver's accepted fp32
-    error would otherwise reach it amplified in heavy worlds);
+    error would otherwise reach it amplified in heavy worlds); and end to end against the
+    oracle's own step within that bound plus |J_s| fb, the sensors' qacc Jacobian times the
+    per-dof qacc bound of check (1);
   - the env step's fused `decimation`-substep mjx_step equal, bit for bit, to that many
     single steps, over every world.
 The multipliers sit at about twice the largest ratio measured over the four configurations
@@ -263,6 +265,26 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
     stats["sens_ratio"] = max(stats["sens_ratio"], float((es / sb).max()) if es.size else 0.0)
     _expect((es <= sb).all(), f"{where}: sensordata {int(np.argmax(es / sb))} err {es.max():.3e} "
             f"(value {float(s_cmp[int(np.argmax(es / sb))]):.3e})", stats)
+    # end to end (the non-contact sensors against the oracle's own step): within the sensor
+    # bound plus what the accepted qacc error can move them, |J_s| fb with J_s the sensors'
+    # qacc Jacobian (acceleration-stage sensors are affine in qacc: column k is the change
+    # of the oracle's sensors at the engine's qacc + fb_k e_k), formed only where the
+    # plain bound does not already hold
+    nc_ = ~cs
+    e2e = np.abs(s - s_ref)[nc_]
+    b0 = (SENS_ABS + SENS_REL * np.abs(s_ref))[nc_]
+    if nc_.any() and not (e2e <= b0).all():
+      slack = np.zeros(int(nc_.sum()))
+      for k in range(m.nv):
+        qk = qa.copy()
+        qk[k] += fb[k]
+        col = ol.step_given_qacc(m, *args, qk, nconmax=sim.nconmax, njmax=sim.njmax)["sensordata"]
+        slack += np.abs(col - gpu["sensordata"])[nc_]
+      stats["sens_e2e_jac_checked"] = stats.get("sens_e2e_jac_checked", 0) + 1
+      bj = b0 + slack + 1e-6
+      stats["sens_e2e_jac_ratio"] = max(stats.get("sens_e2e_jac_ratio", 0.0), float((e2e / bj).max()))
+      _expect((e2e <= bj).all(), f"{where}: sensordata end to end err {e2e.max():.3e} > "
+              f"sensor bound + |J_s| fb", stats)
   # (3) end to end against the oracle's own step (statistics: includes both solvers'
   # stopping points)
   stats["e2e_qvel_abs"] = max(stats["e2e_qvel_abs"], float(np.abs(st1["qvel"][i] - ref["qvel"]).max()))

@@ -56,7 +56,7 @@ def test_specs_carry_the_task_capacities():
   caps = {}
   for mm in re.finditer(r"^MJX_SPEC\(\d+, (\w+),.*, (\d+), (\d+)\)$", text, re.M):
     caps.setdefault(mm.group(1), []).append((int(mm.group(2)), int(mm.group(3))))
-  assert caps["g1_tracking"] == [(64, 250)]
+  assert caps["g1_tracking"] == [(64, 250), (48, 160)]
   for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
     assert caps[name] == [(48, 160), (64, 300)], name
   for name in ("go1_velocity", "go1_velocity_rough"):
