@@ -2894,8 +2894,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
     }
     STAMP(12);
-    // hand-off: B pack (J rows already written) and the A part of the C pack
-    const int C = d.nconmax;
+    // hand-off: B pack (J rows already written) and the A part of the C pack; the contact
+    // arrays only up to the live contacts (phase C reads none past ncon)
+    const int C = ncon;
     const int C4 = (C + 3) & ~3;
     const int nr4 = (nefc + 3) & ~3;
     cp4(gw + LB.ints, S + L.ints, 8, lane);
