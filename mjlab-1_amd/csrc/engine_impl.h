@@ -1257,6 +1257,13 @@ template <int SP> struct SpecTree {
   };
 #include "specs.inc"
 #undef MJX_SPEC_TREE
+// which carve roles a specialisation serves (bit 0 fast, bit 1 max / re-solve): kernels of
+// the other role are not compiled for it (phase_kernel returns null; the generic stand in)
+template <int SP> struct SpecRole { static constexpr int mask = 3; };
+#define MJX_SPEC_ROLE(id, m)                                                  \
+  template <> struct SpecRole<id> { static constexpr int mask = m; };
+#include "specs.inc"
+#undef MJX_SPEC_ROLE
 // the tree form is compiled for a specialisation whose dof tree is known and matches its nv
 template <int SP> constexpr bool kTree =
     SP > 0 && SpecTree<SP>::npar == ModelSpec<SP>::dims().nv && SpecTree<SP>::get().on;
@@ -3617,15 +3624,24 @@ using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 // of the overflow re-solve; 7: C fused with the next substep's A
 template <int NR, int SP>
 StepFn phase_kernel(int ph) {
+  constexpr int role = SpecRole<SP>::mask;
   switch (ph) {
     case 0: return step_phase<NR, 0, SP>;
-    case 1: return step_phase<NR, 1, SP>;
     case 2: return step_phase<NR, 2, SP>;
     case 3: return step_newton_lat<NR, SP>;
     case 4: return step_ovf<NR, 0, SP, false>;
-    case 5: return step_ovf<NR, 1, SP, true>;
-    case 6: return step_ovf<NR, 2, SP, false>;
-    default: return step_ca<NR, SP>;
+    case 1:
+      if constexpr ((role & 1) != 0) return step_phase<NR, 1, SP>;
+      else return nullptr;
+    case 5:
+      if constexpr ((role & 2) != 0) return step_ovf<NR, 1, SP, true>;
+      else return nullptr;
+    case 6:
+      if constexpr ((role & 2) != 0) return step_ovf<NR, 2, SP, false>;
+      else return nullptr;
+    default:
+      if constexpr ((role & 1) != 0) return step_ca<NR, SP>;
+      else return nullptr;
   }
 }
 
