@@ -17,7 +17,15 @@ checks here use only the model's masses, inertias and the position-level kinemat
     mass of a free-floating system without gravity;
   - Coulomb friction: a box on an incline sticks when tan(theta) < mu / sqrt(2) (the
     pyramidal cone's inscribed bound) and slides with a = g (sin theta - mu cos theta) when
-    tan(theta) > mu.
+    tan(theta) > mu;
+  - the soft-contact model's documented behaviour (MuJoCo "Computation: soft constraints"):
+    a frictionless contact with solref (timeconst, dampratio) and a constant impedance d
+    makes the penetration r a damped oscillator, r'' = (1 - d) a0 + d (-B r' - K d r) with
+    d^2 K = 1 / (timeconst dampratio)^2 and d B = 2 / timeconst, i.e. natural frequency
+    1 / (timeconst dampratio) and damping ratio dampratio, about the equilibrium
+    r_eq = (1 - d) a0 / omega^2; and with solimp's sigmoid impedance d(r) the resting
+    penetration solves d(r)^2 K r = -(1 - d(r)) g.  These are closed forms of the model's
+    definition (no constraint Jacobian, no solver), checked on trajectories.
 """
 
 from __future__ import annotations
@@ -91,6 +99,52 @@ INCLINE_XML = """
   </worldbody>
 </mujoco>
 """
+
+
+# a frictionless sphere on a plane, both geoms with one solref / solimp / margin
+SPHERE_XML = """
+<mujoco>
+  <option timestep="{h}" integrator="Euler"/>
+  <worldbody>
+    <geom name="floor" type="plane" size="5 5 0.1" condim="1" solref="{tc} {dr}"
+      solimp="{solimp}" margin="{margin}"/>
+    <body name="ball" pos="0 0 1">
+      <freejoint name="ball_joint"/>
+      <geom name="ball_geom" type="sphere" size="{R}" mass="{mass}" condim="1"
+        solref="{tc} {dr}" solimp="{solimp}" margin="{margin}"/>
+    </body>
+  </worldbody>
+</mujoco>
+"""
+
+
+def soft_sphere(tc: float, dr: float, solimp=(0.95, 0.95, 0.001, 0.5, 2.0), h: float = 1e-4,
+                margin: float = 0.005, R: float = 0.1, mass: float = 2.0):
+  spec = Spec.from_string(SPHERE_XML.format(h=h, tc=tc, dr=dr, solimp=" ".join(str(v) for v in solimp),
+                                            margin=margin, R=R, mass=mass))
+  spec.option.update(timestep=h, integrator="euler")
+  return spec.compile()
+
+
+def solimp_impedance(solimp, r: float) -> float:
+  """MuJoCo's documented impedance d(r): x = |r| / width clipped to [0, 1], the sigmoid
+  y(x) = x^p / mid^(p-1) below the midpoint and 1 - (1-x)^p / (1-mid)^(p-1) above it,
+  d = dmin + y (dmax - dmin)."""
+  dmin, dmax, width, mid, p = solimp
+  x = min(1.0, abs(r) / width)
+  if x <= mid:
+    y = x ** p / mid ** (p - 1)
+  else:
+    y = 1.0 - (1.0 - x) ** p / (1.0 - mid) ** (p - 1)
+  return dmin + y * (dmax - dmin)
+
+
+def damped_oscillator(e0: float, omega: float, zeta: float, t: np.ndarray) -> np.ndarray:
+  """e(t) of e'' + 2 zeta omega e' + omega^2 e = 0 from e(0) = e0, e'(0) = 0."""
+  if zeta >= 1.0:
+    return e0 * (1.0 + omega * t) * np.exp(-omega * t)
+  wd = omega * np.sqrt(1.0 - zeta * zeta)
+  return e0 * np.exp(-zeta * omega * t) * (np.cos(wd * t) + zeta * omega / wd * np.sin(wd * t))
 
 
 def pendulum(L: float = 0.5):

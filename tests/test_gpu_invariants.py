@@ -179,3 +179,48 @@ def test_gpu_incline_stick_and_slip(mu, gpu_device):
       assert np.all(np.abs(z - 0.1) < 5e-3)
     else:
       assert np.all(np.abs(v1) < 5e-3) and np.all(np.abs(x) < 5e-3)
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_gpu_soft_contact_is_the_documented_oscillator(case, gpu_device):
+  """The engine's soft contact against the damped oscillator its solref defines
+  (tests/test_oracle_invariants.py::test_soft_contact_is_the_documented_oscillator)."""
+  from test_oracle_invariants import SOFT_CASES, soft_start
+  tc, dr, d = SOFT_CASES[case]
+  R, margin = 0.1, 0.005
+  m, omega, r_eq, e0, n = soft_start(tc, dr, d, R, margin)
+  sim = _sim(m, 1, gpu_device)
+  q = np.array(m.key_qpos, float)
+  q[2] = R + margin + r_eq + e0
+  _set(sim, q, np.zeros(m.nv))
+  z = torch.zeros(n, device=sim.data.qpos.device, dtype=torch.float64)
+  for k in range(n):
+    sim.step()
+    z[k] = sim.data.qpos[0, 2]
+  t = (np.arange(n) + 1) * m.timestep
+  e = z.cpu().numpy() - (R + margin + r_eq)
+  ref = inv.damped_oscillator(e0, omega, dr, t)
+  # fp32 positions near 0.1 m: ulp 7e-9 m, a few percent of |e0| >= 4.4e-4 m at most
+  assert np.abs(e - ref).max() <= 0.02 * abs(e0), (np.abs(e - ref).max(), e0)
+
+
+def test_gpu_soft_contact_resting_penetration_follows_solimp(gpu_device):
+  solimp = (0.5, 0.95, 0.002, 0.5, 2.0)
+  tc, dr, R = 0.02, 1.0, 0.1
+  m = inv.soft_sphere(tc, dr, solimp=solimp, h=2e-4, margin=0.0, R=R)
+  K = 1.0 / (solimp[1] * tc * dr) ** 2
+  f = lambda r: inv.solimp_impedance(solimp, r) ** 2 * K * r + (1 - inv.solimp_impedance(solimp, r)) * inv.G
+  lo, hi = -0.05, 0.0
+  for _ in range(100):
+    mid = 0.5 * (lo + hi)
+    lo, hi = (mid, hi) if f(mid) < 0 else (lo, mid)
+  r_eq = 0.5 * (lo + hi)
+  sim = _sim(m, 1, gpu_device)
+  q = np.array(m.key_qpos, float)
+  q[2] = R
+  _set(sim, q, np.zeros(m.nv))
+  for _ in range(5000):
+    sim.step()
+  torch.cuda.synchronize()
+  zr = float(sim.data.qpos[0, 2]) - R
+  assert zr == pytest.approx(r_eq, rel=2e-3, abs=2e-7), (zr, r_eq)

@@ -235,3 +235,71 @@ def test_incline_stick_and_slip(mu):
   a = (od.qvel[0] - v0) / (od.time - t0)
   assert a == pytest.approx(inv.G * (np.sin(th) - mu * np.cos(th)), rel=3e-2)
   assert abs(od.qpos[2] - 0.1) < 5e-3  # sliding on the plane, not tipping over or sinking
+
+
+# (timeconst, dampratio, constant impedance d)
+SOFT_CASES = [(0.02, 1.0, 0.95), (0.05, 0.3, 0.5), (0.04, 0.5, 0.7)]
+
+
+def soft_start(tc, dr, d, R=0.1, margin=0.005):
+  """(model, omega, r_eq, e0, steps): the oscillator's parameters and a start below the
+  equilibrium that keeps the contact detected (r < 0) and pushing for the whole run."""
+  m = inv.soft_sphere(tc, dr, solimp=(d, d, 0.001, 0.5, 2.0), margin=margin, R=R)
+  omega = 1.0 / (tc * dr)
+  r_eq = -(1.0 - d) * inv.G / omega ** 2
+  e0 = -1e-3 if dr >= 1.0 else 0.4 * r_eq  # underdamped: overshoots by < |e0| < |r_eq|
+  n = int(round((6.0 / omega if dr >= 1.0 else 3.0 * 2 * np.pi / omega) / m.timestep))
+  return m, omega, r_eq, e0, n
+
+
+@pytest.mark.parametrize("tc,dr,d", SOFT_CASES)
+def test_soft_contact_is_the_documented_oscillator(tc, dr, d):
+  """A frictionless sphere resting on a plane with a constant impedance d, started below its
+  equilibrium with no velocity: the penetration follows the damped oscillator of natural
+  frequency 1 / (tc dr) and damping ratio dr about r_eq = -(1 - d) g / omega^2 (the
+  constraint's position is dist - margin)."""
+  R, margin = 0.1, 0.005
+  m, omega, r_eq, e0, n = soft_start(tc, dr, d, R, margin)
+  od = OracleData(m)
+  q = np.array(m.key_qpos, float)
+  q[2] = R + margin + r_eq + e0
+  od.qpos[:] = q
+  od.qvel[:] = 0.0
+  z = np.empty(n)
+  for k in range(n):
+    od.step()
+    z[k] = od.qpos[2]
+  t = (np.arange(n) + 1) * m.timestep
+  e = z - (R + margin + r_eq)
+  ref = inv.damped_oscillator(e0, omega, dr, t)
+  # semi-implicit Euler at h omega <= 0.007: measured 0.16-0.30 % of e0
+  assert np.abs(e - ref).max() <= 0.01 * abs(e0), (np.abs(e - ref).max(), e0)
+  assert np.abs(od.qvel[[0, 1, 3, 4, 5]]).max() < 1e-9  # no lateral / rotational motion
+
+
+def test_soft_contact_resting_penetration_follows_solimp():
+  """With solimp's sigmoid impedance (width 2 mm) the sphere comes to rest at the depth
+  where d(r)^2 K r = -(1 - d(r)) g, K = 1 / (dmax tc dr)^2 -- the documented impedance
+  curve, found here by bisection."""
+  solimp = (0.5, 0.95, 0.002, 0.5, 2.0)
+  tc, dr, R, margin = 0.02, 1.0, 0.1, 0.0
+  m = inv.soft_sphere(tc, dr, solimp=solimp, h=2e-4, margin=margin, R=R)
+  K = 1.0 / (solimp[1] * tc * dr) ** 2
+  f = lambda r: inv.solimp_impedance(solimp, r) ** 2 * K * r + (1 - inv.solimp_impedance(solimp, r)) * inv.G
+  lo, hi = -0.05, 0.0  # f(lo) < 0 < f(hi)
+  for _ in range(100):
+    mid = 0.5 * (lo + hi)
+    lo, hi = (mid, hi) if f(mid) < 0 else (lo, mid)
+  r_eq = 0.5 * (lo + hi)
+  od = OracleData(m)
+  q = np.array(m.key_qpos, float)
+  q[2] = R
+  od.qpos[:] = q
+  od.qvel[:] = 0.0
+  for _ in range(5000):  # 1 s: >> the 20 ms time constant
+    od.step()
+  assert abs(od.qvel[2]) < 1e-6
+  assert od.qpos[2] - R == pytest.approx(r_eq, rel=1e-3, abs=1e-7), (od.qpos[2] - R, r_eq)
+  # the impedance matters: a constant d = dmax would rest elsewhere
+  d = solimp[1]
+  assert abs(r_eq - (-(1 - d) * inv.G / (d * d * K))) > 1e-5
