@@ -125,7 +125,10 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
  * truncated (the reference's budget semantics: its nconmax is pooled, sim/sim.py:82-92; its
  * njmax, 300 rows for the velocity tasks, bounds each world).  Only what overflows the max
  * capacity is dropped (counted by mjx_sim_stats).  The contact output arrays hold
- * nconmax_max slots per world; a masked forward runs at the max capacity throughout. */
+ * nconmax_max slots per world; a masked forward runs at the max capacity throughout.  A batch
+ * the engine splits into concurrent halves (large batches of models without Newton row
+ * classes) gets no re-solve: its max capacity is the fast carve (mjx_sim_info reports the
+ * capacity wired). */
 int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax, int nconmax_max,
                       int njmax_max, mjxSim** out);
 int mjx_sim_destroy(mjxSim* sim);

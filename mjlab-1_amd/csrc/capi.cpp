@@ -56,6 +56,7 @@ struct FieldInfo {
   int64_t count, width;
   bool per_world;     // data field (leading nworld) or expanded model field
   bool model;
+  bool scalar = false;  // one value per world (time, ncon, ...): shape [nworld]
 };
 }  // namespace
 
@@ -527,7 +528,18 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
       return fail("per-world LDS footprint exceeds 160 KiB; lower njmax/nconmax");
     }
   }
-  s->big = nconmax_max > nconmax || njmax_max > njmax;
+  s->spec = mjx::find_spec(s->d, model->dof_parentid.data());
+  s->nrowclass = mjx::choose_row_classes(s->d, s->spec, s->row_cap);
+  // batch splits (launch_step): large batches of models without row classes run as
+  // concurrent halves.  MJX355_SPLIT=<n> overrides (diagnostic; 1 = one launch set per phase),
+  // also for models with row classes (each split then forks its own class streams).
+  s->side.nsplit = nworld >= mjx::kSplitMinWorlds && s->nrowclass == 0 ? 2 : 1;
+  if (const char* ev = getenv("MJX355_SPLIT")) s->side.nsplit = std::max(1, std::min(atoi(ev), mjx::kMaxSplit));
+  // The overflow re-solve forks its chain from the stream that ran phase A.  With batch
+  // splits that is a split stream, and a second-level fork from a captured side stream
+  // crashes hipStreamEndCapture under the HIP runtime torch bundles:
+  // split batches keep the fast carve as their max capacity (overflow drops, counted).
+  s->big = (nconmax_max > nconmax || njmax_max > njmax) && s->side.nsplit == 1;
   s->con_stride = s->big ? nconmax_max : nconmax;
   if (s->big) {
     s->dbig = s->d;
@@ -547,18 +559,11 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
     // re-solve list capacity per split and substep parity: every world may be listed
     s->ovf_cap = nworld;
   }
-  s->spec = mjx::find_spec(s->d, model->dof_parentid.data());
-  s->nrowclass = mjx::choose_row_classes(s->d, s->spec, s->row_cap);
   for (int k = 0; k < mjx::kRowClasses; k++) {
     mjx::Dims ds = s->d;
     ds.njmax = k < s->nrowclass ? s->row_cap[k] : s->d.njmax;
     s->lds_ph[3 + k] = mjx::make_lds(ds, 1);
   }
-  // batch splits (launch_step): large batches of models without row classes run as
-  // concurrent halves.  MJX355_SPLIT=<n> overrides (diagnostic; 1 = one launch set per phase),
-  // also for models with row classes (each split then forks its own class streams).
-  s->side.nsplit = nworld >= mjx::kSplitMinWorlds && s->nrowclass == 0 ? 2 : 1;
-  if (const char* ev = getenv("MJX355_SPLIT")) s->side.nsplit = std::max(1, std::min(atoi(ev), mjx::kMaxSplit));
   {
     hipError_t e = hipSuccess;
     if (s->side.nsplit > 1) {
@@ -636,13 +641,17 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
   if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
   size_t k = 0;
   char* base = (char*)s->arena;
+  // a field whose count is the literal 1 (fields.h) is a per-world scalar; every other keeps
+  // its count axis even when the model makes it 1 (qpos of a one-dof model is [nworld, 1])
 #define X_FLT(name, cnt, w)                                                                  \
   s->dd.name = (float*)(base + offs[k++].second);                                            \
-  s->fields[#name] = FieldInfo{s->dd.name, true, (int64_t)(cnt), (int64_t)(w), true, false}; \
+  s->fields[#name] = FieldInfo{s->dd.name, true, (int64_t)(cnt), (int64_t)(w), true, false,  \
+                               std::string(#cnt) == "1"};                                    \
   s->names.push_back(#name);
 #define X_INT(name, cnt, w)                                                                    \
   s->dd.name = (int32_t*)(base + offs[k++].second);                                            \
-  s->fields[#name] = FieldInfo{s->dd.name, false, (int64_t)(cnt), (int64_t)(w), true, false};  \
+  s->fields[#name] = FieldInfo{s->dd.name, false, (int64_t)(cnt), (int64_t)(w), true, false,  \
+                               std::string(#cnt) == "1"};                                      \
   s->names.push_back(#name);
   MJX_DATA_FLOAT_FIELDS(X_FLT)
   MJX_DATA_INT_FIELDS(X_INT)
@@ -803,7 +812,7 @@ int mjx_field(mjxSim* s, const char* cname, DLManagedTensor** out) {
   auto* t = new DLManagedTensor();
   std::vector<int64_t> shape;
   shape.push_back(lead);
-  if (!(fi.count == 1 && fi.width == 1 && !fi.model)) shape.push_back(fi.count);
+  if (!fi.scalar) shape.push_back(fi.count);
   if (fi.width > 1) shape.push_back(fi.width);
   t->dl_tensor.data = ptr;
   t->dl_tensor.device = DLDevice{kDLROCM, s->model->device};

@@ -27,6 +27,12 @@
 
 #include "engine.h"
 
+// FMA contraction only within one expression (the front end's fmuladd), never across
+// statements in the back end: one source line then rounds the same in every kernel it is
+// inlined into (step_phase, the re-solve's step_ovf, step_ca), so a world's substep is bit
+// for bit the same whichever launch set ran it.
+#pragma clang fp contract(on)
+
 namespace mjx {
 
 #define MINVAL 1e-15f

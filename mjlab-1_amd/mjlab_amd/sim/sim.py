@@ -274,7 +274,6 @@ class Simulation:
     # contact is dropped)
     self.fast_capacity = world_capacity(cfg, model)
     self.nconmax, self.njmax = max_capacity(cfg, model)
-    _warn_capacity(cfg, self.nconmax, self.njmax)
     self._sim = ctypes.c_void_p()
     if not hasattr(L, "mjx_sim_create_ex"):  # an older engine build (MJX355_LIB, scripts/lib_ab.sh)
       self.nconmax, self.njmax = self.fast_capacity
@@ -284,6 +283,11 @@ class Simulation:
       check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
                                 self.fast_capacity[1], self.nconmax, self.njmax,
                                 ctypes.byref(self._sim)))
+      # the capacity the engine wired: batch-split launch topologies (large batches of
+      # models without Newton row classes) have no re-solve, their max is the fast carve
+      info = self.info()
+      self.nconmax, self.njmax = info["nconmax_max"], info["njmax_max"]
+    _warn_capacity(cfg, self.nconmax, self.njmax)
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
                          for i in range(L.mjx_field_count(self._sim))}
     self._data_bridge = DeviceBridge(self, "", None)

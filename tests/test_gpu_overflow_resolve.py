@@ -5,13 +5,17 @@
 The reference pools its contact budget over worlds (`sim/sim.py:82-91`: nconmax is a
 per-world *average*, one world may hold more) and its njmax bounds a world's rows: at the
 velocity task's njmax=300 a world with 49..64 contacts loses nothing there, and loses
-nothing here.  Worlds are placed at pelvis heights that give the oracle (at the max
-capacity) 40..64 contacts and 160..256 rows (measured in `_HEIGHTS`), so both kinds of
-overflow occur next to worlds that fit; every world is then shadowed on the oracle
-substep by substep (the rollout-parity checks of test_gpu_rollout_parity.py), the
-re-solve counter is checked against the worlds that overflowed, nothing is dropped, and
-the fused / graph-captured multi-substep step (the re-solve chain on its own stream,
-joined before the next substep's phase A) equals single steps bit for bit.
+nothing here.  Two set-ups:
+  - parity: a small fast carve (20 / 80) and G1 worlds standing up to 25 mm into the floor
+    (14-28 contacts), so about half the worlds overflow it in physical states; every world
+    is shadowed on the oracle at 64 / 300 substep by substep (the rollout-parity checks of
+    test_gpu_rollout_parity.py), the re-solve counter equals the worlds that overflowed,
+    nothing is dropped;
+  - the task's own 48 / 160 carve with worlds placed at pelvis heights that give 40..64
+    contacts and 160..256 rows (`_HEIGHTS`, measured on the oracle): the fused and
+    graph-captured multi-substep step (the re-solve chain on its own stream, joined before
+    the next substep's phase A) equals single steps bit for bit, also at the bench batch,
+    and the masked forward matches the oracle's contact counts.
 """
 
 from __future__ import annotations
@@ -40,14 +44,35 @@ def _stats():
               per_dof_within=0, e2e_qvel_abs=0.0, e2e_qpos_abs=0.0, niter_equal=0)
 
 
-def _sim(device, n=NWORLD):
+def _sim(device, n=NWORLD, engine_capacity=None):
   from mjlab_amd.envs import load_env_cfg
   from mjlab_amd.scenes import load_scene
   from mjlab_amd.sim import Simulation
   cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.sim.engine_capacity = engine_capacity
   m = load_scene("g1_velocity")
   sim = Simulation(n, cfg.sim, m, device)
   return sim, m
+
+
+# a fast carve of 20 contacts / 80 rows: G1 worlds standing 0-25 mm into the floor hold
+# 14-28 contacts (56-112 rows), so about half of them overflow it -- physical states the
+# rollout-parity bounds were made for (the deep placements below launch the robot)
+SMALL = (20, 80)
+
+
+def _place_standing(sim, m, seed):
+  rng = np.random.default_rng(seed)
+  n = sim.num_envs
+  q = np.tile(np.asarray(m.key_qpos, float), (n, 1))
+  q[:, 2] -= 0.005 * (np.arange(n) % 6)
+  q[:, 7:] += rng.uniform(-0.05, 0.05, (n, m.nq - 7))
+  d = sim.data
+  d.qpos[:] = torch.as_tensor(q, dtype=torch.float32)
+  d.qvel[:] = torch.as_tensor(rng.normal(0.0, 0.05, (n, m.nv)), dtype=torch.float32)
+  d.qacc_warmstart.zero_()
+  d.ctrl[:] = torch.as_tensor(np.asarray(m.key_qpos, float)[7:][None] + rng.uniform(-0.1, 0.1, (n, m.nu)),
+                              dtype=torch.float32)
 
 
 def _place(sim, m, seed):
@@ -81,8 +106,10 @@ def test_capacities(gpu_device):
 
 
 def test_overflow_resolved_matches_oracle(gpu_device):
-  sim, m = _sim(gpu_device)
-  _place(sim, m, 0)
+  """Worlds past a small fast carve re-solved at 64 / 300, shadowed on the oracle at 64 / 300."""
+  sim, m = _sim(gpu_device, engine_capacity=SMALL)
+  assert sim.fast_capacity == SMALL and (sim.nconmax, sim.njmax) == (64, 300)
+  _place_standing(sim, m, 0)
   ev0 = sim.event_counts().clone()
   sel = np.arange(sim.num_envs)
   states = [_snap(sim, sel, _STATE)]
@@ -94,13 +121,13 @@ def test_overflow_resolved_matches_oracle(gpu_device):
     states.append(_snap(sim, sel, _STATE))
     outs.append(_snap(sim, sel, _OUT))
     nc, ne = outs[-1]["ncon"].reshape(-1), outs[-1]["nefc"].reshape(-1)
-    overflowing += int(((nc > 48) | (ne > 160)).sum())
+    overflowing += int(((nc > SMALL[0]) | (ne > SMALL[1])).sum())
   ev = (sim.event_counts() - ev0).cpu().tolist()
   assert ev[:3] == [0, 0, 0], f"contacts dropped: {ev}"
   # one re-solve per world-substep whose contacts or rows overflowed the fast carve
-  assert ev[3] == overflowing > K * NWORLD // 3, (ev, overflowing)
+  assert ev[3] == overflowing > K * NWORLD // 4, (ev, overflowing)
   st = sim.stats()
-  assert st["resolved"] >= ev[3] and st["max_ncon"] > 48 and st["max_nefc"] > 160
+  assert st["resolved"] >= ev[3] and st["max_ncon"] > SMALL[0] and st["max_nefc"] > SMALL[1]
   stats = _stats()
   over_checked = 0
   for t in range(K):
@@ -111,10 +138,10 @@ def test_overflow_resolved_matches_oracle(gpu_device):
       assert not ref["overflow"], f"world {w} substep {t}: the oracle overflows 64/300"
       before = stats["checked"]
       _check_step(m, ref, st0, st1, out, int(w), stats, f"world {w} substep {t}", sim)
-      if stats["checked"] > before and (ref["ncon"] > 48 or ref["nefc"] > 160):
+      if stats["checked"] > before and (ref["ncon"] > SMALL[0] or ref["nefc"] > SMALL[1]):
         over_checked += 1
   assert stats["checked"] >= 0.8 * K * NWORLD, stats
-  assert over_checked >= K * NWORLD // 3, over_checked
+  assert over_checked >= K * NWORLD // 4, over_checked
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
   assert len(stats["out_of_model"]) <= 0.02 * stats["checked"] + 1, stats["out_of_model"]
 
@@ -154,7 +181,12 @@ def _fused_vs_single(sim, nsub, graph):
   torch.cuda.synchronize()
   ev_s = (sim.event_counts() - ev1).cpu().tolist()
   for k, v in fused.items():
-    assert torch.equal(v, getattr(d, k)), f"{'graph' if graph else 'fused'} {nsub}-substep != single steps in {k}"
+    same = torch.equal(v, getattr(d, k))
+    if not same and v.dim() > 1:
+      bad = (v != getattr(d, k)).any(dim=-1).nonzero().flatten().tolist()
+      over = (((d.ncon > 48) | (d.nefc > 160)).nonzero().flatten().tolist())
+      print(f"{k}: {len(bad)} worlds differ, e.g. {bad[:12]}; overflowing after the steps: {over[:24]}")
+    assert same, f"{'graph' if graph else 'fused'} {nsub}-substep != single steps in {k}"
   assert ev_f == ev_s and ev_f[:3] == [0, 0, 0] and ev_f[3] > 0, (ev_f, ev_s)
 
 

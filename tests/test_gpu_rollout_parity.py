@@ -236,7 +236,8 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
       qfrc_smooth_err=float(np.abs(out["qfrc_smooth"][i] - (fs_o["qacc_smooth"] @ fs_o["qM"].T)).max()),
       act_force_err=float(np.abs(out["actuator_force"][i] - fs_o["actuator_force"]).max()),
       qvel_in=float(st0["qvel"][i][j]), dv=float(itg["qvel"][j] - st0["qvel"][i][j])))
-  _expect((ev <= vb).all(), f"{where}: qvel err {ev.max():.3e} (dof {int(np.argmax(ev / vb))})", stats)
+  _expect((ev <= vb).all(), f"{where}: qvel err {ev.max():.3e} (dof {int(np.argmax(ev / vb))}, "
+          f"ncon {ncon}, nefc {nefc}; {stats.get('qvel_detail', [None])[-1]})", stats)
   ep = np.abs(st1["qpos"][i] - itg["qpos"])
   pb = QPOS_ABS + QPOS_ULPS * np.abs(itg["qpos"]) + m.timestep * vb.max()
   stats["qpos_ratio"] = max(stats["qpos_ratio"], float((ep / pb).max()))
