@@ -179,6 +179,9 @@ class OracleSimulation:
         setattr(self.model, name, t)
     self._default_model_fields: dict[str, torch.Tensor] = {}
     self._events = torch.zeros(3, dtype=torch.int32)
+    # the engine's per-world counters ([nworld, 8]: contacts, rows, contact / row overflow and
+    # unsupported-pair events, cumulative)
+    self.engine_counters = torch.zeros(self.num_envs, 8, dtype=torch.int32)
     self._versions = [None] * n
     self.nan_guard = _NullGuard()
     self.reset()
@@ -248,6 +251,8 @@ class OracleSimulation:
     ov = od.overflow
     for bit in range(3):
       self._events[bit] += (ov >> bit) & 1
+      self.engine_counters[w, 2 + bit] += (ov >> bit) & 1
+    self.engine_counters[w, 0], self.engine_counters[w, 1] = od.ncon, od.nefc
 
   def _run(self, mask, fn) -> None:
     for w in range(self.num_envs):

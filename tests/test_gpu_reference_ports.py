@@ -54,13 +54,15 @@ def _matches_oracle(sim):
   cs = np.zeros(m.nsensordata, bool)
   for ty, a, dm in zip(m.sensor_type, m.sensor_adr, m.sensor_dim):
     cs[a:a + dm] |= int(ty) == SENS_CONTACT
-  counters = sim.engine_counters.cpu().numpy()
+  counters = None
   for w in range(sim.num_envs):
     ref = ol.forward(m, q[w], v[w], ws[w], c[w], float(t[w]), nconmax=sim.nconmax, njmax=sim.njmax)
     if ref["overflow"] & 3:
       # the test's own njmax (the reference's 20 rows) is too small for this state: both
       # drop work -- the oracle single rows, the engine whole contacts -- so only the event
       # is compared
+      if counters is None:
+        counters = sim.engine_counters.cpu().numpy()
       assert counters[w, 2] + counters[w, 3] > 0, f"world {w}: the oracle overflows, the engine does not"
       continue
     assert int(ncon[w]) == ref["ncon"], f"world {w}: ncon {int(ncon[w])} vs oracle {ref['ncon']}"
