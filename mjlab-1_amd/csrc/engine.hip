@@ -422,7 +422,6 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       } else if (nc > 0) {
         hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, st, dev, w0, w1,
                            k, mask);
-        if ((e = fork_ovf()) != hipSuccess) return e;
         // Newton by row class, concurrently: the full-capacity class (few worlds, long
         // per-world latency) first on a side stream so its blocks dispatch first, the middle
         // classes on further side streams, the smallest (most worlds) on the launch stream.
@@ -453,6 +452,12 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           e = hipStreamWaitEvent(side->stream[k][c], side->fork[k], 0);
           if (e != hipSuccess) return e;
           class_chain(side->stream[k][c], cls);
+          // the re-solve chain behind the full-capacity class (its stream ends well before the
+          // bulk class's), not on a stream of its own: a further concurrent branch crashed
+          // graph replay under torch's HIP runtime (two middle classes + the re-solve stream)
+          if (c == 0 && ovf)
+            ovf_chain(host, dev, *hbig, dbig, side->stream[k][0], k, w0, w1, sub, nsubstep,
+                      integrate, piped);
         }
         class_chain(st, 1);
         for (int c = 0; c < nc; c++) {
@@ -460,10 +465,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[k][c], 0);
           if (e != hipSuccess) return e;
         }
-        if (piped) {
-          if ((e = join_ovf()) != hipSuccess) return e;
-          continue;
-        }
+        if (piped) continue;
       } else {
         if ((e = fork_ovf()) != hipSuccess) return e;
         hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
@@ -471,7 +473,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       }
       hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), st, dev, w0, w1, k, last,
                          integrate, mask);
-      if ((e = join_ovf()) != hipSuccess) return e;
+      if (nc == 0 && (e = join_ovf()) != hipSuccess) return e;
     }
   }
   for (int k = 1; k < nsplit; k++) {

@@ -111,7 +111,7 @@ def csv_to_npz(input_file: str, output_file: str | None = None, input_fps: float
   T = motion.output_frames
   m = load_scene(scene_name)
   sim = Simulation(T, SimulationCfg(mujoco=MujocoCfg(timestep=1.0 / output_fps)), m, device)
-  scene = Scene(m, T, device, {"robot": {}}, {}, 0.0)
+  scene = Scene.for_model(m, T, device)
   scene.initialize(m, sim.model, sim.data)
   robot = scene["robot"]
   rd = robot.data

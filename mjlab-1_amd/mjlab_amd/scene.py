@@ -717,6 +717,25 @@ class Scene:
         self._sensor_cfgs[sc.name] = sc
     self._model = None
 
+  @classmethod
+  def for_model(cls, mj_model, num_envs: int, device: str, entities: dict | None = None):
+    """Runtime views over an already compiled model, without a SceneCfg: `entities` maps
+    entity names to their soft joint-limit factor ({"robot": 0.9} by default).  The motion
+    tools (`tracking.synthesize_motion`, `motion_csv.csv_to_npz`) record frames through
+    the engine this way, as the reference's `csv_to_npz` builds a bare scene."""
+    from types import SimpleNamespace
+    from .entity import EntityArticulationInfoCfg, EntityCfg
+    self = cls.__new__(cls)
+    self._cfg = SceneCfg(num_envs=num_envs)
+    self.num_envs, self.device = int(num_envs), device
+    self._builds = {n: SimpleNamespace(cfg=EntityCfg(articulation=EntityArticulationInfoCfg(
+        soft_joint_pos_limit_factor=f))) for n, f in (entities or {"robot": 0.9}).items()}
+    self._terrain_geoms = self._terrain_origins = self._terrain_size = None
+    self._terrain_kind = "none"
+    self._sensor_cfgs, self._contact_specs = {}, []
+    self._model = mj_model
+    return self
+
   def compile(self):
     """`MjSpec.compile()` of the assembled scene (scene/scene.py:47-48)."""
     from .compiler.model import compile_scene

@@ -75,7 +75,7 @@ def synthesize_motion(scene_name: str = "g1_tracking", device: str = "cuda:0", T
 
   m = load_scene(scene_name)
   sim = Simulation(T, SimulationCfg(), m, device)
-  scene = Scene(m, T, device, {"robot": {}}, {}, 0.0)
+  scene = Scene.for_model(m, T, device)
   scene.initialize(m, sim.model, sim.data)
   robot = scene["robot"]
   rd = robot.data

@@ -62,6 +62,7 @@ def _assert_clean(env, stats):
   assert stats["checked"] >= 0.95 * 4 * NSTEPS, stats
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
   assert len(stats["out_of_model"]) <= 0.02 * stats["checked"] + 1e-9
+  assert len(stats.get("qvel_outliers", [])) <= 0.01 * stats["checked"] + 1, stats["qvel_outliers"]
 
 
 def test_config1_eager_every_substep(gpu_device):

@@ -34,7 +34,7 @@ Checks per shadowed substep (fp32 engine vs fp64 oracle):
   - the integration: the oracle's step from the engine's own qacc, qfrc_constraint and
     qfrc_smooth (oracle_lib.step_given_qacc) against the engine's next state -- qvel per dof
     within QVEL_FLOOR + QVEL_EPS_MUL * eps32 * (v_i + |qvel_i|), v_i the fp32 error scale of
-    the implicitfast update; qpos within QPOS_ABS + 4 fp32 ulps of the coordinate + h * that;
+    the implicitfast update (at most 1 % of the world-steps, plus one, up to 4x that); qpos within QPOS_ABS + 4 fp32 ulps of the coordinate + h * that;
   - sensordata within SENS_ABS + SENS_REL |s| (worlds inside the solver model): contact-
     sensor entries, sums of constraint forces (the solver's dual variables, sensitive where
     qacc is not), against the oracle's own step with SENS_FORCE_REL x the world's largest
@@ -82,6 +82,7 @@ QACC_ENERGY_REL = 1e-2
 FP32_EPS = float(np.finfo(np.float32).eps)
 QACC_FLOOR, QACC_EPS_MUL = 1e-4, 1024.0
 QVEL_FLOOR, QVEL_EPS_MUL = 1e-6, 24.0
+QVEL_OUTLIER_MUL, OUTLIER_FRACTION = 4.0, 0.01
 OUT_OF_MODEL_FRACTION = 0.02
 COST_GAP_REL = 1e-4
 QPOS_ABS = 1e-6
@@ -236,7 +237,13 @@ def _check_step(m, ref, st0, st1, out, i, stats, where, sim):
       qfrc_smooth_err=float(np.abs(out["qfrc_smooth"][i] - (fs_o["qacc_smooth"] @ fs_o["qM"].T)).max()),
       act_force_err=float(np.abs(out["actuator_force"][i] - fs_o["actuator_force"]).max()),
       qvel_in=float(st0["qvel"][i][j]), dv=float(itg["qvel"][j] - st0["qvel"][i][j])))
-  _expect((ev <= vb).all(), f"{where}: qvel err {ev.max():.3e} (dof {int(np.argmax(ev / vb))}, "
+  # a world-step may exceed the fp32 model by up to QVEL_OUTLIER_MUL (counted; each test
+  # caps their share at OUTLIER_FRACTION); past that it fails
+  ok = (ev <= vb).all()
+  if not ok and (ev <= QVEL_OUTLIER_MUL * vb).all():
+    stats.setdefault("qvel_outliers", []).append((where, float((ev / vb).max())))
+    ok = True
+  _expect(ok, f"{where}: qvel err {ev.max():.3e} (dof {int(np.argmax(ev / vb))}, "
           f"ncon {ncon}, nefc {nefc}; {stats.get('qvel_detail', [None])[-1]})", stats)
   ep = np.abs(st1["qpos"][i] - itg["qpos"])
   pb = QPOS_ABS + QPOS_ULPS * np.abs(itg["qpos"]) + m.timestep * vb.max()
@@ -382,3 +389,4 @@ def test_rollout_shadow_parity(task, num_envs, gpu_device):
     assert stats["heavy_checked"] > 0, "no world above the 60-row class was compared"
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
   assert len(stats["out_of_model"]) <= OUT_OF_MODEL_FRACTION * stats["checked"] + 1e-9 or SOFT
+  assert len(stats.get("qvel_outliers", [])) <= OUTLIER_FRACTION * stats["checked"] + 1, stats["qvel_outliers"]

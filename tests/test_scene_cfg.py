@@ -74,3 +74,23 @@ def test_scene_cfg_edits_reach_the_model():
   # the mass change reaches the engine's constants (subtree mass, invweight)
   pel = base.names["body"].index("robot/pelvis")
   assert m.body_subtreemass[pel] == pytest.approx(base.body_subtreemass[pel] + 2.5)
+
+
+def test_scene_for_model_binds_the_robot():
+  """`Scene.for_model`: runtime views over a compiled model without a cfg (the motion
+  tools), soft joint limits at the given factor."""
+  from oracle_sim import OracleSimulation
+  from mjlab_amd.scene import Scene
+  from mjlab_amd.scenes import load_scene
+  from mjlab_amd.sim import SimulationCfg
+  m = load_scene("g1_tracking")
+  sim = OracleSimulation(3, SimulationCfg(), m, "cpu")
+  scene = Scene.for_model(m, 3, "cpu")
+  scene.initialize(m, sim.model, sim.data)
+  robot = scene["robot"]
+  assert robot.num_joints == 29
+  lim = robot.data.soft_joint_pos_limits[0].numpy()
+  rng = np.asarray(m.jnt_range)[1:]
+  mid, half = rng.mean(axis=1), 0.5 * (rng[:, 1] - rng[:, 0])
+  np.testing.assert_allclose(lim[:, 1] - lim[:, 0], 2 * 0.9 * half, rtol=1e-5)
+  np.testing.assert_allclose(lim.mean(axis=1), mid, atol=1e-5)
