@@ -142,9 +142,16 @@ def test_config1_captured_every_substep(gpu_device):
       assert torch.equal(d.qpos, s1["qpos"]), f"step {k}: graph physics != single steps (qpos)"
       assert torch.equal(d.qacc_warmstart, s1["qacc_warmstart"]), f"step {k}: qacc_warmstart"
       assert torch.equal(d.time, s1["time"]), f"step {k}: time"
-      assert torch.equal(d.qvel[:, 2:], s1["qvel"][:, 2:]), f"step {k}: qvel"
       same_xy = torch.equal(d.qvel[:, :2], s1["qvel"][:, :2])
       pushed += int(not same_xy)
+      if same_xy:
+        assert torch.equal(d.qvel[:, 2:], s1["qvel"][:, 2:]), f"step {k}: qvel"
+      else:
+        # a push (push_by_setting_velocity) rewrites the whole root twist: x / y get the
+        # kick, the rest goes through the world <-> body-frame round trip of the reference's
+        # write_root_velocity_to_sim, so it matches to rounding, not bit for bit
+        torch.testing.assert_close(d.qvel[:, 2:], s1["qvel"][:, 2:], rtol=1e-6, atol=1e-6,
+                                   msg=f"step {k}: qvel after a push")
       for n in ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time"):
         assert torch.equal(air[n], a1[n]), f"step {k}: engine air time {n}"
     # continue the graph's trajectory (post-physics events and resets included)
