@@ -186,7 +186,7 @@ struct Params {
 // piped C / next-A launches of a class), kSelOvf: the world is the blockIdx-th entry of the
 // overflow list of parity kSelRPar, kSelAPar: the parity of the substep phase A computes
 // (the list it appends overflowing worlds to).
-constexpr int kOvfGrid = 256;  // workgroups of a re-solve launch (each loops over listed worlds)
+constexpr int kOvfGrid = 64;  // workgroups of a re-solve launch (each loops over listed worlds)
 constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;

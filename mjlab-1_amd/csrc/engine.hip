@@ -310,7 +310,13 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
                       bool next_a) {
   const int last = sub == nsubstep - 1;
   const int par = sub & 1;
-  const int g = std::min(hbig.ovf_cap, kOvfGrid);
+  // the grid: every re-solve launch of an empty list still dispatches it (measured on G1,
+  // nothing listed: 256 workgroups -1.0 %); MJX355_OVF_GRID overrides
+  static const int grid = [] {
+    const char* e = getenv("MJX355_OVF_GRID");
+    return e && atoi(e) > 0 ? atoi(e) : kOvfGrid;
+  }();
+  const int g = std::min(hbig.ovf_cap, grid);
   const int sel = k | kSelOvf | (par ? kSelRPar : 0);
   hipLaunchKernelGGL(step_fn(hbig, 4), dim3(g), dim3(kWave), lds_bytes(hbig, 0), cs, dbig, w0, w1,
                      sel, last, integrate, nullptr);
@@ -356,13 +362,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
     const char* e = getenv("MJX355_CLASS_PIPE");
     return !e || atoi(e) != 0;
   }();
-  // a class pipeline's C and next A as one launch (step_ca); MJX355_FUSE_CA=0/1
-  static const bool fuse_ca = [] {
-    const char* e = getenv("MJX355_FUSE_CA");
-    return e && atoi(e) != 0;
-  }();
-  const StepFn fCA = step_fn(host, 7);
-  const size_t lds_ca = std::max(lds_bytes(host, 0), lds_bytes(host, 2));
+
   if (nsplit > 1 && nc > 0) {
     // (diagnostic topology; the overflow re-solve is not wired into it)
     if (ovf) return hipErrorNotSupported;
@@ -434,12 +434,6 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           hipLaunchKernelGGL(cls ? fB : fBL, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
                              cs, dev, w0, w1, k, last, cls, mask);
           if (!piped) return;
-          if (fuse_ca && !last) {
-            hipLaunchKernelGGL(fCA, dim3(n), dim3(kWave), lds_ca, cs, dev, w0, w1,
-                               k | (cls + 1) << 8 | (((sub + 1) & 1) ? kSelAPar : 0),
-                               sub + 1 == nsubstep - 1, integrate, mask);
-            return;
-          }
           hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
                              k | (cls + 1) << 8, last, integrate, mask);
           if (!last)

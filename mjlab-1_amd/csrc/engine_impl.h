@@ -29,7 +29,7 @@
 
 // FMA contraction only within one expression (the front end's fmuladd), never across
 // statements in the back end: one source line then rounds the same in every kernel it is
-// inlined into (step_phase, the re-solve's step_ovf, step_ca), so a world's substep is bit
+// inlined into (step_phase, the re-solve's step_ovf), so a world's substep is bit
 // for bit the same whichever launch set ran it.
 #pragma clang fp contract(on)
 
@@ -3609,25 +3609,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
   }
 }
 
-// Phase C of substep s fused with phase A of substep s + 1 for the same world (a class
-// pipeline's C -> next A, MJX355_FUSE_CA): one launch and one launch tail fewer per class
-// and substep.  C of a non-last substep (`last` is A's); the state C stores is read back
-// by A from HBM after an agent-scope fence (the vector L1 holds C's input lines).
-template <int NR, int SP>
-__global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_ca(const Params* __restrict__ P, int w0,
-                                                                int w1, int sel, int last, int integrate,
-                                                                const uint8_t* __restrict__ mask) {
-  extern __shared__ __attribute__((aligned(16))) float S[];
-  step_body<NR, 2, SP, false>(S, P, w0, w1, sel, 0, integrate, mask, (int)blockIdx.x);
-  __threadfence();
-  __syncthreads();
-  step_body<NR, 0, SP, false>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
-}
-
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 
 // kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4 / 5 / 6: A / B latency / C
-// of the overflow re-solve; 7: C fused with the next substep's A
+// of the overflow re-solve
 template <int NR, int SP>
 StepFn phase_kernel(int ph) {
   constexpr int role = SpecRole<SP>::mask;
@@ -3646,8 +3631,7 @@ StepFn phase_kernel(int ph) {
       if constexpr ((role & 2) != 0) return step_ovf<NR, 2, SP, false>;
       else return nullptr;
     default:
-      if constexpr ((role & 1) != 0) return step_ca<NR, SP>;
-      else return nullptr;
+      return nullptr;
   }
 }
 
