@@ -335,7 +335,12 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side, const Params* hbig, const Params* dbig) {
   if (nworld <= 0) return hipSuccess;
-  if (mask && hbig) {
+  // MJX355_MASKED_BIG=0: the masked forward in the fast carve, with no re-solve (A/B)
+  static const bool masked_big = [] {
+    const char* e = getenv("MJX355_MASKED_BIG");
+    return !e || atoi(e) != 0;
+  }();
+  if (mask && hbig && masked_big) {
     // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve
     const StepFn fA = step_fn(*hbig, 0), fBL = step_fn(*hbig, 3), fC = step_fn(*hbig, 2);
     hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(*hbig, 0), stream, dbig, 0, nworld, 0,
@@ -419,6 +424,8 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         // masked worlds -- no classify launch, no fork/join latency on this short critical path
         hipLaunchKernelGGL(fBL, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k,
                            last, -1, mask);
+        // (MJX355_MASKED_BIG=0) masked worlds past the fast carve: re-solved in line
+        if (ovf) ovf_chain(host, dev, *hbig, dbig, st, k, w0, w1, sub, nsubstep, integrate, false);
       } else if (nc > 0) {
         hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, st, dev, w0, w1,
                            k, mask);

@@ -1656,7 +1656,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   if (mask && !mask[w]) return;  // masked forward: only the selected worlds
   // a world listed for the overflow re-solve this substep skips this carve's B and C (the
   // class lists already leave it out; the all-world launches check)
-  if (PH != 0 && P->ovf_resolve && !(sel & kSelOvf) && P->ovf_flag[w]) return;
+  // (list-driven launches -- a Newton row class, a class pipeline's C -- never see them:
+  // classify_kernel left them out, and their one extra dependent load stays off the chain)
+  if (PH != 0 && P->ovf_resolve && !(sel & kSelOvf) && !cls1 &&
+      !(PH == 1 && P->nrowclass > 0 && integrate >= 0) && P->ovf_flag[w])
+    return;
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
   float* gc = gw + P->gC;
   float* gf = gw + P->gF;  // implicit-integration factor (phase A writes, phase C reads)
