@@ -122,7 +122,8 @@ struct mjxSim_ {
   int spec_big = 0;
   int gC_big = 0, gF_big = 0, gstride_big = 0;
   float* gscr_big = nullptr;
-  int* ovf = nullptr;  // [kMaxSplit][2][ovf_cap] lists, [kMaxSplit][2] counts, [nworld] flags
+  int* ovf = nullptr;  // [kMaxSplit][2][ovf_cap] lists, [kMaxSplit][2] counts, [nworld] flags,
+                       // [kMaxSplit][2] done counters
   int ovf_cap = 0;
   int con_stride = 0;  // contact slots per world in the contact output arrays
   mjx::Params* dparams_big = nullptr;
@@ -162,6 +163,7 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.ovf_list = s->ovf;
   p.ovf_n = s->ovf ? s->ovf + (size_t)mjx::kMaxSplit * 2 * s->ovf_cap : nullptr;
   p.ovf_flag = s->ovf ? p.ovf_n + mjx::kMaxSplit * 2 : nullptr;
+  p.ovf_done = s->ovf ? p.ovf_flag + s->nworld : nullptr;
   p.con_stride = s->con_stride;
   return p;
 }
@@ -629,7 +631,7 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
     const size_t gb = sizeof(float) * (size_t)nworld * s->gstride_big;
     e = hipMalloc((void**)&s->gscr_big, gb);
     if (e == hipSuccess) e = hipMemset(s->gscr_big, 0, gb);
-    const size_t ob = sizeof(int) * ((size_t)mjx::kMaxSplit * 2 * (s->ovf_cap + 1) + nworld);
+    const size_t ob = sizeof(int) * ((size_t)mjx::kMaxSplit * 2 * (s->ovf_cap + 2) + nworld);
     if (e == hipSuccess) e = hipMalloc((void**)&s->ovf, ob);
     if (e == hipSuccess) e = hipMemset(s->ovf, 0, ob);
     if (e == hipSuccess) e = hipMalloc((void**)&s->dparams_big, sizeof(mjx::Params));

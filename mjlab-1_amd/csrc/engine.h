@@ -179,6 +179,7 @@ struct Params {
   int* ovf_list;   // [kMaxSplit][2][ovf_cap]
   int* ovf_n;      // [kMaxSplit][2]
   int* ovf_flag;   // [nworld]
+  int* ovf_done;   // [kMaxSplit][2] workgroups through the list's last launch (it clears the list)
   int con_stride;  // contact slots per world of the contact output arrays (the max capacity)
 };
 
@@ -190,6 +191,7 @@ constexpr int kOvfGrid = 64;  // workgroups of a re-solve launch (each loops ove
 constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;
+constexpr int kSelClr = 1 << 19;  // the re-solve launch that empties its list on exit
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.

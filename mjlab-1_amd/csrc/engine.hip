@@ -110,11 +110,6 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
       P->wl_list[w0 + atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1)] = w;
 }
 
-// The overflow list of one split and substep parity is emptied by the last launch of the
-// re-solve chain that consumed it (before the substep two ahead, or the next step call,
-// appends to it again).
-__global__ void ovf_clear_kernel(int* n) { *n = 0; }
-
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
 template <int NR>
 static StepFn phase_fn_nr(int ph) {
@@ -202,14 +197,19 @@ static size_t lds_bytes(const Params& host, int ph) {
   return (size_t)host.LP[ph].total * 4 + (size_t)(p > 0 ? p : 0);
 }
 
+// dynamic LDS of step_resolve: the largest of the three phase carves
+static size_t lds_resolve(const Params& host) {
+  return std::max(lds_bytes(host, 0), std::max(lds_bytes(host, 1), lds_bytes(host, 2)));
+}
+
 hipError_t prepare_step(const Params& host) {
   size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
   for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
-  for (int ph = 0; ph < 7; ph++) {  // phase codes of phase_kernel: 3 and 5 are phase B
-    const int c = ph == 3 || ph == 5 ? 1 : ph == 4 ? 0 : ph == 6 ? 2 : ph;
-    if (shmem[c] > 64 * 1024) {
+  for (int ph = 0; ph < 6; ph++) {  // phase codes of phase_kernel
+    const size_t need = ph == 5 ? lds_resolve(host) : shmem[ph == 3 ? 1 : ph == 4 ? 0 : ph];
+    if (need > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)step_fn(host, ph),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem[c]);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)need);
       if (e != hipSuccess) return e;
     }
   }
@@ -300,11 +300,11 @@ static hipError_t launch_split_classes(const Params& host, const Params* dev, in
   return hipGetLastError();
 }
 
-// Overflow re-solve chain of split k at substep `sub` (parity sub & 1), on the split's
-// re-solve stream: the listed worlds' substep at full capacity (max A, latency Newton, C),
-// then -- when the class pipelines carry the next substep's phase A -- that phase A in the
-// normal carve, and the list is emptied.  The grid is fixed (kOvfGrid workgroups, each
-// looping over listed worlds); workgroups past the listed count exit at once.
+// Overflow re-solve chain of split k at substep `sub` (parity sub & 1): the listed worlds'
+// substep at full capacity (step_resolve: max A, latency Newton, C), then -- when the class
+// pipelines carry the next substep's phase A -- that phase A in the normal carve; the last
+// of them empties the list on exit.  The grid is fixed (kOvfGrid workgroups, each looping
+// over listed worlds); workgroups past the listed count exit at once.
 static void ovf_chain(const Params& host, const Params* dev, const Params& hbig, const Params* dbig,
                       hipStream_t cs, int k, int w0, int w1, int sub, int nsubstep, int integrate,
                       bool next_a) {
@@ -318,17 +318,13 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
   }();
   const int g = std::min(hbig.ovf_cap, grid);
   const int sel = k | kSelOvf | (par ? kSelRPar : 0);
-  hipLaunchKernelGGL(step_fn(hbig, 4), dim3(g), dim3(kWave), lds_bytes(hbig, 0), cs, dbig, w0, w1,
-                     sel, last, integrate, nullptr);
-  hipLaunchKernelGGL(step_fn(hbig, 5), dim3(g), dim3(kWave), lds_bytes(hbig, 1), cs, dbig, w0, w1,
-                     sel, last, -1, nullptr);
-  hipLaunchKernelGGL(step_fn(hbig, 6), dim3(g), dim3(kWave), lds_bytes(hbig, 2), cs, dbig, w0, w1,
-                     sel, last, integrate, nullptr);
-  if (next_a && !last)
+  const bool next = next_a && !last;
+  hipLaunchKernelGGL(step_fn(hbig, 5), dim3(g), dim3(kWave), lds_resolve(hbig), cs, dbig, w0, w1,
+                     sel | (next ? 0 : kSelClr), last, integrate, nullptr);
+  if (next)
     hipLaunchKernelGGL(step_fn(host, 4), dim3(g), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
-                       sel | ((sub + 1) & 1 ? kSelAPar : 0), sub + 1 == nsubstep - 1, integrate,
-                       nullptr);
-  hipLaunchKernelGGL(ovf_clear_kernel, dim3(1), dim3(1), 0, cs, host.ovf_n + 2 * k + par);
+                       sel | kSelClr | ((sub + 1) & 1 ? kSelAPar : 0), sub + 1 == nsubstep - 1,
+                       integrate, nullptr);
 }
 
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,

@@ -3602,6 +3602,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
 // workgroups, each looping over the listed worlds.  A separate entry, so that the loop's
 // live ranges stay out of the bulk kernels (inlined into step_phase the loop cost phase A 74
 // VGPRs and phase C 64); its few worlds need no residency.
+// The launch flagged kSelClr is the list's last reader: its last workgroup out empties the
+// list (count and done counter) for the substep after next -- no launch of its own.
+__device__ __forceinline__ void ovf_clear_on_exit(const Params* __restrict__ P, int sel) {
+  if (!(sel & kSelClr)) return;
+  const int li = 2 * (sel & 0xff) + ((sel & kSelRPar) ? 1 : 0);
+  if (threadIdx.x == 0) {
+    __threadfence();  // this workgroup's reads of the list precede the count
+    if (atomicAdd(P->ovf_done + li, 1) == (int)gridDim.x - 1) {
+      P->ovf_n[li] = 0;
+      P->ovf_done[li] = 0;
+    }
+  }
+}
+
 template <int NR, int PH, int SP, bool LAT>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_ovf(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
@@ -3611,12 +3625,35 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
     step_body<NR, PH, SP, LAT>(S, P, w0, w1, sel, last, integrate, mask, bid);
     if (!ovf_more(P, sel, bid + (int)gridDim.x)) break;
   }
+  ovf_clear_on_exit(P, sel);
+}
+
+// The re-solve of a listed world's whole substep in the max carve as ONE launch (phase A,
+// the latency Newton kernel, phase C back to back per world, hand-offs through the max
+// scratch): an empty list then costs one near-empty launch per substep instead of three.
+// LDS: the largest of the three carves.
+template <int NR, int SP>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void step_resolve(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  for (int bid = (int)blockIdx.x;; bid += (int)gridDim.x) {
+    step_body<NR, 0, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
+    __threadfence();  // the packs this wave stored are read back by the next phase
+    __syncthreads();
+    step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, -1, mask, bid);
+    __threadfence();
+    __syncthreads();
+    step_body<NR, 2, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
+    if (!ovf_more(P, sel, bid + (int)gridDim.x)) break;
+  }
+  ovf_clear_on_exit(P, sel);
 }
 
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 
-// kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4 / 5 / 6: A / B latency / C
-// of the overflow re-solve
+// kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4: phase A over a re-solve list
+// (the fast carve's next substep), 5: a listed world's whole substep (step_resolve)
 template <int NR, int SP>
 StepFn phase_kernel(int ph) {
   constexpr int role = SpecRole<SP>::mask;
@@ -3624,15 +3661,14 @@ StepFn phase_kernel(int ph) {
     case 0: return step_phase<NR, 0, SP>;
     case 2: return step_phase<NR, 2, SP>;
     case 3: return step_newton_lat<NR, SP>;
-    case 4: return step_ovf<NR, 0, SP, false>;
+    case 4:
+      if constexpr ((role & 1) != 0) return step_ovf<NR, 0, SP, false>;
+      else return nullptr;
     case 1:
       if constexpr ((role & 1) != 0) return step_phase<NR, 1, SP>;
       else return nullptr;
     case 5:
-      if constexpr ((role & 2) != 0) return step_ovf<NR, 1, SP, true>;
-      else return nullptr;
-    case 6:
-      if constexpr ((role & 2) != 0) return step_ovf<NR, 2, SP, false>;
+      if constexpr ((role & 2) != 0) return step_resolve<NR, SP>;
       else return nullptr;
     default:
       return nullptr;
