@@ -448,13 +448,15 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           const int cls = c == 0 ? 0 : nc + 1 - c;  // 0, then nc, nc-1, ..., 2
           e = hipStreamWaitEvent(side->stream[k][c], side->fork[k], 0);
           if (e != hipSuccess) return e;
-          class_chain(side->stream[k][c], cls);
-          // the re-solve chain behind the full-capacity class (its stream ends well before the
+          // the re-solve chain on the full-capacity class's stream (which ends well before the
           // bulk class's), not on a stream of its own: a further concurrent branch crashed
-          // graph replay under torch's HIP runtime (two middle classes + the re-solve stream)
+          // graph replay under torch's HIP runtime (two middle classes + the re-solve stream).
+          // Ahead of that class, right after classify, while LDS is still free for its
+          // 64 KiB workgroups: behind it, the empty launches waited for the bulk to drain
           if (c == 0 && ovf)
             ovf_chain(host, dev, *hbig, dbig, side->stream[k][0], k, w0, w1, sub, nsubstep,
                       integrate, piped);
+          class_chain(side->stream[k][c], cls);
         }
         class_chain(st, 1);
         for (int c = 0; c < nc; c++) {
