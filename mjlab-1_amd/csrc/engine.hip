@@ -53,11 +53,12 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
   for (int i = t; i < nb; i += kClassifyThreads) bin[i] = 0;
   __syncthreads();
   const int* nefc = P->D.nefc;
-  // worlds listed for the overflow re-solve this substep are not classed (the max launch set
-  // solves them)
-  const int* oflag = P->ovf_resolve ? P->ovf_flag : nullptr;
-  for (int w = w0 + t; w < w1; w += kClassifyThreads)
-    if ((!mask || mask[w]) && !(oflag && oflag[w])) atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1);
+  // worlds listed for the overflow re-solve this substep (phase A left nefc = -1) are not
+  // classed: the max launch set solves them
+  for (int w = w0 + t; w < w1; w += kClassifyThreads) {
+    const int r = nefc[w];
+    if ((!mask || mask[w]) && r >= 0) atomicAdd(&bin[min(r, nb - 1)], 1);
+  }
   __syncthreads();
   // exclusive scan of the bins in descending row count: bin[r] <- #listed worlds with more
   // than r rows.  Thread t owns a contiguous chunk of the reversed bin order.
@@ -105,9 +106,10 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
     seg[2 * t + 1] = max(s1 - s0, 0);
   }
   __syncthreads();  // the segments read the bins before the scatter advances them
-  for (int w = w0 + t; w < w1; w += kClassifyThreads)
-    if ((!mask || mask[w]) && !(oflag && oflag[w]))
-      P->wl_list[w0 + atomicAdd(&bin[min(max(nefc[w], 0), nb - 1)], 1)] = w;
+  for (int w = w0 + t; w < w1; w += kClassifyThreads) {
+    const int r = nefc[w];
+    if ((!mask || mask[w]) && r >= 0) P->wl_list[w0 + atomicAdd(&bin[min(r, nb - 1)], 1)] = w;
+  }
 }
 
 // Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
@@ -448,15 +450,15 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           const int cls = c == 0 ? 0 : nc + 1 - c;  // 0, then nc, nc-1, ..., 2
           e = hipStreamWaitEvent(side->stream[k][c], side->fork[k], 0);
           if (e != hipSuccess) return e;
-          // the re-solve chain on the full-capacity class's stream (which ends well before the
+          class_chain(side->stream[k][c], cls);
+          // the re-solve chain behind the full-capacity class (its stream ends well before the
           // bulk class's), not on a stream of its own: a further concurrent branch crashed
           // graph replay under torch's HIP runtime (two middle classes + the re-solve stream).
-          // Ahead of that class, right after classify, while LDS is still free for its
-          // 64 KiB workgroups: behind it, the empty launches waited for the bulk to drain
+          // Measured ahead of that class instead: G1 -3 % (its 64 KiB workgroups then take
+          // LDS from the bulk class's first Newton waves)
           if (c == 0 && ovf)
             ovf_chain(host, dev, *hbig, dbig, side->stream[k][0], k, w0, w1, sub, nsubstep,
                       integrate, piped);
-          class_chain(side->stream[k][c], cls);
         }
         class_chain(st, 1);
         for (int c = 0; c < nc; c++) {

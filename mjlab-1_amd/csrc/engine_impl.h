@@ -2586,7 +2586,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         }
         slot = __shfl(slot, 0);
         const bool listed = over && slot < P->ovf_cap;
-        if (lane == 0) P->ovf_flag[w] = listed ? 1 : 0;
+        if (lane == 0) {
+          P->ovf_flag[w] = listed ? 1 : 0;
+          if (listed) D.nefc[w] = -1;  // classify_kernel leaves the world out
+        }
         if (listed) return;
       }
       if (nefc > d.njmax) {
