@@ -125,7 +125,7 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
  * truncated (the reference's budget semantics: its nconmax is pooled, sim/sim.py:82-92; its
  * njmax, 300 rows for the velocity tasks, bounds each world).  Only what overflows the max
  * capacity is dropped (counted by mjx_sim_stats).  The contact output arrays hold
- * nconmax_max slots per world; a masked forward runs at the max capacity throughout.  A batch
+ * nconmax_max slots per world; a masked forward re-solves its overflowing worlds too.  A batch
  * the engine splits into concurrent halves (large batches of models without Newton row
  * classes) gets no re-solve: its max capacity is the fast carve (mjx_sim_info reports the
  * capacity wired). */

@@ -637,6 +637,35 @@ __device__ __forceinline__ void rows_load_factor_ltr(float (&A)[NR], float& rd, 
     A[k] = k < ln ? A[k] * (s * ljj) : 0.f;
   }
 }
+// rows_load_factor_ltr in two halves: the loads (issued early -- phase C puts them in flight
+// with its pack's LDS-DMA, so the factor's latency overlaps the pack's) and the scaling.
+template <int NR>
+__device__ __forceinline__ void rows_load_factor_ltr_raw(float (&A)[NR], float& dv, const float* Lp,
+                                                         int nvp, int lane) {
+  const int ln = opaque_lane(lane);
+  const int row = ln < nvp ? ln : 0;
+  const float* rp = Lp + ltr_off(row);
+  const int len = 4 * ((row >> 2) + 1);
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    const float4 v = ld4(rp + (c < len ? c : 0));
+    const bool in = c < len;
+    A[c] = in ? v.x : 0.f; A[c + 1] = in ? v.y : 0.f; A[c + 2] = in ? v.z : 0.f; A[c + 3] = in ? v.w : 0.f;
+  }
+  dv = rp[row];
+}
+template <int NR>
+__device__ __forceinline__ void rows_scale_factor_ltr(float (&A)[NR], float& rd, float dv, int nvp,
+                                                      int lane) {
+  const int ln = opaque_lane(lane);
+  rd = ln < nvp ? dv : 1.f;
+  const float ljj = __builtin_amdgcn_rcpf(rd);
+#pragma unroll
+  for (int k = 0; k < NR; k++) {
+    const float s = rl(rd, k);
+    A[k] = k < ln ? A[k] * (s * ljj) : 0.f;
+  }
+}
 template <int NR>
 __device__ __forceinline__ float rows_solve_ltr(const float (&M)[NR], float rdiag, const float* Lp,
                                                 float x, int nvp, int lane) {
@@ -3310,6 +3339,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   } else {
     // ----------------------------------------------------------- phase C
     cp_pack(S, gc, L.pack_len, lane);  // C pack: carve offsets == pack offsets
+    // the implicit-integration factor (phase A stored it): in flight with the pack
+    float Fa[NR], Fdv = 1.f;
+    if (integrate) rows_load_factor_ltr_raw<NR>(Fa, Fdv, gf, nvp, lane);
     for (int i = lane; i < nvp; i += kWave) {
       const bool in = i < nv;
       S[L.qvel + i] = in ? D.qvel[(size_t)w * nv + i] : 0.f;
@@ -3502,12 +3534,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       // the world's scratch (rows and columns come straight from global memory)
       SUBSTAMP(10);
       {
-        float A[NR], rd;
-        rows_load_factor_ltr<NR>(A, rd, gf, nvp, lane);
+        float rd;
+        rows_scale_factor_ltr<NR>(Fa, rd, Fdv, nvp, lane);
         // a tree-form factor (phase A) is of the reversed matrix: lane i solves for dof nvp-1-i
         const int pl = kTree<SP> ? nvp - 1 - lane : lane;
         const float f = lane < nvp ? S[L.qfrc_smooth + pl] + S[L.qfrc_con + pl] : 0.f;
-        const float acc = rows_solve_ltr<NR>(A, rd, gf, f, nvp, lane);
+        const float acc = rows_solve_ltr<NR>(Fa, rd, gf, f, nvp, lane);
         if (lane < nvp && pl < nv) S[L.qvel + pl] += h * acc;
       }
       sync();

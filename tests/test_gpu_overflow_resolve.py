@@ -13,9 +13,9 @@ nothing here.  Two set-ups:
     nothing is dropped;
   - the task's own 48 / 160 carve with worlds placed at pelvis heights that give 40..64
     contacts and 160..256 rows (`_HEIGHTS`, measured on the oracle): the fused and
-    graph-captured multi-substep step (the re-solve chain on its own stream, joined before
-    the next substep's phase A) equals single steps bit for bit, also at the bench batch,
-    and the masked forward matches the oracle's contact counts.
+    graph-captured multi-substep step (the re-solve chain behind the full-capacity Newton
+    class, joined before the next substep's classify) equals single steps bit for bit, also
+    at the bench batch, and the masked forward matches the oracle's contact counts.
 """
 
 from __future__ import annotations
@@ -214,8 +214,8 @@ def test_large_batch_resolve(gpu_device):
 
 
 def test_masked_forward_at_max_capacity(gpu_device):
-  """forward(mask) (the reset path) runs at the max capacity: an overflowing world's
-  contacts and rows match the oracle's forward."""
+  """forward(mask) (the reset path) re-solves its overflowing worlds at the max capacity:
+  their contacts and rows match the oracle's forward."""
   sim, m = _sim(gpu_device)
   _place(sim, m, 3)
   mask = torch.zeros(sim.num_envs, dtype=torch.bool, device=sim.data.qpos.device)
