@@ -299,6 +299,49 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
     m->dm.body_submask = (const uint64_t*)p;
     if (upload(bdof.data(), sizeof(uint64_t) * bdof.size(), &p)) { delete m; return -1; }
     m->dm.body_dofmask = (const uint64_t*)p;
+    // per-lane records (engine.h DModel::body_rec): level-order bodies, dofs, actuators
+    const int nlev = d.nlevel;
+    std::vector<int32_t> brec((size_t)mjx::kBodyRec * (nb > 0 ? nb : 1), 0);
+    for (int i = 0; i < nb; i++) {
+      int32_t* r = brec.data() + (size_t)mjx::kBodyRec * i;
+      const int b = desc->level_body[i];
+      int lv = 0;
+      for (int l = 1; l < nlev; l++) lv = i >= desc->level_start[l] ? l : lv;
+      const int j0 = desc->body_jntadr[b], jn = desc->body_jntnum[b], k = jn > 0 ? j0 : 0;
+      const int c0 = desc->body_childadr[b], cn = desc->body_childadr[b + 1] - c0;
+      int chp = 0;
+      for (int t = 0; t < 5 && t < cn; t++) chp |= desc->body_child[c0 + t] << (6 * t);
+      const int32_t v[16] = {b, desc->body_parentid[b], lv, j0, jn, desc->jnt_type[k], desc->jnt_qposadr[k],
+                             desc->jnt_dofadr[k], desc->body_dofadr[b], desc->body_dofnum[b],
+                             desc->body_mocapid[b], desc->body_rootid[b], c0, cn, chp, 0};
+      for (int t = 0; t < 16; t++) r[t] = v[t];
+      r[16] = (int32_t)(uint32_t)sub[b]; r[17] = (int32_t)(uint32_t)(sub[b] >> 32);
+      r[18] = (int32_t)(uint32_t)bdof[b]; r[19] = (int32_t)(uint32_t)(bdof[b] >> 32);
+    }
+    if (upload(brec.data(), sizeof(int32_t) * brec.size(), &p)) { delete m; return -1; }
+    m->dm.body_rec = (const int32_t*)p;
+    const int nv = d.nv;
+    std::vector<int32_t> drec((size_t)mjx::kDofRec * (nv > 0 ? nv : 1), 0);
+    for (int i = 0; i < nv; i++) {
+      int32_t* r = drec.data() + (size_t)mjx::kDofRec * i;
+      const int j = desc->dof_jntid[i], body = desc->dof_bodyid[i];
+      const int32_t v[8] = {body, desc->jnt_type[j], desc->jnt_qposadr[j], desc->body_parentid[body],
+                            desc->jnt_dofadr[j], desc->body_dofadr[body], j, 0};
+      for (int t = 0; t < 8; t++) r[t] = v[t];
+      r[8] = (int32_t)(uint32_t)anc[i]; r[9] = (int32_t)(uint32_t)(anc[i] >> 32);
+    }
+    if (upload(drec.data(), sizeof(int32_t) * drec.size(), &p)) { delete m; return -1; }
+    m->dm.dof_rec = (const int32_t*)p;
+    const int nu = d.nu;
+    std::vector<int32_t> arec((size_t)mjx::kActRec * (nu > 0 ? nu : 1), 0);
+    for (int u = 0; u < nu; u++) {
+      int32_t* r = arec.data() + (size_t)mjx::kActRec * u;
+      const int j = desc->actuator_trnid[u];
+      r[0] = desc->jnt_dofadr[j]; r[1] = desc->jnt_qposadr[j];
+      r[2] = desc->actuator_ctrllimited[u]; r[3] = desc->actuator_forcelimited[u];
+    }
+    if (upload(arec.data(), sizeof(int32_t) * arec.size(), &p)) { delete m; return -1; }
+    m->dm.act_rec = (const int32_t*)p;
   }
   {
     // Terrain broadphase tables.  The pair list is [regular pairs | terrain pairs], the

@@ -11,6 +11,7 @@
 namespace mjx {
 
 constexpr int kWave = 64;        // CDNA wavefront width
+constexpr int kBodyRec = 20, kDofRec = 12, kActRec = 4;  // ints per DModel record (int4-aligned)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
 constexpr int kMaxLanes = 64;    // nu, njnt: one lane per actuator / joint (register records)
@@ -60,6 +61,13 @@ struct DModel {
   const uint64_t* dof_ancmask;  // bit j set: dof j is dof i itself or an ancestor (host-derived)
   const uint64_t* body_submask;  // bit c set: body c is in body b's subtree (b included)
   const uint64_t* body_dofmask;  // bit j set: dof j moves body b (dofs of b and its ancestors)
+  // per-lane model records, host-packed (capi.cpp, kBodyRec / kDofRec / kActRec ints each):
+  // the integer part of load_body / the dof record / load_act in one contiguous record, so
+  // a lane's float loads depend on ONE load instead of a chain (level_body -> body_* ->
+  // jnt_* -> qpos0).  body_rec is in level order (record i = level-order body i).
+  const int32_t* body_rec;
+  const int32_t* dof_rec;
+  const int32_t* act_rec;
   // host-derived terrain broadphase tables (capi.cpp).  Static terrain geoms (heightfields,
   // boxes welded to the world) keep no LDS frame: geom_lds = -1, lds_geom its inverse over
   // the others.  st_geom lists the terrain geoms with pairs, in pair-tail order; their pair

@@ -333,14 +333,16 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side, const Params* hbig, const Params* dbig) {
   if (nworld <= 0) return hipSuccess;
-  // The masked forward (a few reset worlds) runs in the fast carve with the re-solve in line
-  // behind it.  MJX355_MASKED_BIG=1: every masked launch in the max carve instead -- its grid
-  // is the whole batch, and at 64 KiB of LDS per workgroup even the unmasked workgroups
-  // dispatch two per CU (jump hfield, 16,384 worlds: -9.6 %)
-  static const bool masked_big = [] {
+  // The masked forward (a few reset worlds): its three launches in the max carve, or in the
+  // fast carve with the re-solve in line behind them.  The max-carve grid is the whole batch,
+  // and at 64 KiB of LDS per workgroup even the unmasked workgroups dispatch two per CU; the
+  // in-line re-solve is a fixed launch on the critical path.  Measured: G1 4,096 worlds max
+  // carve +1.1 %, jump hfield 16,384 worlds fast carve +9.5 %.  MJX355_MASKED_BIG=0/1 forces.
+  static const int masked_big_env = [] {
     const char* e = getenv("MJX355_MASKED_BIG");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : -1;
   }();
+  const bool masked_big = masked_big_env >= 0 ? masked_big_env != 0 : nworld <= 4096;
   if (mask && hbig && masked_big) {
     // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve
     const StepFn fA = step_fn(*hbig, 0), fBL = step_fn(*hbig, 3), fC = step_fn(*hbig, 2);

@@ -1444,28 +1444,28 @@ struct BodyRec {
 struct BodyPtrs {
   const float *pos, *quat, *ipos, *iquat, *mass, *inertia, *jpos, *jaxis, *qpos0;
 };
+__device__ __forceinline__ uint64_t u64_of(int lo, int hi) {
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+// the integer record (DModel::body_rec, level order): one dependent load level, then the
+// body's and its first joint's floats
 __device__ __forceinline__ BodyRec load_body(const DModel& m, const Dims& d, const BodyPtrs& P,
                                              int i) {
+  (void)d;
   BodyRec r;
-  const int b = m.level_body[i];
-  r.b = b;
-  r.lv = 0;
-  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
-  r.p = m.body_parentid[b];
-  r.j0 = m.body_jntadr[b]; r.jn = m.body_jntnum[b];
-  r.d0 = m.body_dofadr[b]; r.dn = m.body_dofnum[b];
-  r.mocap = m.body_mocapid[b];
-  r.root = m.body_rootid[b];
-  r.sub = m.body_submask[b];
-  r.dofs = m.body_dofmask[b];
-  r.c0 = m.body_childadr[b]; r.cn = m.body_childadr[b + 1] - r.c0;
-  r.chp = 0;
-  for (int t = 0; t < 5 && t < r.cn; t++) r.chp |= m.body_child[r.c0 + t] << (6 * t);
+  const int4* rec = reinterpret_cast<const int4*>(m.body_rec + (size_t)kBodyRec * i);
+  const int4 a = rec[0], b4 = rec[1], c4 = rec[2], e4 = rec[3], f4 = rec[4];
+  r.b = a.x; r.p = a.y; r.lv = a.z; r.j0 = a.w;
+  r.jn = b4.x; r.jt = b4.y; r.qa = b4.z; r.da = b4.w;
+  r.d0 = c4.x; r.dn = c4.y; r.mocap = c4.z; r.root = c4.w;
+  r.c0 = e4.x; r.cn = e4.y; r.chp = e4.z;
+  r.sub = u64_of(f4.x, f4.y);
+  r.dofs = u64_of(f4.z, f4.w);
+  const int b = r.b;
   r.pos = v3(P.pos + 3 * b); r.quat = q4(P.quat + 4 * b);
   r.ipos = v3(P.ipos + 3 * b); r.iquat = q4(P.iquat + 4 * b);
   r.mass = P.mass[b]; r.inert = v3(P.inertia + 3 * b);
   const int k = r.jn > 0 ? r.j0 : 0;
-  r.jt = m.jnt_type[k]; r.qa = m.jnt_qposadr[k]; r.da = m.jnt_dofadr[k];
   r.jpos = v3(P.jpos + 3 * k); r.jaxis = v3(P.jaxis + 3 * k);
   r.qp0 = P.qpos0[r.qa];
   return r;
@@ -1483,13 +1483,13 @@ __device__ __forceinline__ JntRec jnt_of(const DModel& m, const BodyPtrs& P, con
 }
 struct BodyLite { int b, p, lv, d0, dn; uint64_t dofs; };
 __device__ __forceinline__ BodyLite load_body_lite(const DModel& m, const Dims& d, int i) {
+  (void)d;
   BodyLite r;
-  r.b = m.level_body[i];
-  r.dofs = m.body_dofmask[r.b];
-  r.lv = 0;
-  for (int lv = 1; lv < d.nlevel; lv++) r.lv = i >= m.level_start[lv] ? lv : r.lv;
-  r.p = m.body_parentid[r.b];
-  r.d0 = m.body_dofadr[r.b]; r.dn = m.body_dofnum[r.b];
+  const int4* rec = reinterpret_cast<const int4*>(m.body_rec + (size_t)kBodyRec * i);
+  const int4 a = rec[0], c4 = rec[2], f4 = rec[4];
+  r.b = a.x; r.p = a.y; r.lv = a.z;
+  r.d0 = c4.x; r.dn = c4.y;
+  r.dofs = u64_of(f4.z, f4.w);
   return r;
 }
 struct DofRec {
@@ -1505,9 +1505,8 @@ __device__ __forceinline__ ActRec load_act(const DModel& m, const float* gear, c
                                            const float* bias, const float* frange,
                                            const float* crange, int u) {
   ActRec r;
-  const int j = m.actuator_trnid[u];
-  r.dof = m.jnt_dofadr[j]; r.qa = m.jnt_qposadr[j];
-  r.ctrllim = m.actuator_ctrllimited[u]; r.forcelim = m.actuator_forcelimited[u];
+  const int4 a = *reinterpret_cast<const int4*>(m.act_rec + (size_t)kActRec * u);
+  r.dof = a.x; r.qa = a.y; r.ctrllim = a.z; r.forcelim = a.w;
   r.gear = gear[u]; r.gain = gain[3 * u];
   r.b0 = bias[3 * u]; r.b1 = bias[3 * u + 1]; r.b2 = bias[3 * u + 2];
   r.fr0 = frange[2 * u]; r.fr1 = frange[2 * u + 1];
@@ -1750,14 +1749,16 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     DofRec Dr;
     {
       const int i = min(lane, max(nv - 1, 0));
-      const int j = m.dof_jntid[i];
       const float* arm = MF(dof_armature);
       const float* damping = MF(dof_damping);
       const float* jstiff = MF(jnt_stiffness);
       const float* qspring = MF(qpos_spring);
-      Dr.body = m.dof_bodyid[i]; Dr.anc = m.dof_ancmask[i];
-      Dr.jt = m.jnt_type[j]; Dr.qa = m.jnt_qposadr[j];
-      Dr.pbody = m.body_parentid[Dr.body]; Dr.jd0 = m.jnt_dofadr[j]; Dr.bd0 = m.body_dofadr[Dr.body];
+      const int4* rec = reinterpret_cast<const int4*>(m.dof_rec + (size_t)kDofRec * i);
+      const int4 a = rec[0], b4 = rec[1], c4 = rec[2];
+      Dr.body = a.x; Dr.jt = a.y; Dr.qa = a.z; Dr.pbody = a.w;
+      Dr.jd0 = b4.x; Dr.bd0 = b4.y;
+      const int j = b4.z;
+      Dr.anc = u64_of(c4.x, c4.y);
       Dr.arm = arm[i]; Dr.damp = damping[i]; Dr.stiff = jstiff[j]; Dr.qs = qspring[Dr.qa];
     }
 #ifdef MJX_STAMPS
