@@ -8,6 +8,10 @@
 #include <initializer_list>
 #include <utility>
 
+#ifndef MJX_JTDJ_MFMA
+#define MJX_JTDJ_MFMA 0
+#endif
+
 namespace mjx {
 
 // register-row length of the dense SPD kernels: exact fits for the shipped robots (Go1 nvp
@@ -23,7 +27,7 @@ constexpr int nr_for_nv(int nv) {
 // left of the diagonal -- at offset 8 b (b + 1) + 4 (b + 1) r.  Dense (chunk k of 4 floats is
 // at 4k), 16-byte aligned rows, 8 nb (nb + 1) floats in all (720 for nvp 36 instead of 1296).
 // The phase hand-offs of the symmetric M (A -> B) and of the implicit-integration factor
-// (A -> C) use it.
+// (A -> C) use it, and phase B stages the Newton Hessian and its factor in it.
 constexpr int ltr_off(int i) { return 8 * (i >> 2) * ((i >> 2) + 1) + 4 * ((i >> 2) + 1) * (i & 3); }
 constexpr int ltr_size(int nvp) { return 8 * (nvp >> 2) * ((nvp >> 2) + 1); }
 
@@ -39,6 +43,11 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   Lds L{};
   const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
   constexpr int A = 1, B = 2, Cp = 4;
+  // M's slot: phase A factors M in full form; phase B holds M in LTR form and stages the
+  // Newton Hessian and its factor in the same form (the MFMA J^T D J variant keeps the full
+  // one), and the slot also takes jt_mul's partial sums (red)
+  const int mslot = ph == 1 && !MJX_JTDJ_MFMA
+                        ? (ltr_size(nv) > 5 * kWave ? ltr_size(nv) : 5 * kWave) : nv * nv;
   struct Slot { int Lds::*f; int n; int mask; };
   const Slot all[] = {
     {&Lds::ints, 8, A | B | Cp},
@@ -57,7 +66,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::cdof, 6 * nv, A | Cp}, {&Lds::cdofdot, 6 * nv, 0}, {&Lds::cacc_v, 6 * nb, Cp},
     {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
-    {&Lds::M, nv * nv, A | B}, {&Lds::H, nv * nv, A | B},
+    {&Lds::M, mslot, A | B}, {&Lds::H, nv * nv, A | B},
     {&Lds::qfrc_bias, nv, 0}, {&Lds::qfrc_passive, nv, 0}, {&Lds::qfrc_act, nv, A},
     {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
     {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
@@ -106,7 +115,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     L.efc_Js = L.efc_aref;
     // the Cholesky stages H in M's slot: rows are loaded before the first column block is
     // published and the factor is stored after the last (LDS ops of a wave run in order)
-    if (nv * nv >= 4 * kWave) L.chol = L.M;
+    if (mslot >= 4 * kWave) L.chol = L.M;
   }
   if (ph == 0) {
     // Phase A stage order is kinematics, com, CRB/M, RNE, smooth solve, subtree momenta,

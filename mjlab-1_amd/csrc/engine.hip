@@ -520,16 +520,21 @@ int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
     return 0;
   };
   if ((size_t)make_lds(d, 1).total * 4 <= (size_t)160 * 1024 / top) return 0;  // no need
-  // one class at 5/6 of the register-bound residency (10 worlds/CU for the G1 Newton
-  // kernel), the rest at full capacity.  Measured (G1 4096, B span per substep): one class
+  // One class below the register-bound residency, the rest at full capacity (gated at 5/6 of
+  // it).  Measured with the round-3 full-form Hessian (G1 4096, B span per substep): one class
   // at 44 / 52 / 60 / 64 / 72 / 84 rows 202 / 196 / 197 / 197 / 203 / 198 us; two classes
   // (44+84, 44+64, 60+100) 207-216 us -- concurrent class launches crowd each other out
   // A class that at most doubles the full carve's residency does not repay the classify
   // launch and the fork/join (Go1 8192: full carve 8 worlds/CU, B + gaps 136 -> 153 us)
+  // Since the Newton Hessian is staged in LTR form (round 4: 60 rows 4052 -> 3476 words) the
+  // class sits at 11/12 of the register-bound residency (G1: 64 rows, 11 worlds/CU).  G1
+  // env-steps/s, caps default-5/6 (72 rows, 10/CU) / 56 (12/CU) / 64 (11/CU): velocity 4096
+  // 2.636 / 2.662 / 2.657 M, jump flat 16384 7.80 / 7.80 / 7.88 M, jump hfield 16384 4.81 /
+  // 4.88 / 4.87 M, rough 4096 2.45 / 2.46 / 2.47 M, tracking 2.46 / 2.47 / 2.46 M.
   const int full_per_cu = (int)((size_t)160 * 1024 / ((size_t)make_lds(d, 1).total * 4));
   for (int w : {(5 * top) / 6}) {
     if (w < 8 || 2 * full_per_cu > w) continue;
-    const int r = cap_for(w);
+    const int r = cap_for((11 * top) / 12);
     if (r > 0 && (n == 0 || r > caps[n - 1]) && n < kRowClasses) caps[n++] = r;
   }
   return n;

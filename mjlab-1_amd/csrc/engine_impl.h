@@ -613,21 +613,27 @@ __device__ __forceinline__ void rows_store_strict_ltr(const float (&A)[NR], floa
                                 c + 2 < ln ? A[c + 2] * rd : c + 2 == ln ? rd : 0.f,
                                 c + 3 < ln ? A[c + 3] * rd : c + 3 == ln ? rd : 0.f));
 }
+// Row `row` of an LTR matrix as a full register row WITHOUT masking: columns past the row's
+// tiles hold the next rows' entries (every read stays inside the ltr_size(nvp) array: the
+// last block's rows are full).  For the callers whose entries above the diagonal are scratch
+// or dropped by their own k < lane select; one base address and immediate offsets, where a
+// per-lane row length costs a select per column (+18 VGPRs in the Newton kernel).
+template <int NR>
+__device__ __forceinline__ void rows_load_ltr_span(float (&A)[NR], const float* rp, int nvp) {
+#pragma unroll
+  for (int c = 0; c < NR; c += 4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < nvp) v = ld4(rp + c);
+    A[c] = v.x; A[c + 1] = v.y; A[c + 2] = v.z; A[c + 3] = v.w;
+  }
+}
 template <int NR>
 __device__ __forceinline__ void rows_load_factor_ltr(float (&A)[NR], float& rd, const float* Lp,
                                                      int nvp, int lane) {
   const int ln = opaque_lane(lane);
   const int row = ln < nvp ? ln : 0;
   const float* rp = Lp + ltr_off(row);
-  const int len = 4 * ((row >> 2) + 1);
-#pragma unroll
-  for (int c = 0; c < NR; c += 4) {
-    // in-row address for every lane, then a select: a per-lane row length under an `if`
-    // is an exec-mask branch per column block
-    const float4 v = ld4(rp + (c < len ? c : 0));
-    const bool in = c < len;
-    A[c] = in ? v.x : 0.f; A[c + 1] = in ? v.y : 0.f; A[c + 2] = in ? v.z : 0.f; A[c + 3] = in ? v.w : 0.f;
-  }
+  rows_load_ltr_span<NR>(A, rp, nvp);  // entries k >= lane are zeroed below
   const float dv = rp[row];
   rd = ln < nvp ? dv : 1.f;
   const float ljj = __builtin_amdgcn_rcpf(rd);
@@ -653,6 +659,19 @@ __device__ __forceinline__ void rows_load_factor_ltr_raw(float (&A)[NR], float& 
     A[c] = in ? v.x : 0.f; A[c + 1] = in ? v.y : 0.f; A[c + 2] = in ? v.z : 0.f; A[c + 3] = in ? v.w : 0.f;
   }
   dv = rp[row];
+}
+// Register rows of a matrix in LTR form (the lower tiles, unmasked), identity rows past nvp:
+// rows_load's counterpart for the blocked Cholesky, whose entries above the diagonal are
+// scratch.
+template <int NR>
+__device__ __forceinline__ void rows_load_ltr(float (&A)[NR], const float* Lp, int nvp, int lane) {
+  rows_load_ltr_span<NR>(A, Lp + ltr_off(lane < nvp ? lane : 0), nvp);
+  if (NR > nvp || kWave > NR) {
+    const int ln = opaque_lane(lane);
+    const bool pad = ln >= nvp;
+#pragma unroll
+    for (int c = 0; c < NR; c++) A[c] = pad ? (c == ln ? 1.f : 0.f) : A[c];
+  }
 }
 template <int NR>
 __device__ __forceinline__ void rows_scale_factor_ltr(float (&A)[NR], float& rd, float dv, int nvp,
@@ -731,6 +750,38 @@ __device__ __forceinline__ void tiles_store_sym(const float (&A)[2][16], const T
     for (int c = 0; c < 4; c++)
       st4v(Mm + (4 * T.bj[s] + c) * nvp + 4 * T.bi[s],
            make_float4(A[s][c], A[s][4 + c], A[s][8 + c], A[s][12 + c]));
+  }
+}
+// Phase B stages the Newton Hessian in LTR form (720 floats for nvp 36, not 1296: the
+// bulk row class's LDS then admits 11 worlds per CU instead of 10).  Tiles -> LTR in the
+// natural order, for rows_load_ltr.
+__device__ __forceinline__ void tiles_store_ltr(const float (&A)[2][16], const Tiles& T, float* Lp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      st4v(Lp + ltr_off(4 * T.bi[s] + r) + 4 * T.bj[s],
+           make_float4(A[s][4 * r], A[s][4 * r + 1], A[s][4 * r + 2], A[s][4 * r + 3]));
+  }
+}
+// Tiles -> the REVERSED matrix (index p <-> nvp-1-p) in LTR form: tile (bi, bj) lands at
+// reversed block (nb-1-bj, nb-1-bi), transposed off the diagonal, flipped on it.  The values
+// are the ones tiles_store_sym + rows_load_rev read (the transposed copy above the diagonal,
+// each diagonal tile's own entries), so the factor is bit for bit the full-layout one.
+__device__ __forceinline__ void tiles_store_rev_ltr(const float (&A)[2][16], const Tiles& T, float* Lp) {
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    if (!T.own[s]) continue;
+    const int I = T.nb - 1 - T.bj[s], J = T.nb - 1 - T.bi[s];
+    const bool dg = T.bi[s] == T.bj[s];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float v[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) v[c] = dg ? A[s][4 * (3 - r) + 3 - c] : A[s][4 * (3 - c) + 3 - r];
+      st4v(Lp + ltr_off(4 * I + r) + 4 * J, make_float4(v[0], v[1], v[2], v[3]));
+    }
   }
 }
 // out = A v for the symmetric matrix held as lower 4x4 register tiles (diagonal blocks
@@ -1630,12 +1681,10 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 // Worlds [w0, w1) -- one split of the batch (launch_step).  `sel` & 0xff selects that
 // split's Newton work-list segments; in phases A and C, sel >> 8 = row class + 1 restricts
 // the launch to that class's worlds (0: every world).
-#if MJX_JTDJ_MFMA
-// the MFMA accumulator must not push the Newton kernel past 168 registers (3 waves / SIMD)
-#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
-#else
-#define MJX_PHASE_ATTR
-#endif
+// Phase B at most 168 registers (3 waves / SIMD): the Newton kernel's allocation drifts with
+// small code changes (G1 161 -> 177 with the LTR Hessian; no spill at 168) and the bulk row
+// class's residency is set by it.  Not for the generic NR 56 / 64 rows (they would spill).
+#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(PH == 1 && NR <= 48 ? 3 : 1)))
 // LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
 // more registers in flight, for the launch that holds the heavy worlds.
 template <int NR, int PH, int SP, bool LAT>
@@ -3159,8 +3208,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
 #pragma unroll
             for (int e2 = 0; e2 < 16; e2++) A[s2][e2] = Mt[s2][e2];
           tiles_add_jtdj(A, T, J, Dv, act, nact, nvp);
-          if (tree_h) tiles_store_sym(A, T, Lm, nvp);  // rows_load_rev reads the upper triangle
-          else tiles_store(A, T, Lm, nvp);
+          if (tree_h) tiles_store_rev_ltr(A, T, Lm);  // H in LTR form (carve.h, phase B)
+          else tiles_store_ltr(A, T, Lm);
 #endif
         }
         sync();
@@ -3169,24 +3218,37 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           float R[NR];
           float rd;
           if (refactor) {
+#if MJX_JTDJ_MFMA
+            rows_load<NR>(R, Lm, nvp, lane);
+            rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);
+            rows_store_strict<NR>(R, rd, Lm, nvp, lane);
+#else
+            rows_load_ltr<NR>(R, Lm, nvp, lane);  // the reversed matrix's rows when tree_h
             if (tree_h) {
-              rows_load_rev<NR>(R, Lm, nvp, lane);
               if constexpr (kTree<SP>) rows_chol_tree<NR, SP>(R, rd, S + LB.chol, lane);
             } else {
-              rows_load<NR>(R, Lm, nvp, lane);
               rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
             }
-            rows_store_strict<NR>(R, rd, Lm, nvp, lane);
+            rows_store_strict_ltr<NR>(R, rd, Lm, nvp, lane);
+#endif
             rows_fwd_rows<NR>(R, rd, lane);
           } else {
+#if MJX_JTDJ_MFMA
             rows_load_factor<NR>(R, rd, Lm, nvp, lane);
+#else
+            rows_load_factor_ltr<NR>(R, rd, Lm, nvp, lane);
+#endif
           }
           sync();
           SUBSTAMP(3);
           // the tree-form factor is of the reversed matrix: lane i solves for dof nvp-1-i
           const int pl = tree_h ? nvp - 1 - lane : lane;
           float xs = lane < nvp ? S[L.srch + pl] : 0.f;
+#if MJX_JTDJ_MFMA
           xs = rows_solve<NR>(R, rd, Lm, xs, nvp, lane);
+#else
+          xs = rows_solve_ltr<NR>(R, rd, Lm, xs, nvp, lane);
+#endif
           sync();
           if (lane < nvp) S[L.srch + pl] = xs;
           sync();
