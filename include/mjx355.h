@@ -127,8 +127,9 @@ int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mj
  * capacity is dropped (counted by mjx_sim_stats).  The contact output arrays hold
  * nconmax_max slots per world; a masked forward re-solves its overflowing worlds too.  A batch
  * the engine splits into concurrent halves (large batches of models without Newton row
- * classes) gets no re-solve: its max capacity is the fast carve (mjx_sim_info reports the
- * capacity wired). */
+ * classes) re-solves behind each half's launches; only a split forced onto a model with row
+ * classes (MJX355_SPLIT, diagnostic) keeps the fast carve as its max capacity (mjx_sim_info
+ * reports the capacity wired). */
 int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax, int nconmax_max,
                       int njmax_max, mjxSim** out);
 int mjx_sim_destroy(mjxSim* sim);

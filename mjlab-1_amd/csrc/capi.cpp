@@ -583,8 +583,11 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
   // The overflow re-solve forks its chain from the stream that ran phase A.  With batch
   // splits that is a split stream, and a second-level fork from a captured side stream
   // crashes hipStreamEndCapture under the HIP runtime torch bundles:
-  // split batches keep the fast carve as their max capacity (overflow drops, counted).
-  s->big = (nconmax_max > nconmax || njmax_max > njmax) && s->side.nsplit == 1;
+  // split batches without row classes run the chain in line on their split stream instead
+  // (launch_step); split batches with row classes (a diagnostic topology) keep the fast
+  // carve as their max capacity (overflow drops, counted).
+  s->big = (nconmax_max > nconmax || njmax_max > njmax) &&
+           (s->side.nsplit == 1 || s->nrowclass == 0);
   s->con_stride = s->big ? nconmax_max : nconmax;
   if (s->big) {
     s->dbig = s->d;

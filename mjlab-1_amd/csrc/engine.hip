@@ -407,8 +407,11 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                            last, integrate, mask);
       // the re-solve chain: forked after this substep's phase A (and classify), joined at the
       // end of the substep -- the empty chain overlaps the class launches
+      // split batches: in line behind phase C on the split stream (a fork from a split
+      // stream is a second-level fork, which breaks graph capture; capi.cpp)
+      const bool ovf_inline = ovf && nsplit > 1;
       auto fork_ovf = [&]() {
-        if (!ovf) return hipSuccess;
+        if (!ovf || ovf_inline) return hipSuccess;
         hipError_t e2 = hipEventRecord(side->ovf_fork[k], st);
         if (e2 == hipSuccess) e2 = hipStreamWaitEvent(side->ovf[k], side->ovf_fork[k], 0);
         if (e2 == hipSuccess)
@@ -418,6 +421,10 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       };
       auto join_ovf = [&]() {
         if (!ovf) return hipSuccess;
+        if (ovf_inline) {
+          ovf_chain(host, dev, *hbig, dbig, st, k, w0, w1, sub, nsubstep, integrate, false);
+          return hipSuccess;
+        }
         hipError_t e2 = hipEventRecord(side->ovf_join[k], side->ovf[k]);
         if (e2 == hipSuccess) e2 = hipStreamWaitEvent(st, side->ovf_join[k], 0);
         return e2;

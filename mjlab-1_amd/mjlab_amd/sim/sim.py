@@ -283,8 +283,8 @@ class Simulation:
       check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
                                 self.fast_capacity[1], self.nconmax, self.njmax,
                                 ctypes.byref(self._sim)))
-      # the capacity the engine wired: batch-split launch topologies (large batches of
-      # models without Newton row classes) have no re-solve, their max is the fast carve
+      # the capacity the engine wired (a diagnostic split forced onto a model with Newton
+      # row classes has no re-solve: its max is the fast carve)
       info = self.info()
       self.nconmax, self.njmax = info["nconmax_max"], info["njmax_max"]
     _warn_capacity(cfg, self.nconmax, self.njmax)

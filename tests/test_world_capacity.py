@@ -59,5 +59,11 @@ def test_specs_carry_the_task_capacities():
   assert caps["g1_tracking"] == [(64, 250), (48, 160)]
   for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
     assert caps[name] == [(48, 160), (64, 300)], name
-  for name in ("go1_velocity", "go1_velocity_rough"):
-    assert caps[name] == [(48, 160), (64, 280)], name
+  # Go1: its tasks' engine_capacity (24, 96) first, the default and the max carve
+  from mjlab_amd.envs import unitree_go1_flat_env_cfg, unitree_go1_rough_env_cfg
+  for name, make in (("go1_velocity", unitree_go1_flat_env_cfg),
+                     ("go1_velocity_rough", unitree_go1_rough_env_cfg)):
+    assert caps[name] == [(24, 96), (48, 160), (64, 280)], name
+    sim, go1 = make().sim, load_scene(name)
+    assert world_capacity(sim, go1) == (24, 96)
+    assert max_capacity(sim, go1) == (64, 280)
