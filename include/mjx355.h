@@ -177,6 +177,14 @@ int mjx_sim_stats(mjxSim* sim, int32_t* out, void* stream);
  * capacity's kernels (csrc/specs.inc entry, 0 = generic), [6] re-solve list capacity per
  * substep, [7] Newton row classes. */
 int mjx_sim_info(const mjxSim* sim, int32_t* out);
+/* Diagnostics (parity tests): the joint-space inertia M of every world as the last substep's
+ * phase A formed it (mjData.qM, mj_crb + armature; the reference reads it from mujoco_warp's
+ * Data.qM), copied from the engine's phase hand-off scratch into the device buffer `out`:
+ * float [nworld][L] with L = 8 nb (nb + 1), nb = ceil(nv / 4), the lower 4 x 4 tiles of the
+ * nvp x nvp matrix row by row (row i = 4b + r holds columns [0, 4(b + 1)) at 8 b (b + 1) +
+ * 4 (b + 1) r).  `big` = 1 reads the max-capacity scratch (worlds the overflow re-solve ran).
+ * Valid after mjx_step / mjx_forward until the next launch; stream-ordered. */
+int mjx_sim_mass_matrix(mjxSim* sim, int big, float* out, void* stream);
 /* Diagnostics: per-stage cycle sums uint64[48] (non-zero only in the -DMJX_STAMPS build). */
 int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
 /* Which step kernels the sim launches: k > 0 = kernels compiled for entry k of

@@ -930,6 +930,18 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
 
 int mjx_sim_spec(const mjxSim* s) { return s ? s->spec : -1; }
 
+int mjx_sim_mass_matrix(mjxSim* s, int big, float* out, void* stream) {
+  if (!s || !out) return fail("null argument");
+  if (big && !s->big) return fail("the sim has no max-capacity scratch");
+  const int nvp = (s->d.nv + 3) & ~3;
+  const size_t n = (size_t)mjx::ltr_size(nvp);
+  const float* src = (big ? s->gscr_big : s->gscr) + (big ? s->lds_big[1].M : s->lds_ph[1].M);
+  const size_t pitch = sizeof(float) * (size_t)(big ? s->gstride_big : s->gstride);
+  HIPCHK(hipMemcpy2DAsync(out, sizeof(float) * n, src, pitch, sizeof(float) * n, s->nworld,
+                          hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
 int mjx_sim_info(const mjxSim* s, int32_t* out) {
   if (!s || !out) return fail("null argument");
   const int32_t v[8] = {s->d.nconmax, s->d.njmax, s->big ? s->dbig.nconmax : s->d.nconmax,

@@ -103,6 +103,8 @@ class ContactSensorCfg:
       _, names = ent.find_bodies([match.pattern])
     else:
       raise ValueError("Secondary mode must be one of {'geom','body','subtree'}")
+    if not names:  # contact_sensor.py:459-462
+      raise ValueError(f"Secondary pattern '{match.pattern}' matched nothing in '{match.entity}'")
     if len(names) == 1 or self.secondary_policy == "first":
       return names[0]
     raise ValueError(f"Secondary pattern '{match.pattern}' matched multiple: {names}. "

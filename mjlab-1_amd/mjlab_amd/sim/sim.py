@@ -232,12 +232,16 @@ def max_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
 _capacity_warned: set = set()
 
 
-def _warn_capacity(cfg: SimulationCfg, ncon: int, rows: int) -> None:
+def _warn_capacity(cfg: SimulationCfg, model, ncon: int, rows: int) -> None:
   """Warn once per distinct clamp: a world whose contacts or rows overflow the max
   capacity drops whole contacts (counted in `engine_counters`, `stats()` and the env's
   extras["log"]["Sim/..."] entries)."""
   asked = (cfg.nconmax, cfg.njmax)
-  if (cfg.njmax is not None and cfg.njmax > rows) and asked not in _capacity_warned:
+  # rows past 4 * ncon + 2 * (limited joints) cannot occur (every row belongs to a pyramidal
+  # contact or a joint limit): warn only when the capacity is below what njmax allows of that
+  nlim = int(np.sum(model.jnt_limited)) if model.njnt else 0
+  reachable = 4 * ncon + 2 * nlim
+  if (cfg.njmax is not None and min(cfg.njmax, reachable) > rows) and asked not in _capacity_warned:
     _capacity_warned.add(asked)
     import warnings
     warnings.warn(
@@ -287,7 +291,7 @@ class Simulation:
       # row classes has no re-solve: its max is the fast carve)
       info = self.info()
       self.nconmax, self.njmax = info["nconmax_max"], info["njmax_max"]
-    _warn_capacity(cfg, self.nconmax, self.njmax)
+    _warn_capacity(cfg, model, self.nconmax, self.njmax)
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
                          for i in range(L.mjx_field_count(self._sim))}
     self._data_bridge = DeviceBridge(self, "", None)
@@ -434,7 +438,34 @@ class Simulation:
     """Device [4] int32 view: overflow_events() followed by the re-solve count --
     world-substeps that overflowed the fast carve and were re-solved at the max capacity
     (nothing dropped)."""
+    if "engine_events" not in self._field_names:  # an older engine build (scripts/ab.sh)
+      return torch.cat([self.overflow_events(), self.overflow_events().new_zeros(1)])
     return self.field("engine_events")[0, :4]
+
+  def mass_matrix(self, big: bool = False) -> torch.Tensor:
+    """[nworld, nv, nv] fp32 joint-space inertia M as the last substep's phase A formed it
+    (mjData.qM; diagnostic copy from the engine's phase hand-off scratch, mjx_sim_mass_matrix).
+    `big`: the max-capacity scratch, where the overflow re-solve formed the M of the worlds
+    it ran.  Stream-ordered, no host sync."""
+    nv = self.mj_model.nv
+    nvp = (nv + 3) & ~3
+    nb = nvp // 4
+    ltr = torch.empty(self.num_envs, 8 * nb * (nb + 1), dtype=torch.float32, device=self.device)
+    check(lib().mjx_sim_mass_matrix(self._sim, int(big), ctypes.c_void_p(ltr.data_ptr()),
+                                    _stream_handle(self._torch_device)))
+    rows, cols = [], []
+    for i in range(nvp):
+      b, r = i >> 2, i & 3
+      off = 8 * b * (b + 1) + 4 * (b + 1) * r
+      rows.append(torch.arange(off, off + i + 1))
+      cols.append(torch.full((i + 1,), i, dtype=torch.long))
+    idx = torch.cat(rows).to(ltr.device)
+    ii = torch.cat(cols).to(ltr.device)
+    jj = torch.cat([torch.arange(i + 1) for i in range(nvp)]).to(ltr.device)
+    full = torch.zeros(self.num_envs, nvp, nvp, dtype=torch.float32, device=ltr.device)
+    full[:, ii, jj] = ltr[:, idx]
+    full[:, jj, ii] = ltr[:, idx]
+    return full[:, :nv, :nv]
 
   def stats(self) -> dict:
     """Engine counters: max contacts/rows seen, overflow and unsupported-pair events,

@@ -1529,7 +1529,7 @@ void orc_step(const mjxModelDesc* m, orcData* d) {
   double h = m->timestep;
   double* A = (double*)malloc(sizeof(double) * (nv * nv + nv));
   double* f = A + nv * nv;
-  memcpy(A, d->qM, sizeof(double) * nv * nv);
+  memcpy(A, d->qM_given ? d->qM_given : d->qM, sizeof(double) * nv * nv);
   int need = 0;
   if (m->integrator == MJX_INT_IMPLICITFAST) {
     for (int i = 0; i < nv; i++) if (m->dof_damping[i] > 0) { A[i * nv + i] += h * m->dof_damping[i]; need = 1; }
@@ -1673,8 +1673,9 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
                         double time, const double* qacc, const double* qfrc_constraint,
-                        const double* qfrc_smooth, double* out_qpos, double* out_qvel,
-                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost) {
+                        const double* qfrc_smooth, const double* qM, double* out_qpos,
+                        double* out_qvel, double* out_sensordata, double* out_qfrc_constraint,
+                        double* out_cost, double* out_efc_force, int* out_nefc) {
   orcData* d = orc_data_new(m, nconmax, njmax);
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -1684,20 +1685,116 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
   d->qacc_given = qacc;
   d->qfrc_constraint_given = qfrc_constraint;
   d->qfrc_smooth_given = qfrc_smooth;
+  d->qM_given = qM;
   orc_step(m, d);
   if (out_qpos) memcpy(out_qpos, d->qpos, sizeof(double) * m->nq);
   if (out_qvel) memcpy(out_qvel, d->qvel, sizeof(double) * m->nv);
   if (out_sensordata) memcpy(out_sensordata, d->sensordata, sizeof(double) * m->nsensordata);
   if (out_qfrc_constraint) memcpy(out_qfrc_constraint, d->qfrc_constraint, sizeof(double) * m->nv);
   if (out_cost) *out_cost = d->cost;
+  if (out_efc_force) memcpy(out_efc_force, d->efc_force, sizeof(double) * d->nefc);
+  if (out_nefc) *out_nefc = d->nefc;
   int ov = d->overflow;
   orc_data_free(d);
   return ov;
 }
 
+/* |terms| of the CRB mass matrix (orc_mass_matrix_scale); d after orc_forward */
+static void mass_abs(const mjxModelDesc* m, const orcData* d, double* out) {
+  const int nb = m->nbody, nv = m->nv;
+  double* cab = (double*)calloc((size_t)10 * nb + 6 * nv, sizeof(double));
+  double* dab = cab + 10 * nb;
+  for (int b = 1; b < nb; b++) {
+    double* c = cab + 10 * b;
+    const double* off = d->subtree_com + 3 * m->body_rootid[b];
+    const double* R = d->ximat + 9 * b;
+    const double* I = m->body_inertia + 3 * b;
+    double full[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        full[3 * i + j] = fabs(R[3 * i] * I[0] * R[3 * j]) + fabs(R[3 * i + 1] * I[1] * R[3 * j + 1]) +
+                          fabs(R[3 * i + 2] * I[2] * R[3 * j + 2]);
+    double dv[3], ms = m->body_mass[b], t[3];
+    v3_sub(dv, d->xipos + 3 * b, off);
+    /* the offset is a difference of rounded positions: it carries eps times the magnitude of
+     * the coordinates it came from (about the tree root, where the engine forms it); each
+     * component's magnitude takes that on, so the terms bound their first-order sensitivity
+     * to it too */
+    const double* root = d->xpos + 3 * m->body_rootid[b];
+    v3_sub(t, d->xipos + 3 * b, root);
+    double rho = v3_norm(t);
+    v3_sub(t, off, root);
+    rho += v3_norm(t);
+    for (int k = 0; k < 3; k++) dv[k] = fabs(dv[k]) + rho;
+    const double dd = v3_dot(dv, dv);
+    c[0] = full[0] + ms * (dd + dv[0] * dv[0]);
+    c[1] = full[4] + ms * (dd + dv[1] * dv[1]);
+    c[2] = full[8] + ms * (dd + dv[2] * dv[2]);
+    c[3] = full[1] + ms * fabs(dv[0] * dv[1]);
+    c[4] = full[2] + ms * fabs(dv[0] * dv[2]);
+    c[5] = full[5] + ms * fabs(dv[1] * dv[2]);
+    c[6] = ms * fabs(dv[0]); c[7] = ms * fabs(dv[1]); c[8] = ms * fabs(dv[2]);
+    c[9] = ms;
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    const int p = m->body_parentid[b];
+    if (p > 0)
+      for (int i = 0; i < 10; i++) cab[10 * p + i] += cab[10 * b + i];
+  }
+  /* cdof = [axis; axis x (com_root - anchor)]: its moment arm takes on the magnitude of the
+   * coordinates it came from, as above */
+  for (int i = 0; i < 6 * nv; i++) dab[i] = fabs(d->cdof[i]);
+  for (int k = 0; k < m->njnt; k++) {
+    const int b = m->jnt_bodyid[k], dof = m->jnt_dofadr[k], rb = m->body_rootid[b];
+    const int nd = m->jnt_type[k] == MJX_JNT_FREE ? 6 : m->jnt_type[k] == MJX_JNT_BALL ? 3 : 1;
+    double t[3];
+    v3_sub(t, d->xanchor + 3 * k, d->xpos + 3 * rb);
+    double rho = v3_norm(t);
+    v3_sub(t, d->subtree_com + 3 * rb, d->xpos + 3 * rb);
+    rho += v3_norm(t);
+    for (int i = 0; i < nd; i++) {
+      double* c = dab + 6 * (dof + i);
+      const double wn = c[0] + c[1] + c[2];  /* |axis| (1-norm) */
+      for (int j = 3; j < 6; j++) c[j] += wn * rho;
+    }
+  }
+  memset(out, 0, sizeof(double) * nv * nv);
+  for (int i = 0; i < nv; i++) {
+    /* inert_mul with every product in absolute value (the cross products' two terms added) */
+    const double* I = cab + 10 * m->dof_bodyid[i];
+    const double* w = dab + 6 * i; const double* u = w + 3;
+    const double* h = I + 6;
+    double f[6];
+    f[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2] + h[1] * u[2] + h[2] * u[1];
+    f[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2] + h[2] * u[0] + h[0] * u[2];
+    f[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2] + h[0] * u[1] + h[1] * u[0];
+    f[3] = I[9] * u[0] + h[1] * w[2] + h[2] * w[1];
+    f[4] = I[9] * u[1] + h[2] * w[0] + h[0] * w[2];
+    f[5] = I[9] * u[2] + h[0] * w[1] + h[1] * w[0];
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      const double v = dot6(dab + 6 * j, f);
+      out[i * nv + j] = v;
+      out[j * nv + i] = v;
+    }
+    out[i * nv + i] += fabs(m->dof_armature[i]);
+  }
+  free(cab);
+}
+
+int orc_mass_matrix_scale(const mjxModelDesc* m, const double* qpos, double* out_Mabs) {
+  orcData* d = orc_data_new(m, 1, 1);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  kinematics(m, d);
+  com_pos(m, d);
+  mass_abs(m, d, out_Mabs);
+  orc_data_free(d);
+  return 0;
+}
+
 int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                          const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                         double time, double* out_scale, double* out_vscale) {
+                         double time, const double* a_extra, double* out_scale,
+                         double* out_vscale) {
   orcData* d = orc_data_new(m, nconmax, njmax);
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -1712,7 +1809,7 @@ int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const do
   double* col = a + nv;
   memcpy(H, d->qM, sizeof(double) * nv * nv);
   for (int i = 0; i < nv; i++) {
-    double s = fabs(d->qfrc_smooth[i]);
+    double s = fabs(d->qfrc_smooth[i]) + (a_extra ? a_extra[i] : 0.0);
     for (int k = 0; k < nv; k++) s += fabs(d->qM[i * nv + k] * d->qacc[k]);
     a[i] = s;
   }

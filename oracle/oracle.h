@@ -55,6 +55,7 @@ typedef struct {
   const double* qacc_given;
   const double* qfrc_constraint_given;  /* with qacc_given: the integration uses this */
   const double* qfrc_smooth_given;      /* with qacc_given: and this */
+  const double* qM_given;               /* with qacc_given (may be NULL): the integration's M */
   double cost;  /* the constraint-problem cost at the final qacc (Gauss + active rows) */
   /* scratch */
   double* work;
@@ -94,8 +95,9 @@ int orc_forward_dump(const mjxModelDesc* m, int nconmax, int njmax, const double
 int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                         const double* qvel, const double* qacc_warmstart, const double* ctrl,
                         double time, const double* qacc, const double* qfrc_constraint,
-                        const double* qfrc_smooth, double* out_qpos, double* out_qvel,
-                        double* out_sensordata, double* out_qfrc_constraint, double* out_cost);
+                        const double* qfrc_smooth, const double* qM, double* out_qpos,
+                        double* out_qvel, double* out_sensordata, double* out_qfrc_constraint,
+                        double* out_cost, double* out_efc_force /* njmax */, int* out_nefc);
 
 /* fp32 error scale of the Newton solution: mj_forward (fp64 solve), then at the solution
  * x the Hessian H = M + J_a^T D_a J_a of the active rows and, per dof j, the magnitude of
@@ -104,10 +106,23 @@ int orc_step_given_qacc(const mjxModelDesc* m, int nconmax, int njmax, const dou
  * whose gradient is exact to eps relative to its terms lands within eps * out_scale of x.
  * out_vscale (may be NULL): the same for the implicit integration's velocity update,
  * h * sum_j |A^-1_ij| (|qfrc_smooth_j| + |qfrc_constraint_j| + sum_k |A_jk dv_k|) with
- * A = M + h D (the implicitfast matrix) and dv the update. */
+ * A = M + h D (the implicitfast matrix) and dv the update.  a_extra (may be NULL) is added
+ * to a_j: a perturbation of the problem data already divided by eps (the parity tests pass
+ * the engine's measured mass-matrix and smooth-force differences, |dM| |x| + |d qfrc_smooth|,
+ * so the scale covers a solver that solved the engine's problem exactly to rounding). */
 int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
                          const double* qvel, const double* qacc_warmstart, const double* ctrl,
-                         double time, double* out_scale, double* out_vscale);
+                         double time, const double* a_extra, double* out_scale,
+                         double* out_vscale);
+
+/* Magnitude of the terms an evaluation of M sums (the composite-rigid-body algorithm about
+ * the root's subtree com, MuJoCo's mj_crb / cinert / cdof convention, as the engine forms
+ * it): out_Mabs[i][j] = |cdof_j| . (|crb_abs(body(i))| |cdof_i|), with crb_abs the subtree
+ * sum of each body's cinert term magnitudes (|I_c| + m (|d|^2 + d_k^2), m |d_k d_l|, m |d_k|,
+ * m) and every product taken in absolute value; armature on the diagonal.  A finite-
+ * precision M is exact to (a few) eps times this, not times |M|: a light dof deep in a tree
+ * (an ankle roll) is a small difference of O(m d^2) terms. */
+int orc_mass_matrix_scale(const mjxModelDesc* m, const double* qpos, double* out_Mabs);
 
 #ifdef __cplusplus
 }

@@ -78,42 +78,61 @@ def forward(model, qpos, qvel=None, qacc_warmstart=None, ctrl=None, time=0.0, st
 
 
 def step_given_qacc(model, qpos, qvel, qacc_warmstart, ctrl, time, qacc, qfrc_constraint=None,
-                    qfrc_smooth=None, nconmax=256, njmax=1024):
+                    qfrc_smooth=None, nconmax=256, njmax=1024, qM=None):
   """One mj_step whose constraint stage takes `qacc` instead of solving for it (forces,
   qfrc_constraint, sensors and the integration follow from it; with `qfrc_constraint` and
   `qfrc_smooth` the integration uses those instead), plus the constraint problem's cost at
-  that qacc.  Single world; returns a dict of fp64 arrays."""
+  that qacc.  With `qM` (nv x nv) the implicit integration uses that mass matrix (the
+  engine's own) instead of the oracle's.  Single world; returns a dict of fp64 arrays."""
   desc, keep = make_desc(model)
   f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
   nq, nv, nu, ns = model.nq, model.nv, model.nu, model.nsensordata
   out = dict(qpos=np.zeros(nq), qvel=np.zeros(nv), sensordata=np.zeros(max(ns, 1)),
-             qfrc_constraint=np.zeros(nv))
-  cost = ctypes.c_double()
+             qfrc_constraint=np.zeros(nv), efc_force=np.zeros(max(njmax, 1)))
+  cost, nefc = ctypes.c_double(), ctypes.c_int()
   a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
   g = f64(qacc, nv)
   fc = None if qfrc_constraint is None else f64(qfrc_constraint, nv)
   fs = None if qfrc_smooth is None else f64(qfrc_smooth, nv)
+  mq = None if qM is None else np.ascontiguousarray(qM, dtype=np.float64).reshape(nv, nv)
   ov = lib().orc_step_given_qacc(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
-                                 ctypes.c_double(time), _p(g), _p(fc), _p(fs), _p(out["qpos"]), _p(out["qvel"]),
-                                 _p(out["sensordata"]), _p(out["qfrc_constraint"]), ctypes.byref(cost))
+                                 ctypes.c_double(time), _p(g), _p(fc), _p(fs), _p(mq),
+                                 _p(out["qpos"]), _p(out["qvel"]),
+                                 _p(out["sensordata"]), _p(out["qfrc_constraint"]), ctypes.byref(cost),
+                                 _p(out["efc_force"]), ctypes.byref(nefc))
   del keep
   out["sensordata"] = out["sensordata"][:ns]
+  out["efc_force"] = out["efc_force"][:nefc.value]
   out["cost"], out["overflow"] = cost.value, ov
   return out
 
 
-def qacc_error_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256, njmax=1024):
+def mass_matrix_scale(model, qpos):
+  """[nv, nv] magnitudes of the terms the CRB mass matrix sums (orc_mass_matrix_scale): the
+  scale of an fp32 M's formation error."""
+  desc, keep = make_desc(model)
+  out = np.zeros((model.nv, model.nv))
+  lib().orc_mass_matrix_scale(ctypes.byref(desc), _p(np.ascontiguousarray(qpos, dtype=np.float64)),
+                              _p(out))
+  del keep
+  return out
+
+
+def qacc_error_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256, njmax=1024,
+                     extra=None):
   """Per-dof fp32 error scales (orc_qacc_error_scale): of the Newton solution, |H^-1| times
   the magnitudes of the gradient's terms at the fp64 solution; and of the implicitfast
-  velocity update, h |A^-1| times the magnitudes of its right-hand side's terms.  Returns
-  (qacc_scale, qvel_scale)."""
+  velocity update, h |A^-1| times the magnitudes of its right-hand side's terms.  `extra`
+  (nv, already divided by eps) adds a perturbation of the problem data to the gradient's
+  term magnitudes.  Returns (qacc_scale, qvel_scale)."""
   desc, keep = make_desc(model)
   f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
   nq, nv, nu = model.nq, model.nv, model.nu
   out, vout = np.zeros(nv), np.zeros(nv)
   a = [f64(qpos, nq), f64(qvel, nv), f64(qacc_warmstart, nv), f64(ctrl, nu)]
+  ex = None if extra is None else f64(extra, nv)
   lib().orc_qacc_error_scale(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a),
-                             ctypes.c_double(time), _p(out), _p(vout))
+                             ctypes.c_double(time), _p(ex), _p(out), _p(vout))
   del keep
   return out, vout
 
