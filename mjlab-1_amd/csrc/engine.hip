@@ -329,6 +329,14 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
                        integrate, nullptr);
 }
 
+static bool ovf_stream_env() {
+  static const bool on = [] {
+    const char* e = getenv("MJX355_OVF_STREAM");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side, const Params* hbig, const Params* dbig) {
@@ -439,6 +447,10 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       } else if (nc > 0) {
         hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(kClassifyThreads), 0, st, dev, w0, w1,
                            k, mask);
+        // MJX355_OVF_STREAM=1 (diagnostic, scripts/capture_probe*): the re-solve chain on a
+        // stream of its own, forked here and joined after the class joins -- round 4's
+        // topology, kept to reproduce its graph-replay crash
+        if (ovf_stream_env() && (e = fork_ovf()) != hipSuccess) return e;
         // Newton by row class, concurrently: the full-capacity class (few worlds, long
         // per-world latency) first on a side stream so its blocks dispatch first, the middle
         // classes on further side streams, the smallest (most worlds) on the launch stream.
@@ -468,7 +480,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           // graph replay under torch's HIP runtime (two middle classes + the re-solve stream).
           // Measured ahead of that class instead: G1 -3 % (its 64 KiB workgroups then take
           // LDS from the bulk class's first Newton waves)
-          if (c == 0 && ovf)
+          if (c == 0 && ovf && !ovf_stream_env())
             ovf_chain(host, dev, *hbig, dbig, side->stream[k][0], k, w0, w1, sub, nsubstep,
                       integrate, piped);
         }
@@ -478,6 +490,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           if (e == hipSuccess) e = hipStreamWaitEvent(st, side->join[k][c], 0);
           if (e != hipSuccess) return e;
         }
+        if (ovf_stream_env() && (e = join_ovf()) != hipSuccess) return e;
         if (piped) continue;
       } else {
         if ((e = fork_ovf()) != hipSuccess) return e;

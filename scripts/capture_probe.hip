@@ -8,6 +8,10 @@
 //   2 lds:  kernels take 96 KiB of dynamic LDS (hipFuncSetAttribute beforehand)
 //   4 args: kernels take the engine's 7 arguments
 //   8 wide: the classify launch is one 1024-thread block
+//  16 ovf:  per split a re-solve stream forked after classify (its own event) and joined after
+//           the class joins -- round 4's crashing topology (origin -> class streams + re-solve
+//           stream, flat forks); its chain is 3 launches (+ the next A when piped)
+//  32 replays: replay the instantiated graph 50 times instead of 2
 //
 // Topology per substep (as launch_step): origin --split_fork--> split streams; on split
 // stream k: [A] -> classify -> record fork[k] -> class streams wait -> class chains
@@ -74,6 +78,13 @@ static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, 
   std::vector<std::vector<hipStream_t>> cls(nsplit, std::vector<hipStream_t>(nc));
   std::vector<std::vector<hipEvent_t>> join(nsplit, std::vector<hipEvent_t>(nc));
   std::vector<hipEvent_t> fork(nsplit);
+  std::vector<hipStream_t> ovf(nsplit);
+  std::vector<hipEvent_t> ovf_fork(nsplit), ovf_join(nsplit);
+  for (int k = 0; k < nsplit; k++) {
+    CK(hipStreamCreateWithFlags(&ovf[k], hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&ovf_fork[k], hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&ovf_join[k], hipEventDisableTiming));
+  }
   for (int k = 0; k < nsplit; k++) {
     CK(hipEventCreateWithFlags(&fork[k], hipEventDisableTiming));
     for (int c = 0; c < nc; c++) {
@@ -125,6 +136,14 @@ static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, 
       if (!(nc > 0 && piped) || sub == 0) launch(st, base + 0);  // A
       if (nc > 0) {
         classify(st, base + 1);
+        if (feat & 16) {
+          CK(hipEventRecord(ovf_fork[k], st));
+          CK(hipStreamWaitEvent(ovf[k], ovf_fork[k], 0));
+          launch(ovf[k], 40 + 4 * k);      // max-carve A
+          launch(ovf[k], 40 + 4 * k + 1);  // latency Newton
+          launch(ovf[k], 40 + 4 * k + 2);  // C
+          if (piped && !last) launch(ovf[k], 40 + 4 * k + 3);  // next A
+        }
         CK(hipEventRecord(fork[k], st));
         for (int c = 0; c < nc; c++) {
           CK(hipStreamWaitEvent(cls[k][c], fork[k], 0));
@@ -142,6 +161,10 @@ static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, 
         for (int c = 0; c < nc; c++) {
           CK(hipEventRecord(join[k][c], cls[k][c]));
           CK(hipStreamWaitEvent(st, join[k][c], 0));
+        }
+        if (feat & 16) {
+          CK(hipEventRecord(ovf_join[k], ovf[k]));
+          CK(hipStreamWaitEvent(st, ovf_join[k], 0));
         }
         if (piped) continue;
       } else {
@@ -175,14 +198,21 @@ static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, 
   CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
   printf("launch\n");
   fflush(stdout);
-  CK(hipGraphLaunch(exec, origin));
-  CK(hipGraphLaunch(exec, origin));
+  const int nrep = (feat & 32) ? 50 : 2;
+  for (int r = 0; r < nrep; r++) {
+    CK(hipGraphLaunch(exec, origin));
+    if (r % 10 == 9) {
+      CK(hipStreamSynchronize(origin));
+      printf("replay %d ok\n", r + 1);
+      fflush(stdout);
+    }
+  }
   CK(hipStreamSynchronize(origin));
   int got[nslot];
   CK(hipMemcpy(got, slots, sizeof(got), hipMemcpyDeviceToHost));
   for (int k = 0; k < nslot; k++)
-    if (got[k] != 2 * expect[k]) {
-      printf("slot %d: %d != %d\n", k, got[k], 2 * expect[k]);
+    if (got[k] != nrep * expect[k]) {
+      printf("slot %d: %d != %d\n", k, got[k], nrep * expect[k]);
       return 1;
     }
   printf("ok\n");
