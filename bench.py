@@ -284,7 +284,8 @@ def main():
     env.enable_graph(capture=True)
 
   def draw():
-    return 2.0 * torch.rand((args.num_envs, nact), device=device, generator=gen) - 1.0
+    # uniform[-1, 1) random actions, one kernel (2 * rand - 1 was three)
+    return torch.empty((args.num_envs, nact), device=device).uniform_(-1.0, 1.0, generator=gen)
 
   def one_step(a):
     if args.mode == "env":
@@ -369,6 +370,8 @@ def main():
       "config": {"workload": f"{args.task} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
                  "task": args.task, "num_envs_per_gpu": args.num_envs, "decimation": dec,
                  "parallelism": f"dp{world}", "mode": args.mode, "step_path": step_path,
+                 "kernels": ("specialised (csrc/specs.inc entry %d)" % sim.info()["spec"]
+                             if sim.info()["spec"] > 0 else "generic"),
                  "capacity": {"contacts_per_world": sim.nconmax, "rows_per_world": sim.njmax,
                               "asked": {"nconmax": env.cfg.sim.nconmax, "njmax": env.cfg.sim.njmax}}},
       "overflow": {"timed_steps": args.steps, "contact_overflow_events": int(dropped[0]),

@@ -119,7 +119,9 @@ int mjx_model_destroy(mjxModel* model);
  * reference's per-world budget, sim/sim.py:82-92); njmax: constraint rows per world.
  * Data starts at qpos0 (mj_resetData semantics). */
 int mjx_sim_create(const mjxModel* model, int nworld, int nconmax, int njmax, mjxSim** out);
-/* The same with a max capacity (nconmax <= nconmax_max <= 64, njmax <= njmax_max): the step
+/* The same with a max capacity (nconmax <= 64, nconmax <= nconmax_max <= 512, njmax <=
+ * njmax_max, and njmax_max >= nconmax_max past 64 contacts: every contact makes a row, so the
+ * reference's njmax bounds a world's contacts too): the step
  * runs at (nconmax, njmax) per world -- the fast LDS carve -- and a world whose contacts or
  * rows overflow it in a substep is re-solved at (nconmax_max, njmax_max) instead of
  * truncated (the reference's budget semantics: its nconmax is pooled, sim/sim.py:82-92; its

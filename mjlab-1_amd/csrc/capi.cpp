@@ -556,8 +556,11 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
   if (nconmax <= 0 || nconmax > mjx::kWave)
     return fail("nconmax (contacts held per world) must be in [1, 64]");
   if (njmax <= 0) return fail("njmax must be positive");
-  if (nconmax_max < nconmax || nconmax_max > mjx::kWave || njmax_max < njmax)
-    return fail("max capacity: nconmax <= nconmax_max <= 64 and njmax <= njmax_max");
+  if (nconmax_max < nconmax || nconmax_max > mjx::kMaxContacts || njmax_max < njmax)
+    return fail("max capacity: nconmax <= nconmax_max <= 512 and njmax <= njmax_max");
+  if (nconmax_max > mjx::kWave && nconmax_max > njmax_max)
+    return fail("a max capacity past 64 contacts needs njmax_max >= nconmax_max (the contact sort's "
+                "scratch is the row block)");
   HIPCHK(hipSetDevice(model->device));
   auto* s = new mjxSim_();
   s->model = model;

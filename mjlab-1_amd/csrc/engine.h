@@ -11,6 +11,10 @@
 namespace mjx {
 
 constexpr int kWave = 64;        // CDNA wavefront width
+// contacts per world: a fast carve holds at most one per lane (<= kWave); a max (re-solve)
+// carve up to kMaxContacts, kMaxConRounds per lane
+constexpr int kMaxConRounds = 8;
+constexpr int kMaxContacts = kWave * kMaxConRounds;
 constexpr int kBodyRec = 20, kDofRec = 12, kActRec = 4;  // ints per DModel record (int4-aligned)
 constexpr int kMaxBodies = 64;   // dof_bodymask is uint64
 constexpr int kMaxDof = 64;      // one lane per dof in the dof-parallel stages
@@ -200,6 +204,13 @@ constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;
 constexpr int kSelClr = 1 << 19;  // the re-solve launch that empties its list on exit
+// the fused class-chain launch (step_chain: one world's Newton, phase C and the next
+// substep's phase A back to back): kSelChainA runs that phase A, kSelNextLast marks the
+// next substep as the step's last; kSelFusedA: a phase A that follows phase C in the same
+// launch (it reads the state C just stored past the vector L1)
+constexpr int kSelChainA = 1 << 20;
+constexpr int kSelNextLast = 1 << 21;
+constexpr int kSelFusedA = 1 << 22;
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.

@@ -112,24 +112,25 @@ __global__ __launch_bounds__(kClassifyThreads) void classify_kernel(const Params
   }
 }
 
-// Generic kernels: one instantiation per (register-row length NR >= padded nv; phase).
-template <int NR>
-static StepFn phase_fn_nr(int ph) {
-  return phase_kernel<NR, 0>(ph);
-}
+// Generic kernels: one instantiation per (register-row length NR >= padded nv; phase), each
+// NR in its own object (generic.hip with -DMJX_GENERIC_NR, compiled in parallel).
+#define MJX_GENERIC_NRS(X) X(8) X(16) X(20) X(24) X(32) X(36) X(40) X(48) X(56) X(64)
+#define MJX_DECL_GENERIC(nr) StepFn generic_fn_##nr(int ph);
+MJX_GENERIC_NRS(MJX_DECL_GENERIC)
+#undef MJX_DECL_GENERIC
 static StepFn generic_fn(int nv, int ph) {
   // exact fits for the shipped robots (Go1 nvp 20, G1 nvp 36), multiples of 8 otherwise
   const int nvp = (nv + 3) & ~3;
-  if (nvp <= 8) return phase_fn_nr<8>(ph);
-  if (nvp <= 16) return phase_fn_nr<16>(ph);
-  if (nvp <= 20) return phase_fn_nr<20>(ph);
-  if (nvp <= 24) return phase_fn_nr<24>(ph);
-  if (nvp <= 32) return phase_fn_nr<32>(ph);
-  if (nvp <= 36) return phase_fn_nr<36>(ph);
-  if (nvp <= 40) return phase_fn_nr<40>(ph);
-  if (nvp <= 48) return phase_fn_nr<48>(ph);
-  if (nvp <= 56) return phase_fn_nr<56>(ph);
-  return phase_fn_nr<64>(ph);
+  if (nvp <= 8) return generic_fn_8(ph);
+  if (nvp <= 16) return generic_fn_16(ph);
+  if (nvp <= 20) return generic_fn_20(ph);
+  if (nvp <= 24) return generic_fn_24(ph);
+  if (nvp <= 32) return generic_fn_32(ph);
+  if (nvp <= 36) return generic_fn_36(ph);
+  if (nvp <= 40) return generic_fn_40(ph);
+  if (nvp <= 48) return generic_fn_48(ph);
+  if (nvp <= 56) return generic_fn_56(ph);
+  return generic_fn_64(ph);
 }
 
 // Model-specialised kernels (spec.hip, one object per specs.inc entry).
@@ -203,15 +204,31 @@ static size_t lds_bytes(const Params& host, int ph) {
 static size_t lds_resolve(const Params& host) {
   return std::max(lds_bytes(host, 0), std::max(lds_bytes(host, 1), lds_bytes(host, 2)));
 }
+// dynamic LDS of a class chain (step_chain): the class's Newton carve, phase C's and, when it
+// runs the next phase A, phase A's
+static size_t lds_chain(const Params& host, int cls, bool with_a) {
+  size_t b = std::max(lds_bytes(host, cls ? 2 + cls : 1), lds_bytes(host, 2));
+  return with_a ? std::max(b, lds_bytes(host, 0)) : b;
+}
+// MJX355_CHAIN=0: a class's B, C and next A as three launches (A/B diagnostic)
+static bool chain_env() {
+  static const bool on = [] {
+    const char* e = getenv("MJX355_CHAIN");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
 
 hipError_t prepare_step(const Params& host) {
   size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
   for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
-  for (int ph = 0; ph < 6; ph++) {  // phase codes of phase_kernel
-    const size_t need = ph == 5 ? lds_resolve(host) : shmem[ph == 3 ? 1 : ph == 4 ? 0 : ph];
-    if (need > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)step_fn(host, ph),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)need);
+  for (int ph = 0; ph < 8; ph++) {  // phase codes of phase_kernel
+    const size_t need = ph >= 5 ? std::max(shmem[0], std::max(shmem[1], shmem[2]))
+                                : shmem[ph == 3 ? 1 : ph == 4 ? 0 : ph];
+    const StepFn f = step_fn(host, ph);
+    if (need > 64 * 1024 && f) {
+      hipError_t e = hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)need);
       if (e != hipSuccess) return e;
     }
   }
@@ -458,8 +475,18 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         // (B span 240 -> 255 us, G1).
         e = hipEventRecord(side->fork[k], st);
         if (e != hipSuccess) return e;
-        // class c's stream: B, then (piped) C and the next substep's A of the same worlds
+        // class c's stream: B, then (piped) C and the next substep's A of the same worlds --
+        // as one launch (step_chain) unless MJX355_CHAIN=0
         auto class_chain = [&](hipStream_t cs, int cls) {
+          const StepFn fX = piped && chain_env() ? step_fn(host, cls == 0 && newton_lat() ? 7 : 6) : nullptr;
+          if (fX) {
+            const int selx = k | (cls + 1) << 8 | (last ? 0 : kSelChainA) |
+                             (((sub + 1) & 1) ? kSelAPar : 0) |
+                             (sub + 1 == nsubstep - 1 ? kSelNextLast : 0);
+            hipLaunchKernelGGL(fX, dim3(n), dim3(kWave), lds_chain(host, cls, !last), cs, dev, w0, w1,
+                               selx, last, integrate, mask);
+            return;
+          }
           hipLaunchKernelGGL(cls ? fB : fBL, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
                              cs, dev, w0, w1, k, last, cls, mask);
           if (!piped) return;

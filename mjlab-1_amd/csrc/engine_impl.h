@@ -1275,6 +1275,11 @@ template <int SP> struct ModelSpec {
 template <int SP> constexpr int spec_nr() { return nr_for_nv(ModelSpec<SP>::dims().nv); }
 // box-box narrowphase compiled in: generic kernels, and specialisations with such pairs
 template <int SP> constexpr bool kBoxBox = SP == 0 || ModelSpec<SP>::dims().nboxbox > 0;
+// at most one contact per lane of the world's wave (every fast carve, nconmax <= 64): the
+// contact loops of phases A and C are then the single lane-per-contact pass; a max carve past
+// 64 contacts (sim.max_capacity: the reference's njmax bounds a world's contacts too) takes
+// the multi-round forms (rank sort, contacts lane + 64 r)
+template <int SP> constexpr bool kCon1 = SP != 0 && ModelSpec<SP>::dims().nconmax <= kWave;
 template <int SP, int K> struct SpecLds {
   static constexpr Lds get() {
     constexpr Lds v = make_lds(ModelSpec<SP>::dims(), K);
@@ -1469,6 +1474,13 @@ __device__ __forceinline__ void dma_row(float* dst, const float* src, int n, int
   for (int i0 = 0; i0 < n; i0 += kWave)
     if (i0 + lane < n)
       __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + lane), (lds_void_t)(dst + i0), 4, 0, 0);
+}
+// the same through L2 only (sc0 | sc1: past the vector L1), for state a phase earlier in the
+// same launch stored (the L1 may still hold the lines that phase read before storing)
+__device__ __forceinline__ void dma_row_l2(float* dst, const float* src, int n, int lane) {
+  for (int i0 = 0; i0 < n; i0 += kWave)
+    if (i0 + lane < n)
+      __builtin_amdgcn_global_load_lds((glob_void_t)(src + i0 + lane), (lds_void_t)(dst + i0), 4, 0, 17);
 }
 __device__ __forceinline__ void lds_dma_wait() {
   __builtin_amdgcn_s_waitcnt(0);
@@ -1780,8 +1792,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       S[L.qfrc_act + i] = 0.f;
       S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f;
     }
-    dma_row(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
-    dma_row(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
+    if (sel & kSelFusedA) {  // step_chain: phase C stored this state in the same launch
+      dma_row_l2(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
+      dma_row_l2(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
+    } else {
+      dma_row(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
+      dma_row(S + L.qvel, D.qvel + (size_t)w * nv, nv, lane);
+    }
     // lane-aligned inputs stay in registers (lane u: ctrl[u], lane i: qfrc_applied[i])
     const float ctrl_u = lane < nu ? D.ctrl[(size_t)w * nu + lane] : 0.f;
     const float qapp_i = lane < nv ? D.qfrc_applied[(size_t)w * nv + lane] : 0.f;
@@ -2541,44 +2558,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     }
     sync();
     STAMP(3);
-    // deterministic order: bitonic sort of (key, slot) over 64 lanes, then permute
+    // deterministic order: bitonic sort of (key, slot) over 64 lanes, then permute (more than
+    // 64 contacts: a rank sort, the permutation applied field by field)
     int ncon = min(ints[0], d.nconmax);
     {
-      int key = lane < ncon ? Si[L.con_key + lane] : 0x7fffffff;
-      int idx = lane;
-#pragma unroll
-      for (int k = 2; k <= kWave; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          int pk = __shfl_xor(key, j);
-          int pi = __shfl_xor(idx, j);
-          bool up = (lane & k) == 0;
-          bool lower = (lane & j) == 0;
-          bool sw = lower ? (up ? key > pk : key < pk) : (up ? key < pk : key > pk);
-          if (sw) { key = pk; idx = pi; }
-        }
-      }
-      // lane holds the source slot of sorted position `lane`
-      int g1 = 0, g2 = 0;
-      float dist = 0, px = 0, py = 0, pz = 0, nx = 0, ny = 0, nz = 0;
-      if (lane < ncon) {
-        g1 = Si[L.con_g1 + idx]; g2 = Si[L.con_g2 + idx]; dist = S[L.con_dist + idx];
-        px = S[L.con_pos + 3 * idx]; py = S[L.con_pos + 3 * idx + 1]; pz = S[L.con_pos + 3 * idx + 2];
-        nx = S[L.con_n + 3 * idx]; ny = S[L.con_n + 3 * idx + 1]; nz = S[L.con_n + 3 * idx + 2];
-      }
-      sync();
-      if (lane < ncon) {
-        Si[L.con_g1 + lane] = g1; Si[L.con_g2 + lane] = g2; S[L.con_dist + lane] = dist;
-        {  // con_key is dead after the sort: it now holds the packed contact bodies
-          const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-          Si[L.con_key + lane] = b1 | b2 << 8 | m.body_rootid[b1] << 16 | m.body_rootid[b2] << 24;
-        }
-        S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
-        // contact frame (mju_makeFrame): the unit normal; tangents by cframe() at use
-        V3 n = {nx, ny, nz};
-        n = n * (1.0f / fmaxf(norm(n), MINVAL));
-        st3(S + L.con_n + 3 * lane, n);
-        // contact parameters (mj_contactParam semantics)
+      // contact parameters (mj_contactParam semantics) of sorted contact c
+      auto contact_params = [&](int c, int g1, int g2, float dist) {
         const float* fri = MF(geom_friction);
         const float* sref = MF(geom_solref);
         const float* simp = MF(geom_solimp);
@@ -2616,14 +2601,96 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           for (int i = 0; i < 5; i++) si[i] = mix * simp[5 * g1 + i] + (1 - mix) * simp[5 * g2 + i];
         }
         (void)f1;
-        S[L.con_mu + 2 * lane] = fmaxf(MINMU, f0);
-        S[L.con_mu + 2 * lane + 1] = fmaxf(MINMU, f0);
-        Si[L.con_dim + lane] = dim;
+        S[L.con_mu + 2 * c] = fmaxf(MINMU, f0);
+        S[L.con_mu + 2 * c + 1] = fmaxf(MINMU, f0);
+        Si[L.con_dim + c] = dim;
         const float imargin = fmaxf(gmar[g1], gmar[g2]) - fmaxf(ggap[g1], ggap[g2]);
-        S[L.con_imargin + lane] = imargin;
+        S[L.con_imargin + c] = imargin;
         // row impedance and reference K, B are per contact: computed once here
-        S[L.con_imp + lane] = impedance(si, dist, imargin);
-        solref_kb(sr, si, h, S[L.con_kb + 2 * lane], S[L.con_kb + 2 * lane + 1]);
+        S[L.con_imp + c] = impedance(si, dist, imargin);
+        solref_kb(sr, si, h, S[L.con_kb + 2 * c], S[L.con_kb + 2 * c + 1]);
+      };
+      // con_key is dead after the sort: it then holds the packed contact bodies
+      auto con_bodies = [&](int g1, int g2) {
+        const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        return b1 | b2 << 8 | m.body_rootid[b1] << 16 | m.body_rootid[b2] << 24;
+      };
+      if (kCon1<SP> || ncon <= kWave) {
+        int key = lane < ncon ? Si[L.con_key + lane] : 0x7fffffff;
+        int idx = lane;
+#pragma unroll
+        for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            int pk = __shfl_xor(key, j);
+            int pi = __shfl_xor(idx, j);
+            bool up = (lane & k) == 0;
+            bool lower = (lane & j) == 0;
+            bool sw = lower ? (up ? key > pk : key < pk) : (up ? key < pk : key > pk);
+            if (sw) { key = pk; idx = pi; }
+          }
+        }
+        // lane holds the source slot of sorted position `lane`
+        int g1 = 0, g2 = 0;
+        float dist = 0, px = 0, py = 0, pz = 0, nx = 0, ny = 0, nz = 0;
+        if (lane < ncon) {
+          g1 = Si[L.con_g1 + idx]; g2 = Si[L.con_g2 + idx]; dist = S[L.con_dist + idx];
+          px = S[L.con_pos + 3 * idx]; py = S[L.con_pos + 3 * idx + 1]; pz = S[L.con_pos + 3 * idx + 2];
+          nx = S[L.con_n + 3 * idx]; ny = S[L.con_n + 3 * idx + 1]; nz = S[L.con_n + 3 * idx + 2];
+        }
+        sync();
+        if (lane < ncon) {
+          Si[L.con_g1 + lane] = g1; Si[L.con_g2 + lane] = g2; S[L.con_dist + lane] = dist;
+          Si[L.con_key + lane] = con_bodies(g1, g2);
+          S[L.con_pos + 3 * lane] = px; S[L.con_pos + 3 * lane + 1] = py; S[L.con_pos + 3 * lane + 2] = pz;
+          // contact frame (mju_makeFrame): the unit normal; tangents by cframe() at use
+          V3 n = {nx, ny, nz};
+          n = n * (1.0f / fmaxf(norm(n), MINVAL));
+          st3(S + L.con_n + 3 * lane, n);
+          contact_params(lane, g1, g2, dist);
+        }
+      } else if constexpr (!kCon1<SP>) {
+        // rank sort (keys pair * 8 + k are distinct): sorted position of slot c = the number
+        // of keys below its own; perm[position] = slot in the row-id scratch (rows come later,
+        // the carve holds njmax >= nconmax of them)
+        int* perm = Si + L.efc_cid;
+        const int rounds = (ncon + kWave - 1) / kWave;
+        for (int c = lane; c < ncon; c += kWave) {
+          const int kc = Si[L.con_key + c];
+          int rank = 0;
+          for (int j = 0; j < ncon; j++) rank += Si[L.con_key + j] < kc ? 1 : 0;
+          perm[rank] = c;
+        }
+        sync();
+        // apply it field by field through registers (at most kMaxConRounds values per lane)
+        auto permute = [&](float* base, int stride, int comp) {
+          float v[kMaxConRounds];
+#pragma unroll
+          for (int r = 0; r < kMaxConRounds; r++) {
+            const int c = lane + r * kWave;
+            v[r] = r < rounds && c < ncon ? base[stride * perm[c] + comp] : 0.f;
+          }
+          sync();
+#pragma unroll
+          for (int r = 0; r < kMaxConRounds; r++) {
+            const int c = lane + r * kWave;
+            if (r < rounds && c < ncon) base[stride * c + comp] = v[r];
+          }
+          sync();
+        };
+        permute(reinterpret_cast<float*>(Si + L.con_g1), 1, 0);
+        permute(reinterpret_cast<float*>(Si + L.con_g2), 1, 0);
+        permute(S + L.con_dist, 1, 0);
+        for (int t = 0; t < 3; t++) permute(S + L.con_pos, 3, t);
+        for (int t = 0; t < 3; t++) permute(S + L.con_n, 3, t);
+        for (int c = lane; c < ncon; c += kWave) {
+          const int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
+          Si[L.con_key + c] = con_bodies(g1, g2);
+          V3 n = v3(S + L.con_n + 3 * c);
+          n = n * (1.0f / fmaxf(norm(n), MINVAL));
+          st3(S + L.con_n + 3 * c, n);
+          contact_params(c, g1, g2, S[L.con_dist + c]);
+        }
       }
       sync();
     }
@@ -2644,10 +2711,31 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         nlim_rows = (lim_mask & 1) + ((lim_mask >> 1) & 1);
       }
       int lim_total, lim_off = wave_excl_scan(nlim_rows, lane, &lim_total);
-      int cdim = lane < ncon ? Si[L.con_dim + lane] : 0;
-      int crow = lane < ncon ? (cdim == 1 ? 1 : 2 * (cdim - 1)) : 0;
-      if (lane < ncon && cdim != 1 && cdim != 3) atomicOr(&ints[3], 4);
-      int con_total, con_off = wave_excl_scan(crow, lane, &con_total);
+      // contact rows: one contact per lane (offsets by one wave scan), or -- past 64 contacts
+      // -- rounds of contacts lane + 64 r with a running carry, each contact's offset within
+      // the contact rows kept in con_efc (made absolute below)
+      const bool con1 = kCon1<SP> || ncon <= kWave;
+      int cdim = 0, crow = 0, con_total = 0, con_off = 0;
+      if (con1) {
+        cdim = lane < ncon ? Si[L.con_dim + lane] : 0;
+        crow = lane < ncon ? (cdim == 1 ? 1 : 2 * (cdim - 1)) : 0;
+        if (lane < ncon && cdim != 1 && cdim != 3) atomicOr(&ints[3], 4);
+        con_off = wave_excl_scan(crow, lane, &con_total);
+      } else {
+        for (int c0 = 0; c0 < ncon; c0 += kWave) {
+          const int c = c0 + lane;
+          const int cd = c < ncon ? Si[L.con_dim + c] : 0;
+          const int cr = c < ncon ? (cd == 1 ? 1 : 2 * (cd - 1)) : 0;
+          if (c < ncon && cd != 1 && cd != 3) atomicOr(&ints[3], 4);
+          int tot, off = wave_excl_scan(cr, lane, &tot);
+          if (c < ncon) Si[L.con_efc + c] = con_total + off;
+          con_total += tot;
+        }
+      }
+      auto con_rows = [&](int c) {
+        const int cd = Si[L.con_dim + c];
+        return cd == 1 ? 1 : 2 * (cd - 1);
+      };
       int nefc = lim_total + con_total;
       if (P->ovf_resolve) {
         // contacts or rows past this carve: list the world for the re-solve at full capacity
@@ -2676,14 +2764,23 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       }
       // contacts whose rows do not fit are dropped as whole contacts
       int keep_con = ncon;
-      {
+      if (con1) {
         bool fits = lane < ncon && lim_total + con_off + crow <= d.njmax;
         unsigned long long bal = __ballot(lane < ncon && !fits);
         if (bal) keep_con = __ffsll((long long)bal) - 1;
         keep_con = min(keep_con, ncon);
+        ncon = keep_con;
+        nefc = lim_total + (ncon > 0 ? __shfl(con_off + crow, ncon - 1) : 0);
+      } else {
+        for (int c0 = 0; c0 < ncon; c0 += kWave) {
+          const int c = c0 + lane;
+          const bool fits = c < ncon && lim_total + Si[L.con_efc + c] + con_rows(c) <= d.njmax;
+          const unsigned long long bal = __ballot(c < ncon && !fits);
+          if (bal) { keep_con = c0 + __ffsll((long long)bal) - 1; break; }
+        }
+        ncon = keep_con;
+        nefc = lim_total + (ncon > 0 ? Si[L.con_efc + ncon - 1] + con_rows(ncon - 1) : 0);
       }
-      ncon = keep_con;
-      nefc = lim_total + (ncon > 0 ? __shfl(con_off + crow, ncon - 1) : 0);
       if (lim_total > d.njmax) { nefc = 0; ncon = 0; }
       const float* dinvw = MF(dof_invweight0);
       const float* binvw = MF(body_invweight0);
@@ -2707,18 +2804,28 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       // and phase B factors it densely; otherwise the tree form (rows_chol_tree)
       bool xbranch = false;
       if constexpr (kTree<SP>) {
-        if (lane < ncon) {
-          const int cbk = Si[L.con_key + lane];
+        for (int c = lane; c < ncon; c += kWave) {
+          const int cbk = Si[L.con_key + c];
           const uint64_t m1 = m.body_dofmask[cb_b1(cbk)], m2 = m.body_dofmask[cb_b2(cbk)];
-          xbranch = (m1 & ~m2) != 0ull && (m2 & ~m1) != 0ull;
+          xbranch |= (m1 & ~m2) != 0ull && (m2 & ~m1) != 0ull;
         }
       }
       const int dense_h = __ballot(xbranch) != 0ull || !kTree<SP>;
-      if (lane < ncon) {
-        int r0 = lim_total + con_off;
-        Si[L.con_efc + lane] = r0;
-        for (int k = 0; k < crow; k++)
-          Si[L.efc_cid + r0 + k] = efc_code(cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, lane);
+      if (con1) {
+        if (lane < ncon) {
+          int r0 = lim_total + con_off;
+          Si[L.con_efc + lane] = r0;
+          for (int k = 0; k < crow; k++)
+            Si[L.efc_cid + r0 + k] = efc_code(cdim == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, lane);
+        }
+      } else {
+        for (int c = lane; c < ncon; c += kWave) {
+          const int r0 = lim_total + Si[L.con_efc + c];
+          const int cd = Si[L.con_dim + c];
+          Si[L.con_efc + c] = r0;
+          for (int k = 0; k < con_rows(c); k++)
+            Si[L.efc_cid + r0 + k] = efc_code(cd == 1 ? EFC_FRICTIONLESS : EFC_PYRAMIDAL, c);
+        }
       }
       sync();
       // Jacobian rows: lane per dof; when nvp <= 32 the wave holds kWave / nvp groups of nvp
@@ -2830,8 +2937,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
       // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
-      // there are more than 64 of them (no transposed masks)
-      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0) continue;
+      // there are more than 64 of them (no transposed masks) or more than 64 contacts
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0 &&
+          (kCon1<SP> || ncon <= kWave)) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -2980,7 +3088,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       }
       for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
       size_t wc = (size_t)w * P->con_stride;
-      for (int c = lane; c < P->con_stride; c += kWave) {
+      // contact slots: this output's contacts, and zeros over the previous output's past them
+      // (every slot beyond both is zero already: engine_counters [6] = slots this output
+      // touches, [7] = contacts it holds)
+      int* wsv = D.wstats + 8 * (size_t)w;
+      const int nout = min(P->con_stride, max(ncon, wsv[7]));
+      for (int c = lane; c < nout; c += kWave) {
         bool v = c < ncon;
         D.contact_dist[wc + c] = v ? S[L.con_dist + c] : 0.f;
         D.contact_geom[(wc + c) * 2] = v ? Si[L.con_g1 + c] : -1;
@@ -2990,7 +3103,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         const float fr[9] = {F.n.x, F.n.y, F.n.z, F.t.x, F.t.y, F.t.z, F.b.x, F.b.y, F.b.z};
         for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = v ? fr[t] : 0.f;
       }
-      if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; }
+      if (lane == 0) { D.ncon[w] = ncon; D.nefc[w] = nefc; wsv[6] = nout; wsv[7] = ncon; }
     }
     STAMP(12);
     // hand-off: B pack (J rows already written) and the A part of the C pack; the contact
@@ -3454,7 +3567,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
       // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
       // there are more than 64 of them (no transposed masks)
-      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0) continue;
+      if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0 &&
+          (kCon1<SP> || ncon <= kWave)) continue;
       if (type == SENS_GYRO || type == SENS_VELOCIMETER || type == SENS_ACCELEROMETER) {
         int b = m.site_bodyid[obj];
         const float* R = S + L.sxmat + 9 * obj;
@@ -3551,13 +3665,15 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
         }
       }
     }
-    contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon, lane);
+    if (kCon1<SP> || ncon <= kWave)
+      contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon, lane);
     STAMP(11);
     if (last) {
       size_t wb = (size_t)w * nb;
       for (int i = lane; i < 6 * nb; i += kWave) D.cacc[wb * 6 + i] = S[L.cacc + i];
       size_t wc = (size_t)w * P->con_stride;
-      for (int c = lane; c < P->con_stride; c += kWave) {
+      const int nout = min(P->con_stride, D.wstats[8 * (size_t)w + 6]);  // phase A's output slots
+      for (int c = lane; c < nout; c += kWave) {
         V3 f = {0, 0, 0};
         if (c < ncon && nefc > 0) {
           int r0 = Si[L.con_efc + c];
@@ -3748,10 +3864,47 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   ovf_clear_on_exit(P, sel);
 }
 
+// A row class's chain as ONE launch (MJX355_CHAIN, engine.hip class_chain): per world its
+// Newton (the class's carve; LAT: the latency form for the full-capacity class), its phase C
+// and -- kSelChainA -- the next substep's phase A, back to back in the workgroup, the packs
+// handed over through the per-world scratch as between launches.  A world then flows through
+// B -> C -> A on its own: the launch boundaries no longer make every world of the class wait
+// for the class's slowest Newton (7-10 iterations against a median of 3) before its phase C,
+// and for the slowest phase C before its next phase A.  sel: split | (class + 1) << 8 |
+// kSelChainA | kSelAPar (next A's list parity) | kSelNextLast; `integrate` as for phase C.
+// Between phases: a workgroup-scope release (this wave's pack stores complete before the
+// next phase's LDS-DMA reads them; one wave per workgroup, same CU) -- not an agent-scope
+// fence, whose L2 write-back cost the earlier fused C + A launch 24 %.
+__device__ __forceinline__ void chain_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+template <int NR, int SP, bool LAT>
+__global__ __launch_bounds__(kWave)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : (NR <= 48 ? 3 : 1), LAT ? 2 : 8))) void step_chain(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  const int bid = (int)blockIdx.x;
+  const int split = sel & 0xff;
+  const int cls1 = (sel >> 8) & 0xff;  // class + 1
+  step_body<NR, 1, SP, LAT>(S, P, w0, w1, split, last, cls1 - 1, mask, bid);
+  chain_handoff();
+  step_body<NR, 2, SP, false>(S, P, w0, w1, split | cls1 << 8, last, integrate, mask, bid);
+  if (sel & kSelChainA) {
+    chain_handoff();
+    step_body<NR, 0, SP, false>(S, P, w0, w1, split | cls1 << 8 | (sel & kSelAPar) | kSelFusedA,
+                                (sel & kSelNextLast) ? 1 : 0, integrate, mask, bid);
+  }
+}
+
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 
 // kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4: phase A over a re-solve list
-// (the fast carve's next substep), 5: a listed world's whole substep (step_resolve)
+// (the fast carve's next substep), 5: a listed world's whole substep (step_resolve); 6 / 7: a
+// row class's B -> C -> next A chain as one launch (step_chain; 7: the latency form)
 template <int NR, int SP>
 StepFn phase_kernel(int ph) {
   constexpr int role = SpecRole<SP>::mask;
@@ -3767,6 +3920,12 @@ StepFn phase_kernel(int ph) {
       else return nullptr;
     case 5:
       if constexpr ((role & 2) != 0) return step_resolve<NR, SP>;
+      else return nullptr;
+    case 6:
+      if constexpr ((role & 1) != 0) return step_chain<NR, SP, false>;
+      else return nullptr;
+    case 7:
+      if constexpr ((role & 1) != 0) return step_chain<NR, SP, true>;
       else return nullptr;
     default:
       return nullptr;

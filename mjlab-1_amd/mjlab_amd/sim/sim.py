@@ -210,26 +210,54 @@ def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   return ncon, rows
 
 
+MAX_CONTACTS = 512  # include/mjx355.h mjx_sim_create_ex: 8 contacts per lane of a world's wave
+
+
 def max_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
   """Per-world contacts / rows a world may reach before anything is dropped: a world that
   overflows the fast carve in a substep is re-solved at this capacity (mjx_sim_create_ex).
   The reference pools contacts over worlds ("one world may have more than nconmax",
   sim/sim.py:82-86) and bounds each world's rows by njmax (:87-91): here every world may
-  hold the engine's 64 contacts (one wave lane each) and njmax rows -- or, with njmax unset,
-  as many rows as 64 pyramidal contacts and every joint limit make.  MJX355_RESOLVE=0: no
-  re-solve (overflow drops contacts; diagnostic)."""
+  hold njmax rows and as many contacts as njmax rows allow (every contact makes at least one
+  row; condim-1 contacts make exactly one), up to MAX_CONTACTS -- or, with njmax unset, the
+  rows 64 pyramidal contacts and every joint limit make.  MJX355_RESOLVE=0: no re-solve
+  (overflow drops contacts; diagnostic)."""
   ncon, rows = world_capacity(cfg, model)
   if os.environ.get("MJX355_RESOLVE", "1") == "0" or os.environ.get("MJX355_WORLD_CAPACITY"):
     return ncon, rows
   nlim = int(np.sum(model.jnt_limited)) if model.njnt else 0
-  cmax = 64
-  rmax = 4 * cmax + 2 * nlim
-  if cfg.njmax is not None:
-    rmax = min(rmax, int(cfg.njmax))
-  return max(ncon, cmax), max(rows, rmax)
+  rmax = int(cfg.njmax) if cfg.njmax is not None else 4 * 64 + 2 * nlim
+  rmax = max(rows, rmax)
+  cmax = min(rmax, MAX_CONTACTS)
+  return max(ncon, cmax), rmax
 
 
 _capacity_warned: set = set()
+_generic_warned: set = set()
+
+
+class GenericKernelWarning(RuntimeWarning):
+  """The model has no compile-time specialised step kernels (csrc/specs.inc): it runs the
+  generic kernels, whose LDS offsets, loop bounds and dof-tree factor masks are run-time
+  values (mujoco_warp specialises any model when the graph is captured, sim/sim.py:164-191)."""
+
+
+def _warn_generic(model, info: dict) -> None:
+  if info["spec"] > 0 or os.environ.get("MJX355_NO_SPEC"):
+    return
+  key = (model.nq, model.nv, model.nbody, model.ngeom, model.nsensor, model.npair,
+         info["nconmax"], info["njmax"])
+  if key in _generic_warned:
+    return
+  _generic_warned.add(key)
+  import warnings
+  warnings.warn(
+      f"mjlab_amd.Simulation: no specialised step kernels for this model (nq {model.nq}, nv "
+      f"{model.nv}, nbody {model.nbody}, ngeom {model.ngeom}, nsensor {model.nsensor}, "
+      f"npair {model.npair}, capacity {info['nconmax']} contacts / {info['njmax']} rows): "
+      "running the generic kernels (measured slower on the shipped robots, DESIGN.md section "
+      "3). Add the model to mjlab-1_amd/csrc/specs.inc (scripts/gen_specs.py) and rebuild to "
+      "specialise it.", GenericKernelWarning, stacklevel=3)
 
 
 def _warn_capacity(cfg: SimulationCfg, model, ncon: int, rows: int) -> None:
@@ -291,6 +319,7 @@ class Simulation:
       # row classes has no re-solve: its max is the fast carve)
       info = self.info()
       self.nconmax, self.njmax = info["nconmax_max"], info["njmax_max"]
+      _warn_generic(model, info)
     _warn_capacity(cfg, model, self.nconmax, self.njmax)
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
                          for i in range(L.mjx_field_count(self._sim))}

@@ -38,7 +38,13 @@ def test_edited_scene_cfg_reaches_the_engine(gpu_device):
     secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "force"),
     reduce="netforce"),)
   cfg.events.pop("foot_friction")  # keep the edited friction (no startup randomisation)
-  env = ManagerBasedRlEnv(cfg, device=gpu_device)
+  # the edit adds sensors, so no specialised kernel set matches: the generic kernels run,
+  # and the user is told so (sim.GenericKernelWarning)
+  from mjlab_amd.sim.sim import GenericKernelWarning, _generic_warned
+  _generic_warned.clear()
+  with pytest.warns(GenericKernelWarning, match="no specialised step kernels"):
+    env = ManagerBasedRlEnv(cfg, device=gpu_device)
+  assert env.sim.info()["spec"] == 0
   env.reset()
   sim = env.sim
   base = load_scene("g1_velocity")

@@ -37,16 +37,20 @@ def test_engine_capacity_bounds():
 
 
 def test_max_capacity_is_the_resolve_carve(monkeypatch):
-  """An overflowing world is re-solved at 64 contacts and njmax rows (bounded by what 64
-  pyramidal contacts and every joint limit make); MJX355_RESOLVE=0 turns that off."""
+  """An overflowing world is re-solved at njmax rows and as many contacts (every contact makes
+  a row; the reference pools nconmax, sim/sim.py:82-93), at most MAX_CONTACTS; with njmax
+  unset, the rows 64 pyramidal contacts and every joint limit make.  MJX355_RESOLVE=0 turns
+  the re-solve off."""
+  from mjlab_amd.sim.sim import MAX_CONTACTS
   g1, go1 = load_scene("g1_velocity"), load_scene("go1_velocity")
   cfg = SimulationCfg(nconmax=35, njmax=300)
-  assert max_capacity(cfg, g1) == (64, 300)
-  assert max_capacity(cfg, go1) == (64, 4 * 64 + 2 * 12)
-  assert max_capacity(SimulationCfg(), g1) == (64, 4 * 64 + 2 * 29)
-  assert max_capacity(SimulationCfg(njmax=100), g1) == (64, 100)
+  assert max_capacity(cfg, g1) == (300, 300)
+  assert max_capacity(cfg, go1) == (300, 300)
+  assert max_capacity(SimulationCfg(), g1) == (4 * 64 + 2 * 29, 4 * 64 + 2 * 29)
+  assert max_capacity(SimulationCfg(njmax=100), g1) == (100, 100)
+  assert max_capacity(SimulationCfg(njmax=2000), g1) == (MAX_CONTACTS, 2000)
   from mjlab_amd.tracking import make_tracking_env_cfg
-  assert max_capacity(make_tracking_env_cfg().sim, load_scene("g1_tracking")) == (64, 250)
+  assert max_capacity(make_tracking_env_cfg().sim, load_scene("g1_tracking")) == (250, 250)
   monkeypatch.setenv("MJX355_RESOLVE", "0")
   assert max_capacity(cfg, g1) == (48, 160)
 
@@ -56,14 +60,14 @@ def test_specs_carry_the_task_capacities():
   caps = {}
   for mm in re.finditer(r"^MJX_SPEC\(\d+, (\w+),.*, (\d+), (\d+)\)$", text, re.M):
     caps.setdefault(mm.group(1), []).append((int(mm.group(2)), int(mm.group(3))))
-  assert caps["g1_tracking"] == [(64, 250), (48, 160)]
+  assert caps["g1_tracking"] == [(64, 250), (48, 160), (250, 250)]
   for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
-    assert caps[name] == [(48, 160), (64, 300)], name
+    assert caps[name] == [(48, 160), (300, 300)], name
   # Go1: its tasks' engine_capacity (24, 96) first, the default and the max carve
   from mjlab_amd.envs import unitree_go1_flat_env_cfg, unitree_go1_rough_env_cfg
   for name, make in (("go1_velocity", unitree_go1_flat_env_cfg),
                      ("go1_velocity_rough", unitree_go1_rough_env_cfg)):
-    assert caps[name] == [(24, 96), (48, 160), (64, 280)], name
+    assert caps[name] == [(24, 96), (48, 160), (300, 300)], name
     sim, go1 = make().sim, load_scene(name)
     assert world_capacity(sim, go1) == (24, 96)
-    assert max_capacity(sim, go1) == (64, 280)
+    assert max_capacity(sim, go1) == (300, 300)
