@@ -240,6 +240,9 @@ def main():
   ap.add_argument("--engine-capacity", default=None,
                   help="diagnostic: 'C,R' or 'none' overrides the task's SimulationCfg.engine_capacity "
                        "(the fast LDS carve; worlds past it are re-solved at the max capacity)")
+  ap.add_argument("--edited-scene", action="store_true",
+                  help="diagnostic: the G1 velocity task with tests/scene_edits.py's cfg.scene edit "
+                       "(no compiled specialisation matches it: run-time specialised kernels)")
   ap.add_argument("--allow-overflow", action="store_true",
                   help="exit 0 even if contacts were dropped in the timed steps")
   args = ap.parse_args()
@@ -263,7 +266,14 @@ def main():
   device = f"cuda:{local}"
 
   from mjlab_amd.envs import make_env
-  if args.engine_capacity is None:
+  if args.edited_scene:
+    from mjlab_amd.envs import ManagerBasedRlEnv
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+    from scene_edits import edited_g1_cfg
+    cfg = edited_g1_cfg(args.num_envs)
+    cfg.seed = mjdist.rank_seed(42, rank)
+    env = ManagerBasedRlEnv(cfg, device=device)
+  elif args.engine_capacity is None:
     env = make_env(args.task, num_envs=args.num_envs, device=device, seed=mjdist.rank_seed(42, rank))
   else:
     from mjlab_amd.envs import ManagerBasedRlEnv, load_env_cfg
@@ -367,11 +377,12 @@ def main():
       "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
       "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
       "data": "synthetic (random-init state from the compiled G1 MJCF; uniform random actions)",
-      "config": {"workload": f"{args.task} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
+      "config": {"workload": f"{args.task}{' (tests/scene_edits.py edit)' if args.edited_scene else ''} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
                  "task": args.task, "num_envs_per_gpu": args.num_envs, "decimation": dec,
                  "parallelism": f"dp{world}", "mode": args.mode, "step_path": step_path,
-                 "kernels": ("specialised (csrc/specs.inc entry %d)" % sim.info()["spec"]
-                             if sim.info()["spec"] > 0 else "generic"),
+                 "kernels": ("generic" if sim.info()["spec"] == 0 else
+                             "specialised at run time (mjlab_amd.jit)" if sim.info()["spec"] >= 1000
+                             else "specialised (csrc/specs.inc entry %d)" % sim.info()["spec"]),
                  "capacity": {"contacts_per_world": sim.nconmax, "rows_per_world": sim.njmax,
                               "asked": {"nconmax": env.cfg.sim.nconmax, "njmax": env.cfg.sim.njmax}}},
       "overflow": {"timed_steps": args.steps, "contact_overflow_events": int(dropped[0]),

@@ -194,6 +194,13 @@ int mjx_sim_profile(mjxSim* sim, uint64_t* out, void* stream);
  * kernels; -1 for a null sim.  No reference counterpart (mujoco_warp specialises by
  * tracing Python at graph-capture time, sim/sim.py:164-191). */
 int mjx_sim_spec(const mjxSim* sim);
+/* Load a run-time specialisation: `path` is a shared library built from csrc/jit.hip for one
+ * model's dims (mjlab_amd/jit.py compiles it with hipcc when a Simulation's model matches no
+ * compiled csrc/specs.inc entry, and caches it).  Returns the specialisation id (>= 1000; a sim
+ * created afterwards with those dims runs its kernels, mjx_sim_spec) or -1.  No reference
+ * counterpart: mujoco_warp specialises kernels for any model by tracing at graph-capture
+ * time (sim/sim.py:164-191); this is the AOT-compiled equivalent. */
+int mjx_spec_register(const char* path);
 /* Diagnostics: enqueue one empty kernel (`mjx::marker_kernel`, one wave, argument `tag`) on
  * `stream`.  bench.py brackets its timed region with tags 1 and 2 outside the timing, so a
  * rocprofv3 kernel trace or --pmc pass of the same command can attribute exactly the

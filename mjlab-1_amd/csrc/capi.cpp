@@ -4,6 +4,7 @@
 // DLPack aliases, and enqueues the engine kernels on the caller's HIP stream.  The
 // Python host mirror of mjlab.sim.Simulation (mjlab_amd/sim/sim.py) binds this with
 // ctypes; INTEGRATION.md shows the same binding for other hosts.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -932,6 +933,28 @@ int mjx_sim_profile(mjxSim* s, uint64_t* out, void* stream) {
 }
 
 int mjx_sim_spec(const mjxSim* s) { return s ? s->spec : -1; }
+
+int mjx_spec_register(const char* path) {
+  if (!path) return fail("null path");
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return fail(std::string("dlopen: ") + dlerror());
+  using AbiFn = int (*)(void);
+  using DimsFn = void (*)(mjx::Dims*);
+  using TreeFn = int (*)(int*, int);
+  using KernFn = mjx::StepFnPtr (*)(int);
+  auto abi = reinterpret_cast<AbiFn>(dlsym(h, "mjx_jit_abi"));
+  auto dims = reinterpret_cast<DimsFn>(dlsym(h, "mjx_jit_dims"));
+  auto tree = reinterpret_cast<TreeFn>(dlsym(h, "mjx_jit_tree"));
+  auto kern = reinterpret_cast<KernFn>(dlsym(h, "mjx_jit_kernel"));
+  if (!abi || !dims || !tree || !kern) return fail(std::string(path) + ": not a jit.hip library");
+  if (abi() != (int)sizeof(mjx::Dims)) return fail(std::string(path) + ": Dims layout mismatch (stale build)");
+  mjx::Dims d{};
+  dims(&d);
+  int par[64];
+  const int n = tree(par, 64);
+  if (n < 0 || n > 64) return fail("bad dof tree in the jit library");
+  return mjx::register_spec(d, par, n, kern);  // the library stays loaded for the process
+}
 
 int mjx_sim_mass_matrix(mjxSim* s, int big, float* out, void* stream) {
   if (!s || !out) return fail("null argument");

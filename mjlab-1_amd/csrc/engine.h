@@ -147,6 +147,11 @@ namespace mjx {
 // the dof tree (dof_parentid, for the tree-form SPD factors), else 0.
 constexpr int kMaxSpecs = 8;
 int find_spec(const Dims& d, const int* dof_parentid);
+// Specialisations compiled at run time (jit.hip, loaded by mjx_spec_register) get ids from
+// kRtSpecBase on; find_spec checks them after the compiled specs.inc entries.
+constexpr int kRtSpecBase = 1000;
+using StepFnPtr = void (*)(const struct Params*, int, int, int, int, int, const uint8_t*);
+int register_spec(const Dims& d, const int* par, int npar, StepFnPtr (*fn)(int));
 
 // Everything a launch needs, resident in device memory (read through the scalar cache
 // instead of occupying ~500 SGPRs of kernarg space).

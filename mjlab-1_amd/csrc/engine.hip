@@ -4,6 +4,8 @@
 // in engine_impl.h; spec.hip compiles them once per specs.inc entry.
 #include "engine_impl.h"
 
+#include <vector>
+
 namespace mjx {
 
 // --------------------------------------------------------------------------- reset
@@ -137,7 +139,25 @@ static StepFn generic_fn(int nv, int ph) {
 #define MJX_SPEC(id, scene, ...) StepFn spec_fn_##id(int ph);
 #include "specs.inc"
 #undef MJX_SPEC
+// Run-time specialisations (jit.hip libraries, mjx_spec_register): ids kRtSpecBase + i.
+struct RtSpec {
+  Dims d;
+  std::vector<int> par;
+  StepFn (*fn)(int);
+};
+static std::vector<RtSpec>& rt_specs() {
+  static std::vector<RtSpec> v;
+  return v;
+}
+int register_spec(const Dims& d, const int* par, int npar, StepFn (*fn)(int)) {
+  rt_specs().push_back(RtSpec{d, std::vector<int>(par, par + npar), fn});
+  return kRtSpecBase + (int)rt_specs().size() - 1;
+}
 static StepFn spec_fn(int spec, int ph) {
+  if (spec >= kRtSpecBase) {
+    const int i = spec - kRtSpecBase;
+    return i < (int)rt_specs().size() ? rt_specs()[i].fn(ph) : nullptr;
+  }
   switch (spec) {
 #define MJX_SPEC(id, scene, ...) case id: return spec_fn_##id(ph);
 #include "specs.inc"
@@ -182,6 +202,10 @@ int find_spec(const Dims& d, const int* dof_parentid) {
   if (eq(d, ModelSpec<id>::dims()) && same_tree(SpecTree<id>::par, SpecTree<id>::npar)) return id;
 #include "specs.inc"
 #undef MJX_SPEC
+  for (int i = 0; i < (int)rt_specs().size(); i++) {
+    const RtSpec& r = rt_specs()[i];
+    if (eq(d, r.d) && same_tree(r.par.data(), (int)r.par.size())) return kRtSpecBase + i;
+  }
   return 0;
 }
 
@@ -210,13 +234,22 @@ static size_t lds_chain(const Params& host, int cls, bool with_a) {
   size_t b = std::max(lds_bytes(host, cls ? 2 + cls : 1), lds_bytes(host, 2));
   return with_a ? std::max(b, lds_bytes(host, 0)) : b;
 }
-// MJX355_CHAIN=0: a class's B, C and next A as three launches (A/B diagnostic)
-static bool chain_env() {
-  static const bool on = [] {
+// Which class chains run as one launch (step_chain).  Default: the bulk class (the fewest
+// rows, most worlds, on the launch stream) when the batch is at most kChainMaxWorlds.
+// Measured (G1 4,096, two interleaved rounds on one box): bulk chained 2.81 M env-steps/s,
+// every class chained 2.70 M, none 2.67 M, only the heavy classes 2.58 M -- the heavy class's
+// latency kernel then runs its C and next A at one wave per SIMD; jump hfield at 16,384
+// worlds (five residency rounds, whose per-slot sums already average the Newton tails):
+// none 4.54 M, bulk 4.52 M, all 4.44 M.  MJX355_CHAIN (A/B diagnostic): 0 none, 1 every
+// class, 2 the bulk class at any batch size, 3 only the others.
+constexpr int kChainMaxWorlds = 8192;
+static bool chain_env(int cls, int nworld) {
+  static const int mode = [] {
     const char* e = getenv("MJX355_CHAIN");
-    return !e || atoi(e) != 0;
+    return e ? atoi(e) : -1;
   }();
-  return on;
+  if (mode < 0) return cls == 1 && nworld <= kChainMaxWorlds;
+  return mode == 1 || (mode == 2 && cls == 1) || (mode == 3 && cls != 1);
 }
 
 hipError_t prepare_step(const Params& host) {
@@ -478,7 +511,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         // class c's stream: B, then (piped) C and the next substep's A of the same worlds --
         // as one launch (step_chain) unless MJX355_CHAIN=0
         auto class_chain = [&](hipStream_t cs, int cls) {
-          const StepFn fX = piped && chain_env() ? step_fn(host, cls == 0 && newton_lat() ? 7 : 6) : nullptr;
+          const StepFn fX = piped && chain_env(cls, nworld) ? step_fn(host, cls == 0 && newton_lat() ? 7 : 6) : nullptr;
           if (fX) {
             const int selx = k | (cls + 1) << 8 | (last ? 0 : kSelChainA) |
                              (((sub + 1) & 1) ? kSelAPar : 0) |

@@ -1261,6 +1261,11 @@ __device__ __forceinline__ int efc_code(int type, int payload) { return type | p
 // and the three phase carves are returned BY VALUE from constexpr functions, so every
 // d.* bound and L.* LDS offset in the kernel folds to an immediate.  SP = 0 binds the
 // run-time Params copies (generic kernels for any model).
+// the specialisation table: csrc/specs.inc, or (a run-time JIT build, jit.hip) the one entry
+// generated for a model no shipped entry matches
+#ifndef MJX_SPECS_FILE
+#define MJX_SPECS_FILE "specs.inc"
+#endif
 template <int SP> struct ModelSpec {
   static constexpr bool on = false;
   static constexpr Dims dims() { return Dims{}; }
@@ -1270,7 +1275,7 @@ template <int SP> struct ModelSpec {
     static constexpr bool on = true;                                          \
     static constexpr Dims dims() { return Dims{__VA_ARGS__}; }                \
   };
-#include "specs.inc"
+#include MJX_SPECS_FILE
 #undef MJX_SPEC
 template <int SP> constexpr int spec_nr() { return nr_for_nv(ModelSpec<SP>::dims().nv); }
 // box-box narrowphase compiled in: generic kernels, and specialisations with such pairs
@@ -1346,14 +1351,14 @@ template <int SP> struct SpecTree {
     static constexpr int npar = sizeof(par) / sizeof(int);                    \
     static constexpr TreeChol get() { return make_tree_chol(par, npar); }     \
   };
-#include "specs.inc"
+#include MJX_SPECS_FILE
 #undef MJX_SPEC_TREE
 // which carve roles a specialisation serves (bit 0 fast, bit 1 max / re-solve): kernels of
 // the other role are not compiled for it (phase_kernel returns null; the generic stand in)
 template <int SP> struct SpecRole { static constexpr int mask = 3; };
 #define MJX_SPEC_ROLE(id, m)                                                  \
   template <> struct SpecRole<id> { static constexpr int mask = m; };
-#include "specs.inc"
+#include MJX_SPECS_FILE
 #undef MJX_SPEC_ROLE
 // the tree form is compiled for a specialisation whose dof tree is known and matches its nv
 template <int SP> constexpr bool kTree =

@@ -20,7 +20,7 @@ EXPORTS = ("mjx_last_error", "mjx_abi_version", "mjx_model_desc_size", "mjx_mode
            "mjx_reset", "mjx_field", "mjx_field_count", "mjx_field_name", "mjx_expand_field",
            "mjx_field_is_expanded", "mjx_sim_stats", "mjx_sim_profile", "mjx_sim_spec",
            "mjx_forward_masked", "mjx_sim_track_air_time", "mjx_marker", "mjx_sim_create_ex",
-           "mjx_sim_info", "mjx_sim_mass_matrix",
+           "mjx_sim_info", "mjx_sim_mass_matrix", "mjx_spec_register",
            # include/mjx355_task.h (fused velocity-task managers; bound in fused.py)
            "mjx_task_create", "mjx_task_destroy", "mjx_task_action", "mjx_task_substep",
            "mjx_task_post", "mjx_task_reset", "mjx_task_observe", "mjx_task_desc_size",
@@ -69,6 +69,8 @@ def lib() -> ctypes.CDLL:
   L.mjx_sim_spec.argtypes = [vp]
   L.mjx_sim_spec.restype = ctypes.c_int
   L.mjx_sim_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), vp]
+  if hasattr(L, "mjx_spec_register"):
+    L.mjx_spec_register.argtypes = [ctypes.c_char_p]
   if hasattr(L, "mjx_sim_mass_matrix"):
     L.mjx_sim_mass_matrix.argtypes = [vp, ci, vp, vp]
   if hasattr(L, "mjx_marker"):

@@ -184,6 +184,13 @@ class SimulationCfg:
   velocity and jump worlds reach; the rare world past it is re-solved at the max capacity
   (`max_capacity`: 64 contacts, `njmax` rows) within the same substep.  A task whose worlds
   reach it often may hold the reference's `njmax` here instead (tracking: (64, 256))."""
+  specialize: Literal["auto", "always", "never"] = "auto"
+  """Kernels for a model no compiled specialisation (csrc/specs.inc) matches (this build's
+  knob; mujoco_warp specialises any model at capture, sim/sim.py:164-191): compile them at
+  Simulation creation (`mjlab_amd.jit`, hipcc, cached by model and sources) -- "always";
+  "auto": load a cached build, and compile one for batches of at least JIT_MIN_WORLDS (a
+  compile takes ~40 s); "never": load and compile nothing (a specialisation another sim
+  already loaded into the process still matches).  MJX355_JIT=0/1 overrides."""
   mujoco: MujocoCfg = field(default_factory=MujocoCfg)
   nan_guard: NanGuardCfg = field(default_factory=NanGuardCfg)
 
@@ -211,6 +218,7 @@ def world_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
 
 
 MAX_CONTACTS = 512  # include/mjx355.h mjx_sim_create_ex: 8 contacts per lane of a world's wave
+JIT_MIN_WORLDS = 1024  # SimulationCfg.specialize "auto": compile kernels for batches this large
 
 
 def max_capacity(cfg: SimulationCfg, model) -> tuple[int, int]:
@@ -319,6 +327,13 @@ class Simulation:
       # row classes has no re-solve: its max is the fast carve)
       info = self.info()
       self.nconmax, self.njmax = info["nconmax_max"], info["njmax_max"]
+      if self._specialise(cfg, model, info):
+        check(L.mjx_sim_destroy(self._sim))
+        self._sim = ctypes.c_void_p()
+        check(L.mjx_sim_create_ex(self._model_ptr, self.num_envs, self.fast_capacity[0],
+                                  self.fast_capacity[1], self.nconmax, self.njmax,
+                                  ctypes.byref(self._sim)))
+        info = self.info()
       _warn_generic(model, info)
     _warn_capacity(cfg, model, self.nconmax, self.njmax)
     self._field_names = {L.mjx_field_name(self._sim, i).decode()
@@ -503,6 +518,32 @@ class Simulation:
     check(lib().mjx_sim_stats(self._sim, out, _stream_handle(self._torch_device)))
     return dict(max_ncon=out[0], max_nefc=out[1], con_overflow=out[2], row_overflow=out[3],
                 unsupported=out[4], max_niter=out[5], resolved=out[6])
+
+  def _specialise(self, cfg: SimulationCfg, model, info: dict) -> bool:
+    """Load (or build) run-time specialised kernels for the carves no compiled specs.inc
+    entry matched (mjlab_amd.jit); True when the sim must be created again to pick them up."""
+    policy = cfg.specialize
+    env = os.environ.get("MJX355_JIT")
+    if env is not None:
+      policy = "always" if env != "0" else "never"
+    if policy == "never" or os.environ.get("MJX355_NO_SPEC"):
+      return False
+    from .. import jit
+    want = []
+    if info["spec"] == 0:
+      want.append((info["nconmax"], info["njmax"], 1))
+    if info["spec_max"] == 0 and (info["nconmax_max"], info["njmax_max"]) != (info["nconmax"], info["njmax"]):
+      want.append((info["nconmax_max"], info["njmax_max"], 2))
+    if not want:
+      return False
+    compile_ok = policy == "always" or self.num_envs >= JIT_MIN_WORLDS
+    loaded = False
+    for ncon, rows, role in want:
+      path = jit.ensure_library(model, ncon, rows, role, compile_ok=compile_ok)
+      if path is not None:
+        jit.register(path)
+        loaded = True
+    return loaded
 
   def info(self) -> dict:
     """Capacities and kernels (mjx_sim_info)."""

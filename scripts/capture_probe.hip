@@ -12,6 +12,8 @@
 //           the class joins -- round 4's crashing topology (origin -> class streams + re-solve
 //           stream, flat forks); its chain is 3 launches (+ the next A when piped)
 //  32 replays: replay the instantiated graph 50 times instead of 2
+//  64 r4 chain: the re-solve chain as round 4 launched it -- max A, Newton, C, the next A
+//           (piped) and a one-thread list-clear kernel (5 launches per substep)
 //
 // Topology per substep (as launch_step): origin --split_fork--> split streams; on split
 // stream k: [A] -> classify -> record fork[k] -> class streams wait -> class chains
@@ -143,6 +145,10 @@ static int probe(int nsplit, int nc, int nsub, int piped, int shared, int feat, 
           launch(ovf[k], 40 + 4 * k + 1);  // latency Newton
           launch(ovf[k], 40 + 4 * k + 2);  // C
           if (piped && !last) launch(ovf[k], 40 + 4 * k + 3);  // next A
+          if (feat & 64) {  // round 4's list clear: a one-thread kernel
+            hipLaunchKernelGGL(work, dim3(1), dim3(1), 0, ovf[k], slots + 60 + k);
+            if (counting) expect[60 + k]++;
+          }
         }
         CK(hipEventRecord(fork[k], st));
         for (int c = 0; c < nc; c++) {

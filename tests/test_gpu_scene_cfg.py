@@ -10,41 +10,38 @@ import torch
 import oracle_lib as ol
 from parity_util import expanded_fields, world_model
 from test_gpu_rollout_parity import _OUT, _STATE, _check_step, _snap
+from scene_edits import edited_g1_cfg
 from test_gpu_config1 import _stats
 
 pytestmark = pytest.mark.gpu
 
 
-def test_edited_scene_cfg_reaches_the_engine(gpu_device):
-  from mjlab_amd.envs import ManagerBasedRlEnv, load_env_cfg
-  from mjlab_amd.scenes import load_scene
-  from mjlab_amd.sensor import ContactMatch, ContactSensorCfg
-  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
-  cfg.scene.num_envs = 16
-  cfg.seed = 3
-  robot = cfg.scene.entities["robot"]
-  base_fn = robot.spec_fn
-
-  def heavier_torso():
-    spec = base_fn()
-    spec.body("torso_link").mass = spec.body("torso_link").mass + 2.5
-    return spec
-
-  robot.spec_fn = heavier_torso
-  robot.collisions[0].friction[r"^(left|right)_foot[1-7]_collision$"] = (0.9,)
-  cfg.scene.sensors = cfg.scene.sensors + (ContactSensorCfg(
-    name="hands", primary=ContactMatch(mode="body", entity="robot",
-                                       pattern=r"^(left|right)_wrist_yaw_link$"),
-    secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "force"),
-    reduce="netforce"),)
-  cfg.events.pop("foot_friction")  # keep the edited friction (no startup randomisation)
-  # the edit adds sensors, so no specialised kernel set matches: the generic kernels run,
-  # and the user is told so (sim.GenericKernelWarning)
+def test_edited_scene_generic_kernels_warn(gpu_device):
+  """specialize="never": the generic kernels run, and the user is told so.  (First in this
+  file: the next test loads the run-time specialisation, which any later sim of these dims
+  in the process then matches.)"""
+  from mjlab_amd.envs import ManagerBasedRlEnv
   from mjlab_amd.sim.sim import GenericKernelWarning, _generic_warned
+  cfg = edited_g1_cfg(16)
+  cfg.sim.specialize = "never"
   _generic_warned.clear()
   with pytest.warns(GenericKernelWarning, match="no specialised step kernels"):
     env = ManagerBasedRlEnv(cfg, device=gpu_device)
   assert env.sim.info()["spec"] == 0
+
+
+
+def test_edited_scene_cfg_reaches_the_engine(gpu_device):
+  from mjlab_amd.envs import ManagerBasedRlEnv
+  from mjlab_amd.scenes import load_scene
+  cfg = edited_g1_cfg(16)
+  # the edit adds sensors, so no compiled specs.inc entry matches: the kernels specialised for
+  # it at run time (mjlab_amd.jit; __graft_entry__.build() compiled them into the in-tree
+  # cache, so no compile happens here)
+  cfg.sim.specialize = "always"
+  env = ManagerBasedRlEnv(cfg, device=gpu_device)
+  info = env.sim.info()
+  assert info["spec"] >= 1000 and info["spec_max"] >= 1000, info  # run-time specialisations
   env.reset()
   sim = env.sim
   base = load_scene("g1_velocity")
