@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MJX_ABI_VERSION 3
+#define MJX_ABI_VERSION 4
 
 /* geom types (MuJoCo mjtGeom numbering) */
 enum { MJX_GEOM_PLANE = 0, MJX_GEOM_HFIELD = 1, MJX_GEOM_SPHERE = 2, MJX_GEOM_CAPSULE = 3,
@@ -59,6 +59,9 @@ typedef struct mjxModelDesc_ {
   int nhfield, nhfielddata, nlevel;
   int nmaskword; /* 32-bit words per contact-sensor geom mask: ceil(ngeom / 32) */
   int iterations, ls_iterations, integrator, cone;
+  /* contact sensors: matches per sensor and world considered, the first contact_maxmatch in
+   * contact order (>= 1; SimulationCfg.contact_sensor_maxmatch, sim/sim.py:95,141) */
+  int contact_maxmatch;
   double timestep, tolerance, ls_tolerance, impratio, meaninertia;
   double gravity[3];
   /* bodies */

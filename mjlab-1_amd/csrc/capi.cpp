@@ -216,6 +216,7 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   if (desc->nu > mjx::kMaxLanes || desc->njnt > mjx::kMaxLanes)
     return fail("at most 64 actuators and 64 joints per world supported");
   if (desc->cone != 0) return fail("only pyramidal cones are supported");
+  if (desc->contact_maxmatch < 1) return fail("contact_maxmatch must be >= 1");
   HIPCHK(hipSetDevice(device));
   auto* m = new mjxModel_();
   m->device = device;
@@ -237,6 +238,7 @@ int mjx_model_create(const mjxModelDesc* desc, int device, mjxModel** out) {
   for (int i = 0; i < 3; i++) o.gravity[i] = (float)desc->gravity[i];
   o.iterations = desc->iterations; o.ls_iterations = desc->ls_iterations;
   o.integrator = desc->integrator; o.cone = desc->cone;
+  o.maxmatch = desc->contact_maxmatch;
 
   auto upload = [&](const void* src, size_t bytes, void** dst) -> int {
     size_t nb = bytes > 0 ? bytes : 4;

@@ -51,6 +51,7 @@ struct Opt {
   float timestep, tolerance, ls_tolerance, impratio, meaninertia;
   float gravity[3];
   int iterations, ls_iterations, integrator, cone;
+  int maxmatch;  // contact-sensor matches per sensor and world (the first ones in contact order)
 };
 
 // Device model: int fields shared, float fields with a per-world stride (0 = shared).

@@ -1600,7 +1600,7 @@ __device__ __forceinline__ V3 point_vel_r(const float* S, const Lds& L, int b, i
 // lowest contact index).
 __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* Si, const Lds& L,
                                                      const DModel& m, const Dims& d, float* sd,
-                                                     int ncon, int lane) {
+                                                     int ncon, int maxmatch, int lane) {
   const int c = lane;
   const bool valid = c < ncon;
   V3 fg = {0, 0, 0}, fc = {0, 0, 0};
@@ -1638,12 +1638,16 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
   // of matching contacts is the output whatever the reduce, so each costs one ballot and
   // popcount kept in its own lane, and all of them go out in one store at the end
   const bool fonly = lane < ncs && dbits == 1 && ddim == 1;
+  // contact_sensor_maxmatch below the contact count: a sensor keeps its first maxmatch
+  // matching contacts (lanes), as the serial form does
+  const bool mtrunc = maxmatch < ncon;
+  const uint64_t below = (1ull << lane) - 1ull;
   const uint64_t mm = m1 | m2;
   float fcount = 0.f;
   uint64_t rest = __ballot(lane < ncs && !fonly);
   for (uint64_t fo = __ballot(fonly); fo; fo &= fo - 1) {
     const int k = __ffsll((long long)fo) - 1;
-    const float f = (float)__popcll(__ballot((mm >> k) & 1ull));
+    const float f = (float)min(__popcll(__ballot((mm >> k) & 1ull)), maxmatch);
     fcount = lane == k ? f : fcount;
   }
   if (fonly) sd[dadr] = fcount;
@@ -1652,7 +1656,12 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     const int bits = __builtin_amdgcn_readlane(dbits, k), reduce = __builtin_amdgcn_readlane(dred, k);
     const int adr = __builtin_amdgcn_readlane(dadr, k), dim = __builtin_amdgcn_readlane(ddim, k);
     float* out = sd + adr;
-    const bool a1 = (m1 >> k) & 1ull, a2 = (m2 >> k) & 1ull;
+    bool a1 = (m1 >> k) & 1ull, a2 = (m2 >> k) & 1ull;
+    if (mtrunc) {
+      const bool keep = __popcll(__ballot(a1 || a2) & below) < maxmatch;
+      a1 = a1 && keep;
+      a2 = a2 && keep;
+    }
     const bool match = a1 || a2;
     const unsigned long long bal = __ballot(match);
     const float found = (float)__popcll(bal);
@@ -2991,6 +3000,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
           bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
           if (!a1 && !a2) continue;
+          if (found >= o.maxmatch) continue;  // contact_sensor_maxmatch: the first matches only
           found++;
           // contact force in contact frame
           int r0 = Si[L.con_efc + c];
@@ -3620,6 +3630,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           bool a1 = ((mk1[g1 >> 5] >> (g1 & 31)) & 1u) && ((mk2[g2 >> 5] >> (g2 & 31)) & 1u);
           bool a2 = ((mk1[g2 >> 5] >> (g2 & 31)) & 1u) && ((mk2[g1 >> 5] >> (g1 & 31)) & 1u);
           if (!a1 && !a2) continue;
+          if (found >= o.maxmatch) continue;  // contact_sensor_maxmatch: the first matches only
           found++;
           // contact force in contact frame
           int r0 = Si[L.con_efc + c];
@@ -3671,7 +3682,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       }
     }
     if (kCon1<SP> || ncon <= kWave)
-      contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon, lane);
+      contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon,
+                           o.maxmatch, lane);
     STAMP(11);
     if (last) {
       size_t wb = (size_t)w * nb;

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _I = ctypes.POINTER(ctypes.c_int32)
 _D = ctypes.POINTER(ctypes.c_double)
 _U64 = ctypes.POINTER(ctypes.c_uint64)
@@ -19,7 +19,7 @@ _U32 = ctypes.POINTER(ctypes.c_uint32)
 
 _INT_SCALARS = ["nq", "nv", "nu", "nbody", "njnt", "ngeom", "nsite", "nsensor", "nsensordata",
                 "npair", "nhfield", "nhfielddata", "nlevel", "nmaskword", "iterations", "ls_iterations",
-                "integrator", "cone"]
+                "integrator", "cone", "contact_maxmatch"]
 _REAL_SCALARS = ["timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia"]
 # (name, ctype) in header order
 _ARRAYS = (

@@ -195,6 +195,7 @@ class Model:
   impratio: float = 1.0
   integrator: int = 1      # 0 euler, 1 implicitfast
   cone: int = 0            # 0 pyramidal, 1 elliptic (unsupported)
+  contact_maxmatch: int = 64  # SimulationCfg.contact_sensor_maxmatch (sim/sim.py:95,141)
   solver: int = 2          # 2 newton
   meaninertia: float = 1.0
   arrays: dict = field(default_factory=dict)

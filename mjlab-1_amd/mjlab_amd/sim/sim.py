@@ -178,6 +178,9 @@ class SimulationCfg:
   """Constraint rows per world: the max capacity a world is re-solved at."""
   ls_parallel: bool = True  # accepted for API compatibility; the line search is exact
   contact_sensor_maxmatch: int = 64
+  """Contact-sensor matches recorded per sensor and world (`sim/sim.py:95,141`): a sensor
+  reduces over its first contact_sensor_maxmatch matching contacts in contact order (the
+  reference records the first that reach its atomic counter) and counts only those."""
   engine_capacity: tuple[int, int] | None = None
   """(contacts, rows) per world of the fast LDS carve every substep runs in (this build's
   knob, not the reference's).  None: 48 contacts and at most 160 rows, far above what the
@@ -303,6 +306,9 @@ class Simulation:
                                       torch.cuda.current_device())
     self._mj_model = model
     cfg.mujoco.apply(self._mj_model)
+    if int(cfg.contact_sensor_maxmatch) < 1:
+      raise ValueError(f"contact_sensor_maxmatch must be >= 1, got {cfg.contact_sensor_maxmatch}")
+    model.contact_maxmatch = int(cfg.contact_sensor_maxmatch)
     L = lib()
     desc, keep = make_desc(model)
     self._model_ptr = ctypes.c_void_p()

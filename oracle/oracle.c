@@ -1452,6 +1452,9 @@ static void sensors(const mjxModelDesc* m, orcData* d) {
           int a1 = in_mask(mk1, con->geom1) && in_mask(mk2, con->geom2);
           int a2 = in_mask(mk1, con->geom2) && in_mask(mk2, con->geom1);
           if (!a1 && !a2) continue;
+          /* SimulationCfg.contact_sensor_maxmatch (sim/sim.py:95,141): mujoco_warp records at
+           * most maxmatch matches per sensor and world; here the first ones in contact order */
+          if (found >= m->contact_maxmatch) continue;
           found++;
           double sg = a1 ? 1.0 : -1.0;
           double f[6], fg[3];

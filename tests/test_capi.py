@@ -62,7 +62,7 @@ def test_abi_version_and_desc_layout(lib):
   lib.mjx_model_desc_size.restype = ctypes.c_size_t
   lib.mjx_task_desc_size.restype = ctypes.c_size_t
   from mjlab_amd._capi import ABI_VERSION
-  assert lib.mjx_abi_version() == ABI_VERSION == 3
+  assert lib.mjx_abi_version() == ABI_VERSION == 4
   assert lib.mjx_model_desc_size() == ctypes.sizeof(ModelDesc)
   assert lib.mjx_task_desc_size() == ctypes.sizeof(TaskDesc)
 

@@ -103,3 +103,43 @@ def test_step_parity(scene, gpu_device):
     niter_equal += int(niter[i]) == r["niter"]
   assert ncontact_worlds > 0
   assert niter_equal >= 0.9 * n
+
+
+@pytest.mark.parametrize("maxmatch", [1, 3])
+def test_contact_sensor_maxmatch(maxmatch, gpu_device):
+  """SimulationCfg.contact_sensor_maxmatch (`sim/sim.py:95,141`) reaches the engine: each
+  contact sensor reduces over (and counts) its first `maxmatch` matching contacts.  The G1
+  foot sensors (found + net force over each foot's 4-14 contacts) then differ from the
+  64-match values, and the engine matches the oracle run with the same cap."""
+  from mjlab_amd.scenes import load_scene
+  from mjlab_amd.sim import MujocoCfg, Simulation, SimulationCfg
+  n = 48
+  m = load_scene("g1_velocity")
+  cfg = SimulationCfg(nconmax=48, njmax=160, contact_sensor_maxmatch=maxmatch,
+                      mujoco=MujocoCfg(timestep=m.timestep, iterations=10, ls_iterations=20))
+  sim = Simulation(n, cfg, m, gpu_device)
+  assert m.contact_maxmatch == maxmatch
+  q, qv, ctrl = g1_states(m, n, seed=2)
+  _load(sim, q, qv, ctrl)
+  sim.step()
+  torch.cuda.synchronize()
+  ref = oracle_step(m, q, qv, np.zeros_like(qv), ctrl, step=True)
+  m.contact_maxmatch = 64
+  full = oracle_step(m, q, qv, np.zeros_like(qv), ctrl, step=True)
+  d = sim.data
+  ncon = d.ncon.cpu().numpy()
+  sens = d.sensordata.cpu().numpy()
+  truncated = 0
+  for i, r in enumerate(ref):
+    assert ncon[i] == r["ncon"], f"world {i}: ncon {ncon[i]} vs {r['ncon']}"
+    ssc = max(1.0, np.abs(r["sensordata"]).max())
+    np.testing.assert_allclose(sens[i], r["sensordata"], atol=3e-3 * ssc, err_msg=f"sens {i}")
+    truncated += not np.allclose(r["sensordata"], full[i]["sensordata"])
+  assert truncated > n // 4
+
+
+def test_contact_sensor_maxmatch_rejects_zero(gpu_device):
+  from mjlab_amd.scenes import load_scene
+  from mjlab_amd.sim import Simulation, SimulationCfg
+  with pytest.raises(ValueError, match="contact_sensor_maxmatch"):
+    Simulation(4, SimulationCfg(contact_sensor_maxmatch=0), load_scene("g1_velocity"), gpu_device)

@@ -155,3 +155,32 @@ def test_rollout_independent_of_thread_count(go1):
   np.testing.assert_array_equal(res[0][0], res[1][0])
   np.testing.assert_array_equal(res[0][1], res[1][1])
   np.testing.assert_allclose(res[0][2], 20 * m.timestep)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5])
+def test_contact_sensor_maxmatch_counts(k):
+  """contact_sensor_maxmatch (sim/sim.py:95,141): a `found` sensor reports min(matches, k)
+  and a sensor whose matches fit under k is unchanged."""
+  from parity_util import g1_states, oracle_step
+  m = load_scene("g1_velocity")
+  n = 16
+  q, qv, c = g1_states(m, n, seed=2)
+  full = oracle_step(m, q, qv, np.zeros_like(qv), c, step=False)
+  m.contact_maxmatch = k
+  cap = oracle_step(m, q, qv, np.zeros_like(qv), c, step=False)
+  st = np.asarray(m.arrays["sensor_type"]).ravel()
+  ip = np.asarray(m.arrays["sensor_intprm"]).reshape(-1, 3)
+  adr = np.asarray(m.arrays["sensor_adr"]).ravel()
+  dim = np.asarray(m.arrays["sensor_dim"]).ravel()
+  fsens = [s for s in range(m.nsensor) if st[s] == 4 and ip[s, 0] & 1]
+  assert fsens
+  capped = 0
+  for a, b in zip(full, cap):
+    for s in fsens:
+      nf = a["sensordata"][adr[s]]
+      assert b["sensordata"][adr[s]] == min(nf, k)
+      capped += nf > k
+      if nf <= k:  # every match kept: the whole sensor is unchanged
+        np.testing.assert_array_equal(a["sensordata"][adr[s]:adr[s] + dim[s]],
+                                      b["sensordata"][adr[s]:adr[s] + dim[s]])
+  assert capped > 0
