@@ -249,3 +249,78 @@ def test_box_edge_across_a_box_edge():
   ex = np.array([np.cos(0.3), 0.0, -np.sin(0.3)])                 # moving edge direction
   n = c[6:9]
   assert abs(n[1]) < 1e-9 and abs(n @ ex) < 1e-9 and n[2] > 0.5   # normal to both edges
+
+
+def _exact_capsule_box(c, a, hl, s):
+  """min over the segment c + t a (|t| <= hl) of the box signed distance (box frame, half
+  sizes s), fp64: dense samples, then golden refinement in the best bracket; returns
+  (distance, t) -- an oracle-independent restatement of what MuJoCo's first capsule-box
+  contact reports (the sphere at the segment point closest to the box)."""
+  def sd(t):
+    q = c[None, :] + np.atleast_1d(t)[:, None] * a[None, :]
+    d = np.abs(q) - s
+    out = np.linalg.norm(np.maximum(d, 0.0), axis=1) + np.minimum(d.max(axis=1), 0.0)
+    return out
+  ts = np.linspace(-hl, hl, 4001)
+  v = sd(ts)
+  k = int(np.argmin(v))
+  lo, hi = ts[max(k - 1, 0)], ts[min(k + 1, len(ts) - 1)]
+  for _ in range(80):
+    m1, m2 = lo + (hi - lo) * 0.382, lo + (hi - lo) * 0.618
+    if sd(m1)[0] <= sd(m2)[0]:
+      hi = m2
+    else:
+      lo = m1
+  t = 0.5 * (lo + hi)
+  cand = [(float(sd(t)[0]), t), (float(v[k]), ts[k])]
+  return min(cand)
+
+
+def test_capsule_box_deepest_contact_is_the_exact_distance():
+  """Against random capsule poses over the box's top face, its +x edge and its corner (the
+  stair geometry: axis-aligned boxes under foot capsules), the deepest contact's depth is
+  the exact capsule-box distance minus the radius, to 1e-4 (this build's tie band: an
+  interior segment point is used when it is deeper than both ends by 1e-4) and to 1e-8
+  where the interior point is clearly deeper and outside the box (1e-5 inside it: the
+  sphere-box face tie band); contacts <= 2, normals unit."""
+  r, hl = 0.05, 0.2
+  m = _probe("capsule", f"{r} {hl}")
+  s = np.array([1.0, 1.0, 0.5])
+  rng = np.random.default_rng(7)
+  clear, n_tested = 0, 0
+  for i in range(300):
+    site = i % 3
+    p = np.array([rng.uniform(-0.8, 0.8), rng.uniform(-0.8, 0.8), 0.0])
+    if site == 1:
+      p[0] = 1.0 + rng.uniform(-0.15, 0.15)
+    elif site == 2:
+      p[:2] = 1.0 + rng.uniform(-0.15, 0.15, 2)
+    p[2] = rng.uniform(-0.02, 0.2)
+    u = rng.normal(size=4)
+    u /= np.linalg.norm(u)
+    q = np.concatenate([p, u])
+    f = ol.forward(m, q)
+    # capsule axis (local z) in the box frame: the box sits at (0, 0, -0.5), unrotated
+    w, x, y, z = u
+    a = np.array([2 * (x * z + w * y), 2 * (y * z - w * x), 1 - 2 * (x * x + y * y)])
+    c = p - np.array([0.0, 0.0, -0.5])
+    dmin, tmin = _exact_capsule_box(c, a, hl, s)
+    ends = min(_exact_capsule_box(c + a * hl, a, 0.0, s)[0], _exact_capsule_box(c - a * hl, a, 0.0, s)[0])
+    if dmin - r > 0.0:  # separated (margin 0): no contact
+      assert f["ncon"] == 0
+      continue
+    n_tested += 1
+    assert 1 <= f["ncon"] <= 2
+    con = f["contact"]
+    np.testing.assert_allclose(np.linalg.norm(con[:, 6:9], axis=1), 1.0, atol=1e-12)
+    deepest = con[:, 2].min()
+    # never deeper than the exact distance, but for the inside case's face tie band (a segment
+    # point inside the box leaves through the +z face when that is within 1e-5 of the least
+    # penetration, so fp32 and fp64 pick the same face)
+    assert deepest >= dmin - r - 1e-5 - 1e-9
+    if ends - dmin > 2e-4:                     # an interior point is clearly the closest
+      clear += 1
+      assert deepest == pytest.approx(dmin - r, abs=1e-5 if dmin < 0 else 1e-8)
+    else:
+      assert deepest <= dmin - r + 1e-4
+  assert n_tested > 100 and clear > 10

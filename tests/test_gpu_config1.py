@@ -62,7 +62,7 @@ def _assert_clean(env, stats, name):
       assert torch.isfinite(v).all(), f"extras['log'][{k!r}] not finite"
   assert stats["checked"] >= 0.95 * 4 * NSTEPS, stats
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
-  assert len(stats["out_of_model"]) <= 0.02 * stats["checked"] + 1e-9
+  assert not stats["out_of_model"], stats["out_of_model"][:5]  # no world-step outside the fp32 model
 
 
 def test_config1_eager_every_substep(gpu_device):

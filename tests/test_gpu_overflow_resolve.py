@@ -146,7 +146,7 @@ def test_overflow_resolved_matches_oracle(gpu_device):
   assert stats["checked"] >= 0.8 * K * NWORLD, stats
   assert over_checked >= K * NWORLD // 4, over_checked
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
-  assert len(stats["out_of_model"]) <= 0.02 * stats["checked"] + 1, stats["out_of_model"]
+  assert not stats["out_of_model"], stats["out_of_model"]  # no world-step outside the fp32 model
 
 
 def _fused_vs_single(sim, nsub, graph):

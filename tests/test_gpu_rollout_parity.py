@@ -26,11 +26,11 @@ Checks per shadowed substep (fp32 engine vs fp64 oracle):
     |H^-1| times the magnitudes of the gradient's terms, H = M + J_a' D_a J_a at the fp64
     solution -- an fp32 solver's gradient is exact only to rounding of those terms -- plus
     the measured differences of the engine's M and smooth force, the data of the problem it
-    solved).  At most
-    OUT_OF_MODEL_FRACTION of the world-steps may fall outside that model, and each of them
-    must still be a near-minimiser of the same problem: the problem's fp64 cost at the
-    engine's qacc within COST_GAP_REL (relative) of the cost at the oracle's, and the
-    mass-matrix energy-norm error sqrt(dq' M dq) / sqrt(q' M q) <= QACC_ENERGY_REL;
+    solved).  No world-step may fall outside that model (OUT_OF_MODEL_FRACTION = 0; the
+    round-5 maximum is 0.47 of the bound); a failure reports whether the engine's answer is
+    still a near-minimiser of the same problem (the problem's fp64 cost at the engine's qacc
+    within COST_GAP_REL of the cost at the oracle's, the mass-matrix energy-norm error
+    sqrt(dq' M dq) / sqrt(q' M q) within QACC_ENERGY_REL) to tell rounding from a defect;
   - the smooth forces: qfrc_smooth (bias, passive, actuator) per dof within QFRC_ABS +
     QFRC_REL |f_i| of the oracle's;
   - the integration: the oracle's step from the engine's own qacc, qfrc_constraint,
@@ -85,7 +85,7 @@ QACC_ENERGY_REL = 1e-2
 FP32_EPS = float(np.finfo(np.float32).eps)
 QACC_FLOOR, QACC_EPS_MUL = 1e-4, 1024.0
 QVEL_FLOOR, QVEL_EPS_MUL = 1e-6, 24.0
-OUT_OF_MODEL_FRACTION = 0.02
+OUT_OF_MODEL_FRACTION = 0.0
 COST_GAP_REL = 1e-4
 QPOS_ABS = 1e-6
 QPOS_ULPS = 2.0 ** -21  # 4 fp32 ulps of the coordinate
@@ -464,4 +464,5 @@ def test_rollout_shadow_parity(task, num_envs, gpu_device):
   if "G1" in task:
     assert stats["heavy_checked"] > 0, "no world above the 60-row class was compared"
   assert stats["niter_equal"] >= 0.8 * stats["checked"]
-  assert len(stats["out_of_model"]) <= OUT_OF_MODEL_FRACTION * stats["checked"] + 1e-9 or SOFT
+  assert len(stats["out_of_model"]) <= OUT_OF_MODEL_FRACTION * stats["checked"] or SOFT, \
+      stats["out_of_model"][:5]
