@@ -67,11 +67,13 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::gxpos, 3 * d.ngeom_lds, A}, {&Lds::gxmat, 9 * d.ngeom_lds, A},
     {&Lds::sxpos, 3 * d.nsite, A | Cp}, {&Lds::sxmat, 9 * d.nsite, A | Cp},
     {&Lds::M, mslot, A | B}, {&Lds::H, nv * nv, A | B},
-    {&Lds::qfrc_bias, nv, 0}, {&Lds::qfrc_passive, nv, 0}, {&Lds::qfrc_act, nv, A},
-    {&Lds::qfrc_smooth, nv, A | B | Cp}, {&Lds::qacc_smooth, nv, A | B}, {&Lds::x, nv, B | Cp},
+    // phase A keeps qfrc_actuator / qfrc_smooth in lane registers and the smooth solve's
+    // qacc_smooth in dead cinert space (below)
+    {&Lds::qfrc_bias, nv, 0}, {&Lds::qfrc_passive, nv, 0}, {&Lds::qfrc_act, nv, 0},
+    {&Lds::qfrc_smooth, nv, B | Cp}, {&Lds::qacc_smooth, nv, B}, {&Lds::x, nv, B | Cp},
     {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
     {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
-    {&Lds::act_force, d.nu, A | Cp}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
+    {&Lds::act_force, d.nu, Cp}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
     {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, 0},
     {&Lds::con_n, 3 * C, A | Cp},  // unit normals: cframe() rebuilds the frame where used
@@ -156,6 +158,16 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     // (crb dead) and RNE's body forces are written there only after that sum
     if (10 * nb >= 6 * nv) L.cdofdot = L.crb;
     else take(&Lds::cdofdot);
+    // qacc_smooth (the smooth solve's right-hand side, then its solution; phase A stores it
+    // to the B pack right after the solve) in cinert's tail past the subtree momenta:
+    // cinert is dead after RNE, and the geom frames land there only at collision
+    int mom_end = L.stlin == L.cinert ? g2.first + 2 * nb3 : g2.first;
+    if (L.stlin == L.cinert && 10 * nb >= 2 * nb3 + nv) {
+      L.qacc_smooth = mom_end;
+      mom_end += nv;
+    } else {
+      take(&Lds::qacc_smooth);
+    }
     const int gp = (3 * d.ngeom_lds + 3) & ~3;
     if (g2.second >= gp + 9 * d.ngeom_lds) {
       L.gxpos = g2.first;
@@ -164,7 +176,6 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     // both phase-A factorizations (implicit-integration factor, smooth solve) run after RNE
     // and before the geom frames are computed: the same dead group holds the Cholesky buffer,
     // at its tail (the subtree momenta at its head are live across the factorizations)
-    const int mom_end = L.stlin == L.cinert ? g2.first + 2 * nb3 : g2.first;
     if (g2.first + g2.second - 4 * kWave >= mom_end) L.chol = g2.first + g2.second - 4 * kWave;
   }
   const int bit = 1 << ph;

@@ -570,6 +570,19 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   return hipGetLastError();
 }
 
+// One-wave workgroups resident per CU at `bytes` of dynamic LDS, as measured on MI355X
+// (scripts/lds_occupancy.hip: the first-round workgroups of a grid of spinning waves).  The
+// hardware fits fewer than 160 KiB / bytes: 13,184 B hold 11 per CU, not 12 (12 need
+// <= 12,800 B), 14,560 B 10, not 11 (11 need <= 14,080 B), 16,384 B 9, 8,192 B 18.
+int lds_residency(size_t bytes) {
+  static const struct { size_t max_bytes; int per_cu; } kTable[] = {
+      {8192, 18}, {10240, 16}, {11264, 14}, {12800, 12}, {14080, 11}, {15360, 10}, {16384, 9},
+      {20480, 8}, {32768, 4}};
+  for (const auto& t : kTable)
+    if (bytes <= t.max_bytes) return t.per_cu;
+  return bytes > 0 ? std::max(1, (int)((size_t)147456 / bytes)) : 32;
+}
+
 int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
   for (int k = 0; k < kRowClasses; k++) caps[k] = 0;
   int n = 0;
@@ -595,11 +608,11 @@ int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
     Dims ds = d;
     for (int r = (d.njmax - 1) & ~3; r >= 8; r -= 4) {
       ds.njmax = r;
-      if ((size_t)make_lds(ds, 1).total * 4 <= (size_t)160 * 1024 / w) return r;
+      if (lds_residency((size_t)make_lds(ds, 1).total * 4) >= w) return r;
     }
     return 0;
   };
-  if ((size_t)make_lds(d, 1).total * 4 <= (size_t)160 * 1024 / top) return 0;  // no need
+  if (lds_residency((size_t)make_lds(d, 1).total * 4) >= top) return 0;  // no need
   // One class below the register-bound residency, the rest at full capacity (gated at 5/6 of
   // it).  Measured with the round-3 full-form Hessian (G1 4096, B span per substep): one class
   // at 44 / 52 / 60 / 64 / 72 / 84 rows 202 / 196 / 197 / 197 / 203 / 198 us; two classes
@@ -611,7 +624,7 @@ int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {
   // env-steps/s, caps default-5/6 (72 rows, 10/CU) / 56 (12/CU) / 64 (11/CU): velocity 4096
   // 2.636 / 2.662 / 2.657 M, jump flat 16384 7.80 / 7.80 / 7.88 M, jump hfield 16384 4.81 /
   // 4.88 / 4.87 M, rough 4096 2.45 / 2.46 / 2.47 M, tracking 2.46 / 2.47 / 2.46 M.
-  const int full_per_cu = (int)((size_t)160 * 1024 / ((size_t)make_lds(d, 1).total * 4));
+  const int full_per_cu = lds_residency((size_t)make_lds(d, 1).total * 4);
   for (int w : {(5 * top) / 6}) {
     if (w < 8 || 2 * full_per_cu > w) continue;
     const int r = cap_for((11 * top) / 12);

@@ -1803,8 +1803,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     // (copied loop by loop, each load-then-LDS-store would wait out a global latency).
     for (int i = lane; i < nvp; i += kWave) {
       if (i >= nv) S[L.qvel + i] = 0.f;  // DMA fills i < nv
-      S[L.qfrc_act + i] = 0.f;
-      S[L.qfrc_smooth + i] = 0.f; S[L.qacc_smooth + i] = 0.f;
     }
     if (sel & kSelFusedA) {  // step_chain: phase C stored this state in the same launch
       dma_row_l2(S + L.qpos, D.qpos + (size_t)w * nq, nq, lane);
@@ -2224,7 +2222,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       qpass_i = pf;
     }
     sync();
-    // actuation: position / motor actuators on joints
+    // actuation: position / motor actuators on joints.  The actuator forces, qfrc_actuator
+    // and qfrc_smooth stay in lane registers (lane u: actuator u, lane i: dof i) and go to
+    // the packs from there: no LDS slots (phase A's carve sets its residency)
+    float act_f = 0.f, act_gf = 0.f;
     if (lane < nu) {
       const int u = lane;
       const float g = Ar.gear;
@@ -2233,16 +2234,28 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if (Ar.ctrllim) c = fminf(fmaxf(c, Ar.cr0), Ar.cr1);
       float f = Ar.gain * c + Ar.b0 + Ar.b1 * len + Ar.b2 * vel;
       if (Ar.forcelim) f = fminf(fmaxf(f, Ar.fr0), Ar.fr1);
-      S[L.act_force + u] = f;
+      act_f = f;
+      act_gf = g * f;
       if (last) {
         D.actuator_length[(size_t)w * nu + u] = len;
         D.actuator_velocity[(size_t)w * nu + u] = vel;
       }
-      atomicAdd(S + L.qfrc_act + Ar.dof, g * f);
     }
-    sync();
-    for (int i = lane; i < nv; i += kWave) {  // nv <= 64: one pass, lane i
-      float f = qpass_i - qbias_i + qapp_i + S[L.qfrc_act + i];
+    // qfrc_actuator of dof i, in lane i: the actuators' g f gathered onto their dofs in
+    // actuator order
+    float qact_i = 0.f;
+    for (int u = 0; u < nu; u++) {
+      const float x = rl(act_gf, u);
+      if (lane == __builtin_amdgcn_readlane(Ar.dof, u)) qact_i += x;
+    }
+    if (lane < ((nu + 3) & ~3)) gc[LC.act_force + lane] = act_f;  // C pack (zero padding)
+    float qfs_i = 0.f;  // lane i < nv: qfrc_smooth of dof i
+    for (int i = lane; i < nvp; i += kWave) {  // nv <= 64: one pass, lane i
+      if (i >= nv) {  // the smooth solve's right-hand side is zero on the padding dofs
+        S[L.qacc_smooth + i] = 0.f;
+        continue;
+      }
+      float f = qpass_i - qbias_i + qapp_i + qact_i;
       if (any_xfrc) {
         uint64_t bm = m.dof_bodymask[i];
         const float* cd = S + L.cdof + 6 * i;
@@ -2254,8 +2267,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           f += dot(jp, v3(xf)) + dot(cang, v3(xf + 3));
         }
       }
-      S[L.qfrc_smooth + i] = f;
+      qfs_i = f;
       S[L.qacc_smooth + i] = f;
+    }
+    if (lane < nvq) {  // both packs (padding zero)
+      gw[LB.qfrc_smooth + lane] = qfs_i;
+      gc[LC.qfrc_smooth + lane] = qfs_i;
     }
     // subtree momenta (for subtreeangmom sensors)
     if (bl) {
@@ -2281,7 +2298,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if (o.integrator == 1 && lane < nu && Ar.b2 != 0.f) {
         bool skip = false;
         if (Ar.forcelim) {
-          const float fo = S[L.act_force + lane];
+          const float fo = act_f;
           skip = fo <= Ar.fr0 || fo >= Ar.fr1;
         }
         if (!skip) act_d = -h * Ar.gear * Ar.gear * Ar.b2;
@@ -2312,6 +2329,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       spd_factor_solve_tree<NR, SP>(S + L.M, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
     else
       spd_factor_solve<NR>(S + L.M, nullptr, S + L.H, S + L.qacc_smooth, S + L.chol, nvp, lane);
+    // qacc_smooth to the B pack and a lane register now: its LDS slot (carve.h: dead cinert
+    // space) is reused by the geom frames at collision
+    const float qacs_i = lane < nvq ? S[L.qacc_smooth + lane] : 0.f;
+    if (lane < nvq) gw[LB.qacc_smooth + lane] = qacs_i;
     STAMP(7);
     // subtree com velocity and angular momentum about the subtree com, as sums over the
     // subtree (broadcast loop): V = sum m vc / M, L = sum h + sum m (x - X) x (vc - V) --
@@ -3095,13 +3116,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       for (int i = lane; i < 9 * d.nsite; i += kWave) D.site_xmat[ws * 9 + i] = S[L.sxmat + i];
       for (int i = lane; i < nv; i += kWave) {
         size_t k = (size_t)w * nv + i;
-        D.qacc_smooth[k] = S[L.qacc_smooth + i];
-        D.qfrc_bias[k] = qbias_i;  // lane i (nv <= 64)
+        D.qacc_smooth[k] = qacs_i;  // lane i (nv <= 64)
+        D.qfrc_bias[k] = qbias_i;
         D.qfrc_passive[k] = qpass_i;
-        D.qfrc_actuator[k] = S[L.qfrc_act + i];
-        D.qfrc_smooth[k] = S[L.qfrc_smooth + i];
+        D.qfrc_actuator[k] = qact_i;
+        D.qfrc_smooth[k] = qfs_i;
       }
-      for (int u = lane; u < nu; u += kWave) D.actuator_force[(size_t)w * nu + u] = S[L.act_force + u];
+      if (lane < nu) D.actuator_force[(size_t)w * nu + lane] = act_f;
       size_t wc = (size_t)w * P->con_stride;
       // contact slots: this output's contacts, and zeros over the previous output's past them
       // (every slot beyond both is zero already: engine_counters [6] = slots this output
@@ -3126,9 +3147,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     const int C = ncon;
     const int C4 = (C + 3) & ~3;
     const int nr4 = (nefc + 3) & ~3;
-    cp4(gw + LB.ints, S + L.ints, 8, lane);
-    cp4(gw + LB.qacc_smooth, S + L.qacc_smooth, nvq, lane);
-    cp4(gw + LB.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
+    cp4(gw + LB.ints, S + L.ints, 8, lane);  // (qacc_smooth, qfrc_smooth: stored above)
     cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
     cp4(gw + LB.efc_D, S + L.efc_D, nr4, lane);
     cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
@@ -3136,7 +3155,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
     cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
     cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
-    cp4(gc + LC.act_force, S + L.act_force, (nu + 3) & ~3, lane);
     cp4(gc + LC.con_g1, S + L.con_g1, C4, lane);
     cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
     cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
@@ -3145,7 +3163,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
     cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
     cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
-    cp4(gc + LC.qfrc_smooth, S + L.qfrc_smooth, nvq, lane);
     STAMP(14);
   } else if constexpr (PH == 1) {
     // ----------------------------------------------------------- phase B (Newton)
