@@ -255,7 +255,7 @@ static bool chain_env(int cls, int nworld) {
 hipError_t prepare_step(const Params& host) {
   size_t shmem[3] = {lds_bytes(host, 0), lds_bytes(host, 1), lds_bytes(host, 2)};
   for (int k = 0; k < host.nrowclass; k++) shmem[1] = std::max(shmem[1], lds_bytes(host, 3 + k));
-  for (int ph = 0; ph < 8; ph++) {  // phase codes of phase_kernel
+  for (int ph = 0; ph < 9; ph++) {  // phase codes of phase_kernel
     const size_t need = ph >= 5 ? std::max(shmem[0], std::max(shmem[1], shmem[2]))
                                 : shmem[ph == 3 ? 1 : ph == 4 ? 0 : ph];
     const StepFn f = step_fn(host, ph);
@@ -402,7 +402,17 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   }();
   const bool masked_big = masked_big_env >= 0 ? masked_big_env != 0 : nworld <= 4096;
   if (mask && hbig && masked_big) {
-    // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve
+    // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve;
+    // A -> B -> C as one launch (step_masked) unless MJX355_MASKED_FUSED=0
+    static const bool fused = [] {
+      const char* e = getenv("MJX355_MASKED_FUSED");
+      return !e || atoi(e) != 0;
+    }();
+    if (const StepFn fM = fused ? step_fn(*hbig, 8) : nullptr) {
+      hipLaunchKernelGGL(fM, dim3(nworld), dim3(kWave), lds_resolve(*hbig), stream, dbig, 0, nworld, 0,
+                         1, integrate, mask);
+      return hipGetLastError();
+    }
     const StepFn fA = step_fn(*hbig, 0), fBL = step_fn(*hbig, 3), fC = step_fn(*hbig, 2);
     hipLaunchKernelGGL(fA, dim3(nworld), dim3(kWave), lds_bytes(*hbig, 0), stream, dbig, 0, nworld, 0,
                        1, integrate, mask);

@@ -3934,11 +3934,31 @@ __attribute__((amdgpu_waves_per_eu(LAT ? 1 : (NR <= 48 ? 3 : 1), LAT ? 2 : 8))) 
   }
 }
 
+// The masked forward (the reset worlds of an env step) in the max carve as ONE launch: phase
+// A, the latency Newton kernel and phase C back to back per masked world, hand-offs as in
+// step_chain.  A workgroup whose world is not masked exits at once.  LDS: the largest of the
+// three max carves.  (Three launches cost two more dispatch ramps and launch gaps on the env
+// step's critical path, for the handful of worlds a step resets.)
+template <int NR, int SP>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_masked(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  const int bid = (int)blockIdx.x;
+  if (w0 + bid >= w1 || !mask[w0 + bid]) return;
+  step_body<NR, 0, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
+  chain_handoff();
+  step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, -1, mask, bid);
+  chain_handoff();
+  step_body<NR, 2, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
+}
+
 using StepFn = void (*)(const Params*, int, int, int, int, int, const uint8_t*);
 
 // kernel of phase code ph: 0 A, 1 B, 2 C, 3 B latency form; 4: phase A over a re-solve list
 // (the fast carve's next substep), 5: a listed world's whole substep (step_resolve); 6 / 7: a
-// row class's B -> C -> next A chain as one launch (step_chain; 7: the latency form)
+// row class's B -> C -> next A chain as one launch (step_chain; 7: the latency form); 8: the
+// masked forward's A -> B -> C in the max carve (step_masked)
 template <int NR, int SP>
 StepFn phase_kernel(int ph) {
   constexpr int role = SpecRole<SP>::mask;
@@ -3960,6 +3980,9 @@ StepFn phase_kernel(int ph) {
       else return nullptr;
     case 7:
       if constexpr ((role & 1) != 0) return step_chain<NR, SP, true>;
+      else return nullptr;
+    case 8:
+      if constexpr ((role & 2) != 0) return step_masked<NR, SP>;
       else return nullptr;
     default:
       return nullptr;
