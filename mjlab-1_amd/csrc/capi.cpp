@@ -745,6 +745,7 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
   if (sync_params(s, nullptr)) { delete s; return -1; }
   e = mjx::prepare_step(host_params(s));
   if (e == hipSuccess && s->big) e = mjx::prepare_step(host_params_big(s));
+  s->side.range_chain = s->nrowclass == 0 && mjx::range_chain_default(host_params(s), nworld, s->side.nsplit);
   if (e != hipSuccess) { delete s; return fail(std::string("prepare: ") + hipGetErrorString(e)); }
   // heightfield geom frames are static: write them once for every world
   for (size_t k = 0; k < model->static_geoms.size(); k++) {

@@ -238,7 +238,11 @@ struct SideStream {
   // next substep's classify)
   hipStream_t ovf[kMaxSplit];
   hipEvent_t ovf_fork[kMaxSplit], ovf_join[kMaxSplit];
+  bool range_chain = false;  // models without row classes: range_chain_default
 };
+// Whether a model without row classes runs each batch range's B -> C -> next A as one
+// launch (engine.hip launch_step; MJX355_RANGE_CHAIN=0/1 overrides).
+bool range_chain_default(const struct Params& host, int nworld, int nsplit);
 // `hbig` / `dbig`: the max-capacity Params (host copy for the launch geometry, device copy
 // for the kernels) of the overflow re-solve, or null (overflow drops contacts).
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,

@@ -462,6 +462,16 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   // so the bulk class's C and next A overlap the heavy class's Newton tail; the streams
   // join before the next classify.  MJX355_CLASS_PIPE=0: phase C / A over every world
   // after the join (diagnostic).
+  // Models without row classes (Go1): each range's B -> C -> next substep's A as one launch
+  // (step_chain over every world of the range), as the class pipelines do for a class, when
+  // range_chain_default chose it.  Worlds listed for the re-solve skip the chain's B, C and
+  // A; the re-solve chain then runs their next A too.  MJX355_RANGE_CHAIN=0/1 forces (A/B).
+  static const int range_chain_env = [] {
+    const char* e = getenv("MJX355_RANGE_CHAIN");
+    return e ? atoi(e) : -1;
+  }();
+  const bool rchain = range_chain_env >= 0 ? range_chain_env != 0 : (side && side->range_chain);
+  const StepFn fR = nc == 0 && !mask && rchain ? step_fn(host, 6) : nullptr;
   for (int sub = 0; sub < nsubstep; sub++) {
     const int last = sub == nsubstep - 1;
     const int apar = (sub & 1) ? kSelAPar : 0;  // phase A of this substep lists into parity sub & 1
@@ -470,7 +480,8 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       if (n <= 0) continue;
       hipStream_t st = sst[k];
       const bool piped = nc > 0 && !mask && pipe;
-      if (!piped || sub == 0)
+      const bool nexta = piped || fR;  // the next substep's phase A runs behind this one's C
+      if (!nexta || sub == 0)
         hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), st, dev, w0, w1, k | apar,
                            last, integrate, mask);
       // the re-solve chain: forked after this substep's phase A (and classify), joined at the
@@ -484,13 +495,13 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         if (e2 == hipSuccess) e2 = hipStreamWaitEvent(side->ovf[k], side->ovf_fork[k], 0);
         if (e2 == hipSuccess)
           ovf_chain(host, dev, *hbig, dbig, side->ovf[k], k, w0, w1, sub, nsubstep, integrate,
-                    piped);
+                    nexta);
         return e2;
       };
       auto join_ovf = [&]() {
         if (!ovf) return hipSuccess;
         if (ovf_inline) {
-          ovf_chain(host, dev, *hbig, dbig, st, k, w0, w1, sub, nsubstep, integrate, false);
+          ovf_chain(host, dev, *hbig, dbig, st, k, w0, w1, sub, nsubstep, integrate, fR != nullptr);
           return hipSuccess;
         }
         hipError_t e2 = hipEventRecord(side->ovf_join[k], side->ovf[k]);
@@ -562,6 +573,14 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         }
         if (ovf_stream_env() && (e = join_ovf()) != hipSuccess) return e;
         if (piped) continue;
+      } else if (fR) {
+        if ((e = fork_ovf()) != hipSuccess) return e;
+        const int selx = k | (last ? 0 : kSelChainA) | (((sub + 1) & 1) ? kSelAPar : 0) |
+                         (sub + 1 == nsubstep - 1 ? kSelNextLast : 0);
+        hipLaunchKernelGGL(fR, dim3(n), dim3(kWave), lds_chain(host, 0, !last), st, dev, w0, w1, selx,
+                           last, integrate, mask);
+        if ((e = join_ovf()) != hipSuccess) return e;
+        continue;
       } else {
         if ((e = fork_ovf()) != hipSuccess) return e;
         hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
@@ -591,6 +610,28 @@ int lds_residency(size_t bytes) {
   for (const auto& t : kTable)
     if (bytes <= t.max_bytes) return t.per_cu;
   return bytes > 0 ? std::max(1, (int)((size_t)147456 / bytes)) : 32;
+}
+
+// The range chain runs phases A and C at the Newton kernel's residency (registers and the
+// largest carve).  Measured (Go1, 24 / 96 carve, two ranges, two interleaved rounds on one
+// box): flat 4,096 worlds (2,048 per range) 5.25 -> 5.60 M env-steps/s, rough 8,192 (4,096
+// per range) 4.57 -> 4.82 M, flat 8,192 7.38 -> 7.07 M.  A range that fits one residency
+// round of the chain gains (two launch ramps and gaps per substep go); so does a model with
+// terrain collision, whose long per-world phase-A tails the chain's per-world flow absorbs;
+// a flat range needing a second round loses the cheap phases' residency.
+bool range_chain_default(const Params& host, int nworld, int nsplit) {
+  const StepFn f = step_fn(host, 6);
+  hipFuncAttributes fa;
+  if (!f || hipFuncGetAttributes(&fa, (const void*)f) != hipSuccess) return false;
+  const int regs = (fa.numRegs + 7) & ~7;
+  const int per_cu = std::min(4 * (regs > 0 ? std::min(8, 512 / regs) : 8),
+                              lds_residency(lds_chain(host, 0, true)));
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 256;
+  const int per_range = (nworld + std::max(nsplit, 1) - 1) / std::max(nsplit, 1);
+  return per_range <= per_cu * ncu || host.d.nstatic > 0;
 }
 
 int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]) {

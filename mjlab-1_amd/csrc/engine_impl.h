@@ -1764,6 +1764,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   if (PH != 0 && P->ovf_resolve && !(sel & kSelOvf) && !cls1 &&
       !(PH == 1 && P->nrowclass > 0 && integrate >= 0) && P->ovf_flag[w])
     return;
+  // ... and a range chain's next phase A (models without row classes: step_chain over every
+  // world of a batch range) skips it too: the re-solve chain runs that world's next A
+  if (PH == 0 && (sel & kSelFusedA) && !cls1 && P->ovf_resolve && P->ovf_flag[w]) return;
   float* gw = P->gscr + (size_t)w * P->gstride;  // [B pack | C pack]
   float* gc = gw + P->gC;
   float* gf = gw + P->gF;  // implicit-integration factor (phase A writes, phase C reads)
