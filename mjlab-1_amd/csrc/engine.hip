@@ -362,8 +362,8 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
                       bool next_a) {
   const int last = sub == nsubstep - 1;
   const int par = sub & 1;
-  // the grid: every re-solve launch of an empty list still dispatches it (measured on G1,
-  // nothing listed: 256 workgroups -1.0 %); MJX355_OVF_GRID overrides
+  // the grid (kOvfGrid: sized for heavy overflow; an empty list costs the same at 1 or 256
+  // workgroups); MJX355_OVF_GRID overrides
   static const int grid = [] {
     const char* e = getenv("MJX355_OVF_GRID");
     return e && atoi(e) > 0 ? atoi(e) : kOvfGrid;
