@@ -209,6 +209,9 @@ struct Params {
 // 20-contact / 80-row fast carve, 3.5 % of world-substeps re-solved): 64 workgroups 1.43 M
 // env-steps/s, 256 1.69 M, 512 1.65 M; with nothing listed the grid size is not measurable.
 constexpr int kOvfGrid = 256;
+// ... and where the chain runs in line on a split stream (the critical path): Go1 flat 8,192
+// worlds at 256 / 64 / 16 workgroups 6.73 / 7.29 / 7.48 M env-steps/s, rough 4.46 / 4.79 / 4.87 M
+constexpr int kOvfGridInline = 16;
 constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;
