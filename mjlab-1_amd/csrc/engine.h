@@ -210,8 +210,10 @@ struct Params {
 // env-steps/s, 256 1.69 M, 512 1.65 M; with nothing listed the grid size is not measurable.
 constexpr int kOvfGrid = 256;
 // ... and where the chain runs in line on a split stream (the critical path): Go1 flat 8,192
-// worlds at 256 / 64 / 16 workgroups 6.73 / 7.29 / 7.48 M env-steps/s, rough 4.46 / 4.79 / 4.87 M
-constexpr int kOvfGridInline = 16;
+// worlds at 256 / 64 / 32 / 16 workgroups 6.73 / 7.32 / 7.40 / 7.41 M env-steps/s; under
+// forced overflow (G1 at a 20 / 80 fast carve, 3.5 % of world-substeps re-solved) 64 / 32 /
+// 16 workgroups 1.49 / 1.17 / 0.81 M
+constexpr int kOvfGridInline = 32;
 constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;

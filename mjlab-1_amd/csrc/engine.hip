@@ -364,8 +364,8 @@ static void ovf_chain(const Params& host, const Params* dev, const Params& hbig,
   const int par = sub & 1;
   // the grid: kOvfGrid on a stream of its own (sized for heavy overflow; an empty list costs
   // the same at 1 or 256 workgroups there), kOvfGridInline where the chain runs in line on
-  // the critical path (split batches: 256 max-carve workgroups per launch cost Go1 8 %, 16
-  // gain 2.6 % over 64);
+  // the critical path (split batches: 256 max-carve workgroups per launch cost Go1 8 %;
+  // engine.h kOvfGridInline);
   // MJX355_OVF_GRID overrides both
   static const int grid_env = [] {
     const char* e = getenv("MJX355_OVF_GRID");

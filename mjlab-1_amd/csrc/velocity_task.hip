@@ -658,11 +658,9 @@ __global__ void k_reset(const mjxTaskDesc* __restrict__ T) {
   t.episode_length[e] = 0;
 }
 
-__global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ acc) {
-  const mjxTaskDesc& t = *T;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) {
-    // logs of the previous kernels' reductions (k_post ran to completion before this launch)
+// logs of the previous kernels' reductions (k_post ran to completion before this launch)
+__device__ void observe_logs(const mjxTaskDesc& t, Acc* __restrict__ acc) {
+  {
     if (acc->count > 0.f) {
       for (int k = 0; k < t.nreward; k++) t.log_reward[k] = acc->reward[k] / acc->count / t.episode_length_s;
       for (int k = 0; k < t.ntermination; k++) t.log_termination[k] = acc->term[k];
@@ -677,7 +675,9 @@ __global__ void k_observe(const mjxTaskDesc* __restrict__ T, Acc* __restrict__ a
     acc->cmd[0] = acc->cmd[1] = 0.f;
     acc->count = 0.f;
   }
-  if (e >= t.nworld) return;
+}
+// env e's command update and interval events, before its observations
+__device__ void observe_env(const mjxTaskDesc& t, int e) {
   const uint64_t step = *t.step_counter, seed = t.seed;
   const Root r = root_state(t, e);
   if (t.command_kind == MJX_CMD_JUMP) {
@@ -783,21 +783,19 @@ __device__ __forceinline__ void obs_jump(const mjxTaskDesc& t, int e, int i) {
   co[i] = v;
 }
 
-__global__ void k_obs(const mjxTaskDesc* __restrict__ T) {
-  const mjxTaskDesc& t = *T;
+// observation elements of env e: the critic's (the jump layout, or the velocity layout)
+__device__ __forceinline__ int obs_count(const mjxTaskDesc& t) {
+  if (t.command_kind == MJX_CMD_JUMP) return t.ncritic;
+  const int nput = 9 + 3 * t.njoint + 3;
+  return t.critic_extras ? nput + 6 * t.nfeet : nput;
+}
+__device__ void obs_elem(const mjxTaskDesc& t, int e, int i) {
   if (t.command_kind == MJX_CMD_JUMP) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= t.nworld * t.ncritic) return;
-    const int e = idx / t.ncritic;
-    obs_jump(t, e, idx - e * t.ncritic);
+    obs_jump(t, e, i);
     return;
   }
   const int nj = t.njoint;
   const int nput = 9 + 3 * nj + 3;  // elements shared by the policy and critic groups
-  const int nel = t.critic_extras ? nput + 6 * t.nfeet : nput;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= t.nworld * nel) return;
-  const int e = idx / nel, i = idx - e * nel;
   const float* sd = t.sensordata + (size_t)e * t.nsensordata;
   float* co = t.obs_critic + (size_t)e * t.ncritic;
   if (i < nput) {
@@ -841,6 +839,28 @@ __global__ void k_obs(const mjxTaskDesc* __restrict__ T) {
     v = copysignf(log1pf(fabsf(fv)), fv) * (fv != 0.f ? 1.f : 0.f);
   }
   co[i] = v;
+}
+
+// Command update, interval events and observations as one launch, a wave per env: lane 0
+// runs the env's command / push update, then the wave's lanes write its observation elements
+// (which read the updated command and velocities).  Each env touches only its own state, so
+// the wave-level hand-off replaces the launch boundary of two kernels (observe, then
+// observations), one dispatch and gap fewer on the env step's critical path.
+constexpr int kObsEnvs = 4;
+__global__ __launch_bounds__(64 * kObsEnvs) void k_observe_obs(const mjxTaskDesc* __restrict__ T,
+                                                               Acc* __restrict__ acc) {
+  const mjxTaskDesc& t = *T;
+  if (blockIdx.x == 0 && threadIdx.x == 0) observe_logs(t, acc);
+  const int e = blockIdx.x * kObsEnvs + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (e >= t.nworld) return;
+  if (lane == 0) observe_env(t, e);
+  // lane 0's stores are complete and visible to the wave's loads (workgroup scope: one CU)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int nel = obs_count(t);
+  for (int i = lane; i < nel; i += 64) obs_elem(t, e, i);
 }
 
 // Terrain-level curriculum over the reset mask (tasks/velocity/mdp/curriculums.py:30-64,
@@ -990,11 +1010,9 @@ int mjx_task_observe(mjxTask* t, void* stream) {
     if (nel > t->host.ncritic || 9 + 3 * nj + 3 > t->host.npolicy)
       return task_fail("observation sizes do not match the velocity task layout");
   }
-  hipLaunchKernelGGL(mjxt::k_observe, dim3((t->nworld + mjxt::kBlock - 1) / mjxt::kBlock),
-                     dim3(mjxt::kBlock), 0, (hipStream_t)stream, t->dev, t->acc);
-  const long n = (long)t->nworld * nel;
-  hipLaunchKernelGGL(mjxt::k_obs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, t->dev);
+  (void)nel;
+  hipLaunchKernelGGL(mjxt::k_observe_obs, dim3((t->nworld + mjxt::kObsEnvs - 1) / mjxt::kObsEnvs),
+                     dim3(64 * mjxt::kObsEnvs), 0, (hipStream_t)stream, t->dev, t->acc);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : task_fail(std::string("k_observe: ") + hipGetErrorString(e));
 }

@@ -276,9 +276,21 @@ class ManagerBasedRlEnv:
       out = tuple(t.clone() for t in self._step_sync_free(self._static_action)[1:])
       obs = {k: v.clone() for k, v in self.obs_buf.items()}
     torch.cuda.current_stream(self.device).wait_stream(s)
+    # fused managers: the action kernel stays outside the graph and runs before each replay,
+    # on the caller's tensor (no copy into the static input buffer)
+    fa = self._fused if self._fused is not None and hasattr(self._fused, "apply_action") else None
+    if os.environ.get("MJX355_GRAPH_ACTION", "0") != "0":  # diagnostic: the action kernel in the graph
+      fa = None
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-      self._graph_out = self._step_sync_free(self._static_action)
+    if fa is not None:
+      fa.action_in_step = False
+    try:
+      with torch.cuda.graph(g):
+        self._graph_out = self._step_sync_free(self._static_action)
+    finally:
+      if fa is not None:
+        fa.action_in_step = True
+    self._graph_action = fa
     self._graph = g
     self._graph_key_captured = self._graph_key()
     self.obs_buf = obs
@@ -299,7 +311,16 @@ class ManagerBasedRlEnv:
         return (*out, self.extras)
       if self._graph is None or self._graph_key() != self._graph_key_captured:
         return (*self._capture(action), self.extras)
-      self._static_action.copy_(action)
+      fa = getattr(self, "_graph_action", None)
+      if fa is not None:
+        a = action
+        if not (a.is_cuda and a.dtype == torch.float32 and a.is_contiguous()
+                and a.device == self._static_action.device and a.shape == self._static_action.shape):
+          self._static_action.copy_(a)
+          a = self._static_action
+        fa.apply_action(a)
+      else:
+        self._static_action.copy_(action)
       self._graph.replay()
       self.obs_buf, self.reward_buf, self.reset_terminated, self.reset_time_outs = self._graph_out
       return (*self._graph_out, self.extras)

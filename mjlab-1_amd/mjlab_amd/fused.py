@@ -593,10 +593,19 @@ class FusedVelocityStep:
       raise MjxError(self._L.mjx_task_last_error().decode())
 
   # ------------------------------------------------------------------ the env step
+  # False while the env records a graph whose replays run apply_action() before them (the
+  # action kernel then reads the caller's tensor: no copy into a static input buffer)
+  action_in_step = True
+
+  def apply_action(self, action: torch.Tensor):
+    stream = ctypes.c_void_p(torch.cuda.current_stream(self.env.sim._torch_device).cuda_stream)
+    self._ok(self._L.mjx_task_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
+
   def step(self, action: torch.Tensor):
     env, L, sim = self.env, self._L, self.env.sim
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
-    self._ok(L.mjx_task_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
+    if self.action_in_step:
+      self._ok(L.mjx_task_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
     if self._engine_air:
       # the engine updates the feet air times every substep (mjx_sim_track_air_time) and
       # nothing reads mjData between substeps: one mjx_step of `decimation` substeps, whose

@@ -410,10 +410,17 @@ class FusedTrackingStep:
       raise MjxError(self._L.mjx_track_last_error().decode())
 
   # ------------------------------------------------------------------ the env step
+  action_in_step = True  # as FusedVelocityStep.action_in_step
+
+  def apply_action(self, action: torch.Tensor):
+    stream = ctypes.c_void_p(torch.cuda.current_stream(self.env.sim._torch_device).cuda_stream)
+    self._ok(self._L.mjx_track_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
+
   def step(self, action: torch.Tensor):
     env, L, sim = self.env, self._L, self.env.sim
     stream = ctypes.c_void_p(torch.cuda.current_stream(sim._torch_device).cuda_stream)
-    self._ok(L.mjx_track_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
+    if self.action_in_step:
+      self._ok(L.mjx_track_action(self._task, ctypes.c_void_p(action.data_ptr()), stream))
     sim.step(nsubstep=env.cfg.decimation)  # mjData outputs written after the last substep
     self._ok(L.mjx_track_post(self._task, stream))
     mask = ctypes.c_void_p(self.reset_buf.data_ptr())
