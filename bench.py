@@ -240,8 +240,8 @@ def main():
   ap.add_argument("--engine-capacity", default=None,
                   help="diagnostic: 'C,R' or 'none' overrides the task's SimulationCfg.engine_capacity "
                        "(the fast LDS carve; worlds past it are re-solved at the max capacity)")
-  ap.add_argument("--edited-scene", action="store_true",
-                  help="diagnostic: the G1 velocity task with tests/scene_edits.py's cfg.scene edit "
+  ap.add_argument("--edited-scene", nargs="?", const="full", default=None, choices=["full", "sensor"],
+                  help="diagnostic: the G1 velocity task with a tests/scene_edits.py cfg.scene edit, full (a heavier torso, foot friction, a contact sensor) or sensor (the contact sensor only) "
                        "(no compiled specialisation matches it: run-time specialised kernels)")
   ap.add_argument("--allow-overflow", action="store_true",
                   help="exit 0 even if contacts were dropped in the timed steps")
@@ -269,8 +269,8 @@ def main():
   if args.edited_scene:
     from mjlab_amd.envs import ManagerBasedRlEnv
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
-    from scene_edits import edited_g1_cfg
-    cfg = edited_g1_cfg(args.num_envs)
+    from scene_edits import edited_g1_cfg, sensor_only_g1_cfg
+    cfg = (edited_g1_cfg if args.edited_scene == "full" else sensor_only_g1_cfg)(args.num_envs)
     cfg.seed = mjdist.rank_seed(42, rank)
     env = ManagerBasedRlEnv(cfg, device=device)
   elif args.engine_capacity is None:
@@ -377,7 +377,7 @@ def main():
       "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
       "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
       "data": "synthetic (random-init state from the compiled G1 MJCF; uniform random actions)",
-      "config": {"workload": f"{args.task}{' (tests/scene_edits.py edit)' if args.edited_scene else ''} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
+      "config": {"workload": f"{args.task}{f' (tests/scene_edits.py {args.edited_scene} edit)' if args.edited_scene else ''} {'env.step' if args.mode == 'env' else 'physics-only decimation x sim.step'}",
                  "task": args.task, "num_envs_per_gpu": args.num_envs, "decimation": dec,
                  "parallelism": f"dp{world}", "mode": args.mode, "step_path": step_path,
                  "kernels": ("generic" if sim.info()["spec"] == 0 else

@@ -30,6 +30,22 @@ def edited_g1_cfg(num_envs: int = 16):
   return cfg
 
 
+def sensor_only_g1_cfg(num_envs: int = 16):
+  """The shipped G1 velocity scene plus the hands contact sensor only: no physics change (the
+  same dynamics, resets and randomisation as the shipped task), but the model dimensions no
+  longer match any compiled specs.inc entry -- the run-time specialisation's cost alone."""
+  from mjlab_amd.envs import load_env_cfg
+  from mjlab_amd.sensor import ContactMatch, ContactSensorCfg
+  cfg = load_env_cfg("Mjlab-Velocity-Flat-Unitree-G1")
+  cfg.scene.num_envs = num_envs
+  cfg.scene.sensors = cfg.scene.sensors + (ContactSensorCfg(
+    name="hands", primary=ContactMatch(mode="body", entity="robot",
+                                       pattern=r"^(left|right)_wrist_yaw_link$"),
+    secondary=ContactMatch(mode="body", pattern="terrain"), fields=("found", "force"),
+    reduce="netforce"),)
+  return cfg
+
+
 def jit_targets(cfg):
   """(model, nconmax, njmax, role) of the run-time specialisations a Simulation of `cfg` loads."""
   from mjlab_amd.scene import Scene
