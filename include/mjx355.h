@@ -140,7 +140,10 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
 int mjx_sim_destroy(mjxSim* sim);
 
 /* One mj_step (forward + implicitfast/Euler integration) for every world, repeated
- * `nsubstep` times inside ONE kernel launch (ctrl/xfrc/qfrc_applied held fixed). */
+ * `nsubstep` times (ctrl/xfrc/qfrc_applied held fixed).  The state (qpos, qvel, act, time,
+ * qacc_warmstart) advances every substep; the derived mjData outputs -- frames, contacts,
+ * forces, subtree momenta and sensordata -- are the last substep's, computed in that substep
+ * only (the contact sensors run every substep: the contact air times read their counts). */
 int mjx_step(mjxSim* sim, int nsubstep, void* stream);
 /* mj_forward without integration (kinematics/sensors/acc for the current state). */
 int mjx_forward(mjxSim* sim, void* stream);

@@ -159,6 +159,11 @@ static mjx::Params host_params(const mjxSim_* s) {
     return e ? atoi(e) : 0;
   }();
   p.stamp_minrows = minrows;
+  static const int outputs_every = [] {
+    const char* e = getenv("MJX355_OUTPUTS_EVERY");
+    return e ? atoi(e) : 0;
+  }();
+  p.outputs_every = outputs_every;
   p.ovf_resolve = s->big ? 1 : 0;
   p.ovf_cap = s->ovf_cap;
   p.ovf_list = s->ovf;

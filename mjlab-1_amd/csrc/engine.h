@@ -193,6 +193,7 @@ struct Params {
   // capacity) re-solves its substep from its state.  The max Params have ovf_resolve = 0:
   // what overflows them is dropped and counted.
   int ovf_resolve;
+  int outputs_every;  // diagnostic (MJX355_OUTPUTS_EVERY=1): sensors / subtree momenta every substep
   int ovf_cap;
   int* ovf_list;   // [kMaxSplit][2][ovf_cap]
   int* ovf_n;      // [kMaxSplit][2]

@@ -2277,8 +2277,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       gw[LB.qfrc_smooth + lane] = qfs_i;
       gc[LC.qfrc_smooth + lane] = qfs_i;
     }
-    // subtree momenta (for subtreeangmom sensors)
-    if (bl) {
+    // subtree momenta (for subtreeangmom sensors and the subtree outputs): like every mjData
+    // output of a fused multi-substep step, only the last substep's are observable, so the
+    // earlier substeps skip them (and the pos / vel / acc sensors below)
+    const bool obs = last != 0 || P->outputs_every;
+    if (bl && obs) {
       const int b = B.b;
       const float* cv = S + L.cvel + 6 * b;
       V3 rel = v3(S + L.xipos + 3 * b) - v3(S + L.subtree_com + 3 * B.root);
@@ -2340,7 +2343,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     // subtree com velocity and angular momentum about the subtree com, as sums over the
     // subtree (broadcast loop): V = sum m vc / M, L = sum h + sum m (x - X) x (vc - V) --
     // the closed form of the child-to-parent recursion (parallel-axis shifts)
-    {
+    if (obs) {
       float* mb = S + L.crb;  // scratch body masses (crb and the RNE forces are dead here)
       if (bl) mb[B.b] = B.mass;
       sync();
@@ -2369,7 +2372,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     }
     // the subtree momenta live in the RNE scratch, which the geom frames take next: their
     // sensors and outputs are written now
-    for (int s = lane; s < d.nsensor; s += kWave) {
+    for (int s = lane; obs && s < d.nsensor; s += kWave) {
       if (m.sensor_type[s] != SENS_SUBTREEANGMOM) continue;
       float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
       const int obj = m.sensor_objid[s];
@@ -2968,7 +2971,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     if (lane == 0) D.nefc[w] = nefc;  // every substep: classify_kernel sorts the Newton work by it
     STAMP(5);
     // =========================================================== sensors
-    for (int s = lane; s < d.nsensor; s += kWave) {
+    // (pos / vel stage: the last substep's only, see the subtree momenta above)
+    for (int s = lane; obs && s < d.nsensor; s += kWave) {
       float* out = D.sensordata + (size_t)w * d.nsensordata + m.sensor_adr[s];
       int obj = m.sensor_objid[s];
       int type = m.sensor_type[s];
@@ -3600,6 +3604,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       int type = m.sensor_type[s];
       // pos/vel-stage sensors run in phase A, acceleration-stage ones in phase C
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
+      // the accelerometers: the last substep's only (contact sensors run every substep: the
+      // contact air times read their found counts)
+      if (!last && !P->outputs_every && type != SENS_CONTACT) continue;
       // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
       // there are more than 64 of them (no transposed masks)
       if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0 &&
