@@ -1600,7 +1600,8 @@ __device__ __forceinline__ V3 point_vel_r(const float* S, const Lds& L, int b, i
 // lowest contact index).
 __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* Si, const Lds& L,
                                                      const DModel& m, const Dims& d, float* sd,
-                                                     int ncon, int maxmatch, int lane) {
+                                                     int ncon, int maxmatch, bool all,
+                                                     const Params* __restrict__ P, int lane) {
   const int c = lane;
   const bool valid = c < ncon;
   V3 fg = {0, 0, 0}, fc = {0, 0, 0};
@@ -1655,6 +1656,11 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     const int k = __ffsll((long long)rest) - 1;
     const int bits = __builtin_amdgcn_readlane(dbits, k), reduce = __builtin_amdgcn_readlane(dred, k);
     const int adr = __builtin_amdgcn_readlane(dadr, k), dim = __builtin_amdgcn_readlane(ddim, k);
+    if (!all) {  // not the last substep: only a contact air time's found count is read
+      bool air = false;
+      for (int i = 0; i < P->nair; i++) air |= P->air_found[i] == adr;
+      if (!air) continue;
+    }
     float* out = sd + adr;
     bool a1 = (m1 >> k) & 1ull, a2 = (m2 >> k) & 1ull;
     if (mtrunc) {
@@ -2061,7 +2067,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if (lane == 0 && stm > MINVAL) st3(S + L.subtree_com, ms * (1.0f / stm));
     }
     sync();
-    {
+    // site frames: for the sensors and the outputs (and phase C's accelerometers), the last
+    // substep's only (nothing in the dynamics reads a site)
+    if (last || P->outputs_every) {
       const float* spos = MF(site_pos);
       const float* squat = MF(site_quat);
       for (int s = lane; s < d.nsite; s += kWave) {
@@ -2185,8 +2193,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       sync();  // cdofdot (crb slot) read by every lane before the body forces land there
       if (bl) {
         const int b = B.b;
+        if (last || P->outputs_every) {  // phase C's post-constraint cacc: the last substep's
 #pragma unroll
-        for (int t = 0; t < 6; t++) gc[LC.cacc_v + 6 * b + t] = a[t];
+          for (int t = 0; t < 6; t++) gc[LC.cacc_v + 6 * b + t] = a[t];
+        }
         float f1[6], iv[6], f2[6];
         inert_mul(f1, S + L.cinert + 10 * b, a);
         inert_mul(iv, S + L.cinert + 10 * b, S + L.cvel + 6 * b);
@@ -3160,8 +3170,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
     cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
     cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
-    cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
-    cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    if (obs) {
+      cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
+      cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
+    }
     cp4(gc + LC.con_g1, S + L.con_g1, C4, lane);
     cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
     cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
@@ -3574,8 +3586,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     STAMP(15);
     // =========================================================== post-constraint acc
     // cacc(b) = cacc_v(b) + sum over the dofs moving b of cdof * qacc, cacc_v(b) = -gravity
-    // + sum cdofdot * qvel from phase A's RNE (broadcast loop over the dofs, no level syncs)
-    {
+    // + sum cdofdot * qvel from phase A's RNE (broadcast loop over the dofs, no level syncs);
+    // for the accelerometers and the cacc output: the last substep's only
+    if (last || P->outputs_every) {
       float a[6];
 #pragma unroll
       for (int t = 0; t < 6; t++) a[t] = S[L.cacc_v + 6 * B.b + t];
@@ -3606,7 +3619,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       if ((type == SENS_ACCELEROMETER || type == SENS_CONTACT) != (PH == 2)) continue;
       // the accelerometers: the last substep's only (contact sensors run every substep: the
       // contact air times read their found counts)
-      if (!last && !P->outputs_every && type != SENS_CONTACT) continue;
+      if (!last && !P->outputs_every) {
+        if (type != SENS_CONTACT) continue;
+        bool air = false;  // a contact sensor whose found count a contact air time reads
+        for (int i = 0; i < P->nair; i++) air |= P->air_found[i] == m.sensor_adr[s];
+        if (!air) continue;
+      }
       // single-slot contact sensors: wave-cooperative below (contact_sensors_wave), unless
       // there are more than 64 of them (no transposed masks)
       if (type == SENS_CONTACT && m.sensor_intprm[3 * s + 2] <= 1 && m.ncsens > 0 &&
@@ -3710,7 +3728,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     }
     if (kCon1<SP> || ncon <= kWave)
       contact_sensors_wave(S, Si, L, m, d, D.sensordata + (size_t)w * d.nsensordata, ncon,
-                           o.maxmatch, lane);
+                           o.maxmatch, last || P->outputs_every, P, lane);
     STAMP(11);
     if (last) {
       size_t wb = (size_t)w * nb;
