@@ -73,7 +73,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::qfrc_smooth, nv, B | Cp}, {&Lds::qacc_smooth, nv, B}, {&Lds::x, nv, B | Cp},
     {&Lds::Mx, nv, B}, {&Lds::grad, nv, 0}, {&Lds::srch, nv, B}, {&Lds::Ms, nv, B},
     {&Lds::qfrc_con, nv, B | Cp}, {&Lds::vtmp, nv, 0},
-    {&Lds::act_force, d.nu, Cp}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
+    {&Lds::act_force, d.nu, 0}, {&Lds::act_len, d.nu, 0}, {&Lds::act_vel, d.nu, 0},
     {&Lds::con_g1, C, A | Cp}, {&Lds::con_g2, C, A | Cp}, {&Lds::con_key, C, A},
     {&Lds::con_dist, C, A | Cp}, {&Lds::con_pos, 3 * C, A | Cp}, {&Lds::con_frame, 9 * C, 0},
     {&Lds::con_n, 3 * C, A | Cp},  // unit normals: cframe() rebuilds the frame where used
@@ -90,10 +90,13 @@ constexpr Lds make_lds(const Dims& d, int ph) {
   };
   int Lds::* const packB[] = {&Lds::ints, &Lds::M, &Lds::qacc_smooth, &Lds::qfrc_smooth,
                                      &Lds::efc_aref, &Lds::efc_D, &Lds::efc_J};
+  // C pack: first what every substep reads (the contact air times' geom matches, the
+  // integration's smooth force), then what only the last substep of a fused step reads (the
+  // acc-stage sensors, contact forces and outputs), then phase B's part
   int Lds::* const packC[] = {
+      &Lds::con_g1, &Lds::con_g2, &Lds::qfrc_smooth,
       &Lds::cdof, &Lds::cacc_v, &Lds::cvel, &Lds::subtree_com, &Lds::sxpos, &Lds::sxmat,
-      &Lds::act_force, &Lds::con_g1, &Lds::con_g2, &Lds::con_dist, &Lds::con_pos,
-      &Lds::con_n, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc, &Lds::qfrc_smooth,
+      &Lds::con_dist, &Lds::con_pos, &Lds::con_n, &Lds::con_mu, &Lds::con_dim, &Lds::con_efc,
       // written by phase B:
       &Lds::ints, &Lds::x, &Lds::qfrc_con, &Lds::efc_force};
   constexpr int kAbsent = 1 << 24;
@@ -105,7 +108,12 @@ constexpr Lds make_lds(const Dims& d, int ph) {
       if (sp.f == f) { L.*f = o; o += (sp.n + 3) & ~3; return; }  // 16-B aligned carve
   };
   if (ph == 1) for (auto f : packB) take(f);
-  if (ph == 2) for (auto f : packC) take(f);
+  if (ph == 2) {
+    for (auto f : packC) {
+      take(f);
+      if (f == &Lds::qfrc_smooth) L.packC_sub = o;
+    }
+  }
   L.pack_len = o;
   L.packC_b = ph == 2 ? L.ints : 0;  // start of the phase-B-written part of the C pack
   if (ph == 1) {

@@ -135,6 +135,7 @@ struct Lds {
   int ints;     // small int block: [0]=raw ncon [1]=nefc [2]=nlimit [3]=flags [4]=ncon [5]=niter
   int pack_len; // length of the phase's input pack (carved first; see make_lds)
   int packC_b;  // C carve: offset of the part of the pack written by phase B
+  int packC_sub; // C carve: end of the part every substep reads (the rest: the last substep's)
   int total;
 };
 

@@ -1613,16 +1613,18 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
     const int g1 = Si[L.con_g1 + c], g2 = Si[L.con_g2 + c];
     m1 = m.geom_csmask1[g1] & m.geom_csmask2[g2];
     m2 = m.geom_csmask1[g2] & m.geom_csmask2[g1];
-    dist = S[L.con_dist + c];
-    const int r0 = Si[L.con_efc + c];
-    if (Si[L.con_dim + c] == 1) {
-      fc.x = S[L.efc_force + r0];
-    } else {
-      float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
-      float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
-      fc = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+    if (all) {  // (before the last substep only found counts are computed: no forces)
+      dist = S[L.con_dist + c];
+      const int r0 = Si[L.con_efc + c];
+      if (Si[L.con_dim + c] == 1) {
+        fc.x = S[L.efc_force + r0];
+      } else {
+        float e0 = S[L.efc_force + r0], e1 = S[L.efc_force + r0 + 1];
+        float e2 = S[L.efc_force + r0 + 2], e3 = S[L.efc_force + r0 + 3];
+        fc = {e0 + e1 + e2 + e3, (e0 - e1) * S[L.con_mu + 2 * c], (e2 - e3) * S[L.con_mu + 2 * c + 1]};
+      }
+      fg = frame_tv(S + L.con_n + 3 * c, fc);
     }
-    fg = frame_tv(S + L.con_n + 3 * c, fc);
   }
   // the sensors' descriptors, lane k = k-th single-slot contact sensor (ncsens <= 64): the
   // loop below reads them with v_readlane instead of a dependent scalar-load chain per sensor
@@ -2261,7 +2263,6 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       const float x = rl(act_gf, u);
       if (lane == __builtin_amdgcn_readlane(Ar.dof, u)) qact_i += x;
     }
-    if (lane < ((nu + 3) & ~3)) gc[LC.act_force + lane] = act_f;  // C pack (zero padding)
     float qfs_i = 0.f;  // lane i < nv: qfrc_smooth of dof i
     for (int i = lane; i < nvp; i += kWave) {  // nv <= 64: one pass, lane i
       if (i >= nv) {  // the smooth solve's right-hand side is zero on the padding dofs
@@ -3167,21 +3168,26 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gw + LB.ints, S + L.ints, 8, lane);  // (qacc_smooth, qfrc_smooth: stored above)
     cp4(gw + LB.efc_aref, S + L.efc_aref, nr4, lane);
     cp4(gw + LB.efc_D, S + L.efc_D, nr4, lane);
-    cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
-    cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
-    cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
+    // (the C pack's last-substep part only in the last substep: carve.h packC)
+    if (obs) {
+      cp4(gc + LC.cdof, S + L.cdof, 6 * nvp, lane);
+      cp4(gc + LC.cvel, S + L.cvel, (6 * nb + 3) & ~3, lane);
+      cp4(gc + LC.subtree_com, S + L.subtree_com, (3 * nb + 3) & ~3, lane);
+    }
     if (obs) {
       cp4(gc + LC.sxpos, S + L.sxpos, (3 * d.nsite + 3) & ~3, lane);
       cp4(gc + LC.sxmat, S + L.sxmat, (9 * d.nsite + 3) & ~3, lane);
     }
     cp4(gc + LC.con_g1, S + L.con_g1, C4, lane);
     cp4(gc + LC.con_g2, S + L.con_g2, C4, lane);
-    cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
-    cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
-    cp4(gc + LC.con_n, S + L.con_n, (3 * C + 3) & ~3, lane);  // normals (C rebuilds frames)
-    cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
-    cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
-    cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
+    if (obs) {
+      cp4(gc + LC.con_dist, S + L.con_dist, C4, lane);
+      cp4(gc + LC.con_pos, S + L.con_pos, (3 * C + 3) & ~3, lane);
+      cp4(gc + LC.con_n, S + L.con_n, (3 * C + 3) & ~3, lane);  // normals (C rebuilds frames)
+      cp4(gc + LC.con_mu, S + L.con_mu, (2 * C + 3) & ~3, lane);
+      cp4(gc + LC.con_dim, S + L.con_dim, C4, lane);
+      cp4(gc + LC.con_efc, S + L.con_efc, C4, lane);
+    }
     STAMP(14);
   } else if constexpr (PH == 1) {
     // ----------------------------------------------------------- phase B (Newton)
@@ -3553,7 +3559,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     cp4(gc + LC.ints, S + L.ints, 8, lane);
     cp4(gc + LC.x, S + L.x, nvq, lane);
     cp4(gc + LC.qfrc_con, S + L.qfrc_con, nvq, lane);
-    cp4(gc + LC.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
+    if (last || P->outputs_every)  // phase C reads the row forces in the last substep only
+      cp4(gc + LC.efc_force, S + L.efc_force, (nefc + 3) & ~3, lane);
     if (last) {
       for (int i = lane; i < nv; i += kWave) {
         size_t k = (size_t)w * nv + i;
@@ -3565,7 +3572,14 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
     STAMP(14);
   } else {
     // ----------------------------------------------------------- phase C
-    cp_pack(S, gc, L.pack_len, lane);  // C pack: carve offsets == pack offsets
+    // C pack (carve offsets == pack offsets): before the last substep of a fused step only
+    // the part every substep reads and phase B's ints / qacc / qfrc_constraint (carve.h)
+    if (last || P->outputs_every) {
+      cp_pack(S, gc, L.pack_len, lane);
+    } else {
+      cp_pack(S, gc, L.packC_sub, lane);
+      cp_pack(S + L.ints, gc + L.ints, L.efc_force - L.ints, lane);
+    }
     // the implicit-integration factor (phase A stored it): in flight with the pack
     float Fa[NR], Fdv = 1.f;
     if (integrate) rows_load_factor_ltr_raw<NR>(Fa, Fdv, gf, nvp, lane);
