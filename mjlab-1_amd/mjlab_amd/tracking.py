@@ -698,9 +698,12 @@ def make_tracking_env_cfg():
     observations=observations,
     actions=actions, commands=commands, events=events, rewards=rewards,
     terminations=terminations,
-    # the reference's njmax (250 rows per world) held in full: random-action tracking worlds
-    # reach 186 rows and 49 contacts, past the default 48 / 160 carve
-    sim=SimulationCfg(nconmax=35, njmax=250, engine_capacity=(64, 256),
+    # the reference's njmax (250 rows per world) as the max capacity; random-action tracking
+    # worlds reach 190 rows and 49 contacts, past the default 48 / 160 carve, so the fast
+    # carve is 56 / 200 (a world past it is re-solved at 250 / 250).  Measured (round 5):
+    # 56 / 200 2.72 M env-steps/s, 64 / 250 2.68 M, 48 / 160 2.46 M (73 re-solves per 100
+    # env steps); DESIGN.md section 3
+    sim=SimulationCfg(nconmax=35, njmax=250, engine_capacity=(56, 200),
                       mujoco=MujocoCfg(timestep=0.005, iterations=10, ls_iterations=20)),
     decimation=4, episode_length_s=10.0)
 

@@ -1,6 +1,6 @@
 """Per-world engine capacity (sim.world_capacity): the default 48-contact / 160-row carve,
-the tracking task's engine_capacity holding the reference's njmax (250 rows,
-`tasks/tracking/tracking_env_cfg.py:307-308`), and the specialised kernels' table
+the tracking task's 56 / 200 fast carve under the reference's njmax (250 rows,
+`tasks/tracking/tracking_env_cfg.py:307-308`) as its max capacity, and the specialised kernels' table
 (specs.inc) carrying the same capacities, so the bench configs never fall back to the
 generic kernels."""
 import os
@@ -24,8 +24,8 @@ def test_default_capacity_clamps_to_the_fast_carve():
 def test_tracking_holds_the_reference_njmax():
   from mjlab_amd.tracking import make_tracking_env_cfg
   cfg = make_tracking_env_cfg()
-  assert cfg.sim.njmax == 250 and cfg.sim.engine_capacity == (64, 256)
-  assert world_capacity(cfg.sim, load_scene("g1_tracking")) == (64, 250)
+  assert cfg.sim.njmax == 250 and cfg.sim.engine_capacity == (56, 200)
+  assert world_capacity(cfg.sim, load_scene("g1_tracking")) == (56, 200)
 
 
 def test_engine_capacity_bounds():
@@ -60,7 +60,7 @@ def test_specs_carry_the_task_capacities():
   caps = {}
   for mm in re.finditer(r"^MJX_SPEC\(\d+, (\w+),.*, (\d+), (\d+)\)$", text, re.M):
     caps.setdefault(mm.group(1), []).append((int(mm.group(2)), int(mm.group(3))))
-  assert caps["g1_tracking"] == [(64, 250), (48, 160), (250, 250)]
+  assert caps["g1_tracking"] == [(56, 200), (48, 160), (250, 250)]
   for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
     assert caps[name] == [(48, 160), (300, 300)], name
   # Go1: its tasks' engine_capacity (24, 96) first, the default and the max carve
