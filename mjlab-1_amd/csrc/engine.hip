@@ -390,6 +390,26 @@ static bool ovf_stream_env() {
   return on;
 }
 
+// Order of the concurrent branches in a captured graph.  Graph replay (ROCm 7 clr) keeps the
+// first child of a fork on the launch queue and starts every further child on a parallel
+// queue, whose start and join each wait on a cross-queue signal (kernel trace, G1 4,096:
+// classify -> bulk chain 12 us on the parallel queue, 5.5 us in line).  So while capturing,
+// the models without row classes capture their critical launch (the range chain, phase B)
+// ahead of the re-solve chain's: Go1 flat 8,192 +1.2 %, rough Go1 +0.6 % (two interleaved
+// rounds).  The row-class fork keeps its order (the full-capacity class first, on the launch
+// queue): bulk chain first measured G1 2.94 -> 2.38 M, tracking 2.71 -> 2.19 M, since the
+// full class's long-latency worlds then start behind the bulk chain's and end last.
+// MJX355_MAIN_FIRST=0 / 1 forces it off / on.
+static bool main_first(hipStream_t st) {
+  static const int mode = [] {
+    const char* e = getenv("MJX355_MAIN_FIRST");
+    return e ? atoi(e) : -1;
+  }();
+  if (mode >= 0) return mode != 0;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+
 hipError_t launch_step(const Params& host, const Params* dev, int nworld, int nsubstep,
                        int integrate, const uint8_t* mask, hipStream_t stream,
                        const SideStream* side, const Params* hbig, const Params* dbig) {
@@ -492,15 +512,25 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       // split batches: in line behind phase C on the split stream (a fork from a split
       // stream is a second-level fork, which breaks graph capture; capi.cpp)
       const bool ovf_inline = ovf && nsplit > 1;
-      auto fork_ovf = [&]() {
+      // (record the fork before the stream's next launch; launch the chain after it while
+      // capturing: main_first)
+      auto ovf_record = [&]() {
         if (!ovf || ovf_inline) return hipSuccess;
-        hipError_t e2 = hipEventRecord(side->ovf_fork[k], st);
-        if (e2 == hipSuccess) e2 = hipStreamWaitEvent(side->ovf[k], side->ovf_fork[k], 0);
+        return hipEventRecord(side->ovf_fork[k], st);
+      };
+      auto ovf_launch = [&]() {
+        if (!ovf || ovf_inline) return hipSuccess;
+        hipError_t e2 = hipStreamWaitEvent(side->ovf[k], side->ovf_fork[k], 0);
         if (e2 == hipSuccess)
           ovf_chain(host, dev, *hbig, dbig, side->ovf[k], k, w0, w1, sub, nsubstep, integrate,
                     nexta, false);
         return e2;
       };
+      auto fork_ovf = [&]() {
+        hipError_t e2 = ovf_record();
+        return e2 == hipSuccess ? ovf_launch() : e2;
+      };
+      const bool mfirst = main_first(st);
       auto join_ovf = [&]() {
         if (!ovf) return hipSuccess;
         if (ovf_inline) {
@@ -577,17 +607,21 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         if (ovf_stream_env() && (e = join_ovf()) != hipSuccess) return e;
         if (piped) continue;
       } else if (fR) {
-        if ((e = fork_ovf()) != hipSuccess) return e;
+        if ((e = ovf_record()) != hipSuccess) return e;
+        if (!mfirst && (e = ovf_launch()) != hipSuccess) return e;
         const int selx = k | (last ? 0 : kSelChainA) | (((sub + 1) & 1) ? kSelAPar : 0) |
                          (sub + 1 == nsubstep - 1 ? kSelNextLast : 0);
         hipLaunchKernelGGL(fR, dim3(n), dim3(kWave), lds_chain(host, 0, !last), st, dev, w0, w1, selx,
                            last, integrate, mask);
+        if (mfirst && (e = ovf_launch()) != hipSuccess) return e;
         if ((e = join_ovf()) != hipSuccess) return e;
         continue;
       } else {
-        if ((e = fork_ovf()) != hipSuccess) return e;
+        if ((e = ovf_record()) != hipSuccess) return e;
+        if (!mfirst && (e = ovf_launch()) != hipSuccess) return e;
         hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
                            0, mask);
+        if (mfirst && (e = ovf_launch()) != hipSuccess) return e;
       }
       hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), st, dev, w0, w1, k, last,
                          integrate, mask);

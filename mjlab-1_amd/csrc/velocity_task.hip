@@ -188,37 +188,40 @@ __device__ __forceinline__ JointSums joint_sums(const mjxTaskDesc& t, int e, int
     // jump terms (tasks/jump/mdp/rewards.py): action acceleration, actuator torques,
     // explosive_takeoff's |actuator_force[i] * joint_vel[i]| (actuator i paired with joint i,
     // as the reference's element-wise product), joint-velocity variance (two passes)
-    float jv_sum = 0.f;
-    for (int j = lane; j < nj; j += 64) {
+    // nj <= 64 (mjx_task_create): lane j holds joint j, straight-line code so the loads of
+    // the env's joints issue together
+    float jv = 0.f;
+    if (lane < nj) {
+      const int j = lane;
       const size_t i = (size_t)e * nj + j;
       const float a2 = t.action[i] - 2.f * t.prev_action[i] + t.prev_prev_action[i];
-      r.acc2 += a2 * a2;
+      r.acc2 = a2 * a2;
       const float f = t.actuator_force[(size_t)e * t.nu + t.act_ctrl[j]];
-      r.torque2 += f * f;
-      const float jv = t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]];
-      if ((t.explosive_joints >> j) & 1ull) r.power += fabsf(f * jv);
-      jv_sum += jv;
+      r.torque2 = f * f;
+      jv = t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]];
+      if ((t.explosive_joints >> j) & 1ull) r.power = fabsf(f * jv);
     }
-    const float jv_mean = wave_add(jv_sum) / (float)nj;
-    for (int j = lane; j < nj; j += 64) {
-      const float d = t.qvel[(size_t)e * t.nv + t.joint_v_adr[j]] - jv_mean;
-      r.jv_var += d * d;
+    const float jv_mean = wave_add(jv) / (float)nj;
+    if (lane < nj) {
+      const float d = jv - jv_mean;
+      r.jv_var = d * d;
     }
     r.acc2 = wave_add(r.acc2);
     r.torque2 = wave_add(r.torque2);
     r.power = wave_add(r.power);
     r.jv_var = wave_add(r.jv_var) / (float)nj;
   }
-  for (int j = lane; j < nj; j += 64) {
+  if (lane < nj) {
+    const int j = lane;
     const float q = t.qpos[(size_t)e * t.nq + t.joint_q_adr[j]];
     const float d = q - t.default_joint_pos[j];
     const float s0 = t.std_standing[j], s1 = t.std_walking[j], s2 = t.std_running[j];
-    r.pose[0] += d * d / (s0 * s0);
-    r.pose[1] += d * d / (s1 * s1);
-    r.pose[2] += d * d / (s2 * s2);
-    r.lim += fmaxf(t.soft_lo[j] - q, 0.f) + fmaxf(q - t.soft_hi[j], 0.f);
+    r.pose[0] = d * d / (s0 * s0);
+    r.pose[1] = d * d / (s1 * s1);
+    r.pose[2] = d * d / (s2 * s2);
+    r.lim = fmaxf(t.soft_lo[j] - q, 0.f) + fmaxf(q - t.soft_hi[j], 0.f);
     const float da = t.action[(size_t)e * nj + j] - t.prev_action[(size_t)e * nj + j];
-    r.rate += da * da;
+    r.rate = da * da;
   }
   for (int k = 0; k < 3; k++) r.pose[k] = wave_add(r.pose[k]);
   r.lim = wave_add(r.lim);
@@ -277,7 +280,6 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
   const int64_t len = t.episode_length[e] + 1;
   const Root r = root_state(t, e);
   const float* sd = t.sensordata + (size_t)e * t.nsensordata;
-  if (lane == 0) t.episode_length[e] = len;
   stage_env(t, e, r, sd, lane, ev);
   const FootVals* F = ev->f;
   // ---- terminations (termination_manager.py:87-97)
@@ -315,8 +317,20 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
   }
   // ---- rewards (reward_manager.py:77-91)
   const float dt = t.step_dt;
-  const float* cmd = t.command + (size_t)e * 3;
   const int nj = t.njoint;
+  // every global value a term reads, loaded before the switch: the wave walks the cases one
+  // after another (lane per term), so a load inside a case is a round trip of its own
+  // (the twist command is [nworld, 3]; the jump command [nworld, 1], which no term reads)
+  float cmd[3] = {0.f, 0.f, 0.f};
+  if (t.command_kind == MJX_CMD_TWIST) {
+    const float* cmdp = t.command + (size_t)e * 3;
+    cmd[0] = cmdp[0]; cmd[1] = cmdp[1]; cmd[2] = cmdp[2];
+  }
+  float hm[3] = {0.f, 0.f, 0.f};
+  if (t.angmom_adr >= 0) { hm[0] = sd[t.angmom_adr]; hm[1] = sd[t.angmom_adr + 1]; hm[2] = sd[t.angmom_adr + 2]; }
+  const float selfcol = t.selfcol_found_adr >= 0 ? sd[t.selfcol_found_adr] : 0.f;
+  float* es = t.episode_sums + (size_t)(lane < t.nreward ? lane : 0) * t.nworld + e;
+  const float es_old = lane < t.nreward ? *es : 0.f;
   float total = 0.f;
   do {
     const int k = lane;
@@ -349,8 +363,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         f = ev->ocv0 * ev->ocv0 + ev->ocv1 * ev->ocv1;
         break;
       case MJX_RW_ANGMOM: {  // rewards.py:110-120
-        const float* h = sd + t.angmom_adr;
-        f = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+        f = hm[0] * hm[0] + hm[1] * hm[1] + hm[2] * hm[2];
         atomicAdd(&acc->metric_sum[MJX_MT_ANGMOM], sqrtf(f));
         atomicAdd(&acc->metric_cnt[MJX_MT_ANGMOM], 1.f);
       } break;
@@ -418,7 +431,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
         atomicAdd(&acc->metric_cnt[MJX_MT_LANDING], n);
         f *= command_gate(t, cmd, p0, p1);  // p1: command_name None
       } break;
-      case MJX_RW_SELF_COLLISION: f = sd[t.selfcol_found_adr]; break;  // rewards.py:88-95
+      case MJX_RW_SELF_COLLISION: f = selfcol; break;  // rewards.py:88-95
       // ---- jump task (tasks/jump/mdp/rewards.py; p0 / p1 as noted)
       case MJX_RW_JUMP_HEIGHT: {  // :20-70, p0 target height, p1 std; stateful, never reset
         const float hz = t.xpos[((size_t)e * t.nbody + t.root_body) * 3 + 2];
@@ -485,8 +498,7 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
     float v = f * w * dt;
     if (!isfinite(v)) v = 0.f;  // nan_to_num
     total = v;
-    float* es = t.episode_sums + (size_t)k * t.nworld + e;
-    const float es_new = *es + v;
+    const float es_new = es_old + v;
     *sr = v / dt;
     // ---- reset bookkeeping of this step's resets (reward manager log)
     if (reset) {
@@ -510,6 +522,8 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
       *es = 0.f;
     }
   }
+  // stored after the env's loads (a store ahead of them would hold up their waits)
+  if (lane == 0) t.episode_length[e] = len;
   // ---- reset bookkeeping (termination/command manager logs)
   if (reset) {
     if (lane < t.ntermination && tm_v) atomicAdd(&acc->term[lane], 1.f);
