@@ -544,8 +544,13 @@ __device__ __forceinline__ void post_env(const mjxTaskDesc& t, const int e, cons
 constexpr int kPostEnvs = 16;
 constexpr int kAccN = (int)(sizeof(Acc) / sizeof(float));
 static_assert(kAccN <= 128, "k_accum: thread per accumulator field");
-__global__ __launch_bounds__(64 * kPostEnvs) void k_post(const mjxTaskDesc* __restrict__ T,
-                                                        float* __restrict__ part) {
+// WPE: waves per SIMD the register budget targets.  One 16-wave block per CU fits at the
+// kernel's natural 68-70 VGPRs (7 waves / SIMD); batches of more than one block per CU
+// (Go1 8,192, jump 16,384 envs) take the 64-VGPR form, two blocks per CU, half the rounds
+// (a few spilled registers)
+template <int WPE>
+__global__ __launch_bounds__(64 * kPostEnvs, WPE) void k_post(const mjxTaskDesc* __restrict__ T,
+                                                          float* __restrict__ part) {
   const mjxTaskDesc& t = *T;
   __shared__ Acc sh;
   float* shf = reinterpret_cast<float*>(&sh);
@@ -861,7 +866,7 @@ __device__ void obs_elem(const mjxTaskDesc& t, int e, int i) {
 // the wave-level hand-off replaces the launch boundary of two kernels (observe, then
 // observations), one dispatch and gap fewer on the env step's critical path.
 constexpr int kObsEnvs = 4;
-__global__ __launch_bounds__(64 * kObsEnvs) void k_observe_obs(const mjxTaskDesc* __restrict__ T,
+__global__ __launch_bounds__(64 * kObsEnvs, 8) void k_observe_obs(const mjxTaskDesc* __restrict__ T,
                                                                Acc* __restrict__ acc) {
   const mjxTaskDesc& t = *T;
   if (blockIdx.x == 0 && threadIdx.x == 0) observe_logs(t, acc);
@@ -935,6 +940,7 @@ struct mjxTask_ {
   mjxt::Acc* acc = nullptr;
   float* part = nullptr;  // [nblock][kAccN] k_post block partials
   int nworld = 0;
+  int ncu = 256;  // compute units of the device the task was created on
 };
 
 static thread_local std::string g_task_err;
@@ -962,6 +968,12 @@ int mjx_task_create(const mjxTaskDesc* desc, mjxTask** out) {
       hipMalloc((void**)&t->part, sizeof(float) * mjxt::kAccN * (nblock > 0 ? nblock : 1)) != hipSuccess) {
     delete t;
     return task_fail("hipMalloc failed");
+  }
+  {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      t->ncu = ncu;
   }
   if (hipMemcpy(t->dev, desc, sizeof(mjxTaskDesc), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(t->acc, 0, sizeof(mjxt::Acc)) != hipSuccess) {
@@ -1003,8 +1015,12 @@ int mjx_task_substep(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_substep, t-
 int mjx_task_post(mjxTask* t, void* stream) {
   if (!t) return task_fail("null task");
   const int nblock = (t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs;
-  hipLaunchKernelGGL(mjxt::k_post, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
-                     t->dev, t->part);
+  if (nblock > t->ncu)
+    hipLaunchKernelGGL(mjxt::k_post<8>, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
+                       t->dev, t->part);
+  else
+    hipLaunchKernelGGL(mjxt::k_post<1>, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
+                       t->dev, t->part);
   hipLaunchKernelGGL(mjxt::k_accum, dim3(1), dim3(128 * mjxt::kAccChunks), 0, (hipStream_t)stream,
                      t->part, nblock, t->acc);
   hipError_t e = hipGetLastError();
