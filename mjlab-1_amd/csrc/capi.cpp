@@ -768,7 +768,7 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
     if (e != hipSuccess) { delete s; return fail(std::string("hfield frames: ") + hipGetErrorString(e)); }
   }
   // initial state: mj_resetData
-  if (mjx::launch_reset(d, s->dm, s->dd, nullptr, nworld, nullptr) != hipSuccess) {
+  if (mjx::launch_reset(d, s->dm, s->dd, nullptr, nworld, s->con_stride, nullptr) != hipSuccess) {
     delete s;
     return fail("reset launch failed");
   }
@@ -834,7 +834,7 @@ int mjx_sim_track_air_time(mjxSim* s, int n, const int32_t* found_adr, float* cu
 
 int mjx_reset(mjxSim* s, const uint8_t* mask, void* stream) {
   if (!s) return fail("null sim");
-  hipError_t e = mjx::launch_reset(s->d, s->dm, s->dd, mask, s->nworld, (hipStream_t)stream);
+  hipError_t e = mjx::launch_reset(s->d, s->dm, s->dd, mask, s->nworld, s->con_stride, (hipStream_t)stream);
   if (e != hipSuccess) return fail(std::string("reset launch: ") + hipGetErrorString(e));
   return 0;
 }

@@ -262,7 +262,7 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
 // Newton row classes (capacities ascending into caps[]); returns how many are used.
 int choose_row_classes(const Dims& d, int spec, int (&caps)[kRowClasses]);
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
-                        int nworld, hipStream_t stream);
+                        int nworld, int con_stride, hipStream_t stream);
 hipError_t launch_marker(int tag, hipStream_t stream);  // empty kernel (profiling brackets)
 
 }  // namespace mjx

@@ -9,7 +9,8 @@
 namespace mjx {
 
 // --------------------------------------------------------------------------- reset
-__global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int nworld) {
+__global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int nworld,
+                             int con_stride) {
   const int w = blockIdx.x;
   if (w >= nworld) return;
   if (mask && !mask[w]) return;
@@ -34,7 +35,20 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
     for (int t = 0; t < 3; t++) D.mocap_pos[((size_t)w * d.nmocap + mid) * 3 + t] = bp[t];
     for (int t = 0; t < 4; t++) D.mocap_quat[((size_t)w * d.nmocap + mid) * 4 + t] = bq[t];
   }
-  if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; }
+  // contact output slots (mj_resetData: no contacts) up to the last output's reach, and the
+  // output bookkeeping of engine_counters [6] / [7] with them (phase A's output trims to it)
+  int* wsv = D.wstats + 8 * (size_t)w;
+  const int nout = min(con_stride, max(wsv[6], wsv[7]));
+  const size_t wc = (size_t)w * con_stride;
+  for (int c = lane; c < nout; c += blockDim.x) {
+    D.contact_dist[wc + c] = 0.f;
+    D.contact_geom[(wc + c) * 2] = -1;
+    D.contact_geom[(wc + c) * 2 + 1] = -1;
+    for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = 0.f;
+    for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = 0.f;
+  }
+  __syncthreads();
+  if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; wsv[6] = 0; wsv[7] = 0; }
 }
 
 // ------------------------------------------------------------------ Newton work lists
@@ -510,8 +524,12 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       // the re-solve chain: forked after this substep's phase A (and classify), joined at the
       // end of the substep -- the empty chain overlaps the class launches
       // split batches: in line behind phase C on the split stream (a fork from a split
-      // stream is a second-level fork, which breaks graph capture; capi.cpp)
-      const bool ovf_inline = ovf && nsplit > 1;
+      // stream is a second-level fork, which breaks graph capture; capi.cpp).  Also in line
+      // behind a range chain on an unsplit batch: the chain's B, C and fused next A skip the
+      // listed worlds by ovf_flag[w], which the re-solve chain's next phase A rewrites, so a
+      // concurrent re-solve could clear a flag before the range chain's workgroup for that
+      // world reads it and the world would run one extra B -> C -> A.
+      const bool ovf_inline = ovf && (nsplit > 1 || fR != nullptr);
       // (record the fork before the stream's next launch; launch the chain after it while
       // capturing: main_first)
       auto ovf_record = [&]() {
@@ -733,9 +751,10 @@ hipError_t launch_marker(int tag, hipStream_t stream) {
 }
 
 hipError_t launch_reset(const Dims& d, const DModel& m, const DData& dd, const uint8_t* mask,
-                        int nworld, hipStream_t stream) {
+                        int nworld, int con_stride, hipStream_t stream) {
   if (nworld <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reset_kernel, dim3(nworld), dim3(kWave), 0, stream, d, m, dd, mask, nworld);
+  hipLaunchKernelGGL(reset_kernel, dim3(nworld), dim3(kWave), 0, stream, d, m, dd, mask, nworld,
+                     con_stride);
   return hipGetLastError();
 }
 

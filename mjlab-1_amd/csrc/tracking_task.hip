@@ -10,6 +10,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdio.h>
+
 #include <string>
 
 #include "../../include/mjx355_task.h"
@@ -678,6 +680,67 @@ static int track_launched(const char* what) {
   return e == hipSuccess ? 0 : track_fail(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// The tracking descriptor's indices and kinds against its declared sizes (as validate_task in
+// velocity_task.hip): a mismatch is an error code, never a device fault.
+static std::string validate_track(const mjxTrackDesc& t) {
+  auto in = [](int v, int n) { return v >= 0 && v < n; };
+  auto span = [](int adr, int len, int n) { return adr >= 0 && adr + len <= n; };
+  char buf[256];
+  auto err = [&](const char* fmt, int a, int b) {
+    snprintf(buf, sizeof buf, fmt, a, b);
+    return std::string(buf);
+  };
+  if (t.nworld <= 0 || t.nq <= 0 || t.nv <= 0 || t.nu <= 0 || t.nbody <= 0 || t.nsensordata < 0)
+    return "non-positive model or batch size";
+  if (t.njoint < 1) return "no joints";
+  const void* need[] = {t.qpos, t.qvel, t.ctrl, t.xpos, t.xquat, t.cvel, t.subtree_com, t.sensordata,
+                        t.encoder_bias, t.env_origins, t.m_joint_pos, t.m_joint_vel, t.m_body_pos,
+                        t.m_body_quat, t.m_body_lin, t.m_body_ang, t.action, t.prev_action,
+                        t.prev_prev_action, t.joint_pos_target, t.episode_length, t.time_steps,
+                        t.body_pos_rel, t.body_quat_rel, t.bin_failed_count, t.current_bin_failed,
+                        t.sampling, t.metrics, t.time_left, t.command_counter, t.episode_sums,
+                        t.step_reward, t.reward_buf, t.reset_buf, t.terminated, t.time_outs,
+                        t.term_dones, t.resample_mask, t.obs_policy, t.obs_critic, t.log_reward,
+                        t.log_termination, t.log_metric, t.step_counter};
+  for (size_t i = 0; i < sizeof need / sizeof need[0]; i++)
+    if (!need[i]) return err("required buffer %d of the descriptor is null", (int)i, 0);
+  if (t.has_push && !t.push_time_left) return "has_push without push_time_left";
+  if (!in(t.root_body, t.nbody)) return err("root_body %d outside [0, %d)", t.root_body, t.nbody);
+  if (!span(t.free_q_adr, 7, t.nq)) return err("free joint qpos %d + 7 past nq %d", t.free_q_adr, t.nq);
+  if (!span(t.free_v_adr, 6, t.nv)) return err("free joint qvel %d + 6 past nv %d", t.free_v_adr, t.nv);
+  for (int j = 0; j < t.njoint; j++) {
+    if (!in(t.joint_q_adr[j], t.nq)) return err("joint %d qpos address outside [0, nq=%d)", j, t.nq);
+    if (!in(t.joint_v_adr[j], t.nv)) return err("joint %d qvel address outside [0, nv=%d)", j, t.nv);
+    if (!in(t.ctrl_of_action[j], t.nu)) return err("action %d ctrl index outside [0, nu=%d)", j, t.nu);
+    if (!in(t.target_of_action[j], t.njoint))
+      return err("action %d target column outside [0, njoint=%d)", j, t.njoint);
+  }
+  for (int k = 0; k < t.nmb; k++)
+    if (!in(t.robot_body[k], t.nbody)) return err("command body %d: model body outside [0, %d)", k, t.nbody);
+  if (!in(t.anchor_motion, t.nmb)) return err("anchor_motion %d outside [0, nmb=%d)", t.anchor_motion, t.nmb);
+  if (!in(t.anchor_body, t.nbody)) return err("anchor_body %d outside [0, %d)", t.anchor_body, t.nbody);
+  if (!span(t.imu_lin_vel_adr, 3, t.nsensordata) || !span(t.imu_ang_vel_adr, 3, t.nsensordata))
+    return err("imu velocity sensors (%d, %d) + 3 past nsensordata", t.imu_lin_vel_adr, t.imu_ang_vel_adr);
+  if (t.selfcol_found_adr >= t.nsensordata)
+    return err("self-collision sensor %d outside [-1, %d)", t.selfcol_found_adr, t.nsensordata);
+  if (t.max_episode_length <= 0 || !(t.step_dt > 0.f)) return "non-positive episode length or step_dt";
+  if (t.sampling_mode < 0 || t.sampling_mode > 2) return err("unknown sampling_mode %d", t.sampling_mode, 0);
+  const uint32_t body_bits = t.nmb >= 32 ? 0xffffffffu : (1u << t.nmb) - 1u;
+  for (int k = 0; k < t.nreward; k++) {
+    const int kind = t.reward_kind[k];
+    if (!in(kind, MJX_TR_SELF_COLLISION + 1)) return err("reward %d: unknown kind %d", k, kind);
+    if (kind == MJX_TR_SELF_COLLISION && t.selfcol_found_adr < 0)
+      return err("reward %d: kind %d needs selfcol_found_adr", k, kind);
+    if (t.reward_bodies[k] & ~body_bits) return err("reward %d: body mask past nmb %d", k, t.nmb);
+  }
+  for (int k = 0; k < t.ntermination; k++) {
+    const int kind = t.termination_kind[k];
+    if (!in(kind, MJX_TT_BODY_POS + 1)) return err("termination %d: unknown kind %d", k, kind);
+    if (t.termination_bodies[k] & ~body_bits) return err("termination %d: body mask past nmb %d", k, t.nmb);
+  }
+  return "";
+}
+
 extern "C" {
 
 size_t mjx_track_desc_size(void) { return sizeof(mjxTrackDesc); }
@@ -693,6 +756,10 @@ int mjx_track_create(const mjxTrackDesc* d, mjxTrack** out) {
   if (d->ncritic != 5 * nj + 9 * nmb + 15 ||
       d->npolicy != 5 * nj + 9 + (d->policy_anchor_pos ? 3 : 0) + (d->policy_lin_vel ? 3 : 0))
     return track_fail("observation sizes do not match the tracking layout");
+  {
+    const std::string why = validate_track(*d);
+    if (!why.empty()) return track_fail("mjx_track_create: " + why);
+  }
   auto* t = new mjxTrack_();
   t->host = *d;
   t->nworld = d->nworld;

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <string>
@@ -953,12 +954,143 @@ extern "C" {
 
 size_t mjx_task_desc_size(void) { return sizeof(mjxTaskDesc); }
 
+}  // extern "C"
+
+// Every index the kernels dereference, checked against the sizes the descriptor declares, and
+// every term / command kind against the buffers and layout it reads, before anything reaches
+// the device: a mismatch is an error code and mjx_task_last_error, never an out-of-bounds
+// access on the GPU (round 5: a twist-command read on the jump task's [nworld, 1] command
+// faulted the device).  Returns "" when the descriptor is consistent.
+static std::string validate_task(const mjxTaskDesc& t) {
+  auto in = [](int v, int n) { return v >= 0 && v < n; };
+  auto span = [](int adr, int len, int n) { return adr >= 0 && adr + len <= n; };
+  char buf[256];
+  auto err = [&](const char* fmt, int a, int b) {
+    snprintf(buf, sizeof buf, fmt, a, b);
+    return std::string(buf);
+  };
+  if (t.nworld <= 0 || t.nq <= 0 || t.nv <= 0 || t.nu <= 0 || t.nbody <= 0 || t.nsensordata < 0 ||
+      t.nsite < 0)
+    return "non-positive model or batch size";
+  if (t.njoint < 1 || t.njoint > MJX_TASK_MAX_JOINTS || t.nfeet < 0 || t.nfeet > MJX_TASK_MAX_FEET ||
+      t.nreward < 0 || t.nreward > MJX_TASK_MAX_TERMS || t.ntermination < 0 ||
+      t.ntermination > MJX_TASK_MAX_TERMS || t.nillegal < 0 || t.nillegal > MJX_TASK_MAX_CONTACT_SLOTS)
+    return "task descriptor exceeds compiled capacities";
+  if (t.command_kind != MJX_CMD_TWIST && t.command_kind != MJX_CMD_JUMP)
+    return err("unknown command_kind %d (%d kinds)", t.command_kind, 2);
+  // buffers every launch reads or writes
+  const void* need[] = {t.qpos, t.qvel, t.ctrl, t.time, t.xpos, t.xquat, t.cvel, t.subtree_com,
+                        t.sensordata, t.env_origins, t.action, t.prev_action, t.prev_prev_action,
+                        t.joint_pos_target, t.episode_length, t.command, t.cmd_time_left,
+                        t.command_counter, t.metric_err_xy, t.metric_err_yaw, t.episode_sums,
+                        t.step_reward, t.reward_buf, t.reset_buf, t.terminated, t.time_outs,
+                        t.term_dones, t.obs_policy, t.obs_critic, t.log_reward, t.log_termination,
+                        t.log_command, t.log_metric, t.step_counter, t.is_standing_env};
+  for (size_t i = 0; i < sizeof need / sizeof need[0]; i++)
+    if (!need[i]) return err("required buffer %d of the descriptor is null", (int)i, 0);
+  if (t.nfeet > 0 && (!t.site_xpos || !t.cur_air || !t.last_air || !t.cur_contact ||
+                      !t.last_contact || !t.last_time || !t.peak_heights))
+    return "feet declared but a foot buffer (site_xpos, air / contact times, peak heights) is null";
+  if (t.has_push && !t.push_time_left) return "has_push without push_time_left";
+  if (t.command_kind == MJX_CMD_TWIST && t.heading_command &&
+      (!t.heading_target || !t.heading_error || !t.is_heading_env))
+    return "heading_command without its heading buffers";
+  // entity indexing
+  if (!in(t.root_body, t.nbody)) return err("root_body %d outside [0, %d)", t.root_body, t.nbody);
+  if (t.orient_body >= t.nbody) return err("orient_body %d outside [-1, %d)", t.orient_body, t.nbody);
+  if (!span(t.free_q_adr, 7, t.nq)) return err("free joint qpos %d + 7 past nq %d", t.free_q_adr, t.nq);
+  if (!span(t.free_v_adr, 6, t.nv)) return err("free joint qvel %d + 6 past nv %d", t.free_v_adr, t.nv);
+  for (int j = 0; j < t.njoint; j++) {
+    if (!in(t.joint_q_adr[j], t.nq)) return err("joint %d qpos address outside [0, nq=%d)", j, t.nq);
+    if (!in(t.joint_v_adr[j], t.nv)) return err("joint %d qvel address outside [0, nv=%d)", j, t.nv);
+    if (!in(t.ctrl_of_action[j], t.nu)) return err("action %d ctrl index outside [0, nu=%d)", j, t.nu);
+    if (!in(t.target_of_action[j], t.njoint))
+      return err("action %d joint_pos_target column outside [0, njoint=%d)", j, t.njoint);
+  }
+  for (int s = 0; s < t.nfeet; s++) {
+    if (!in(t.foot_site[s], t.nsite)) return err("foot %d site outside [0, nsite=%d)", s, t.nsite);
+    if (!in(t.foot_site_body[s], t.nbody)) return err("foot %d body outside [0, nbody=%d)", s, t.nbody);
+    if (!in(t.feet_found_adr[s], t.nsensordata))
+      return err("foot %d found sensor outside [0, nsensordata=%d)", s, t.nsensordata);
+    if (!span(t.feet_force_adr[s], 3, t.nsensordata))
+      return err("foot %d force sensor + 3 past nsensordata %d", s, t.nsensordata);
+  }
+  for (int k = 0; k < t.nillegal; k++)
+    if (!in(t.illegal_found_adr[k], t.nsensordata))
+      return err("illegal-contact slot %d outside [0, nsensordata=%d)", k, t.nsensordata);
+  if (!span(t.imu_lin_vel_adr, 3, t.nsensordata) || !span(t.imu_ang_vel_adr, 3, t.nsensordata))
+    return err("imu velocity sensors (%d, %d) + 3 past nsensordata", t.imu_lin_vel_adr, t.imu_ang_vel_adr);
+  if (t.angmom_adr >= 0 && !span(t.angmom_adr, 3, t.nsensordata))
+    return err("angular-momentum sensor %d + 3 past nsensordata %d", t.angmom_adr, t.nsensordata);
+  if (t.selfcol_found_adr >= t.nsensordata)
+    return err("self-collision sensor %d outside [-1, %d)", t.selfcol_found_adr, t.nsensordata);
+  if (t.max_episode_length <= 0 || !(t.step_dt > 0.f)) return "non-positive episode length or step_dt";
+  // terms: kinds, and what each reads
+  for (int k = 0; k < t.nreward; k++) {
+    const int kind = t.reward_kind[k];
+    if (!in(kind, MJX_RW_IS_ALIVE + 1)) return err("reward %d: unknown kind %d", k, kind);
+    switch (kind) {
+      case MJX_RW_TRACK_LIN: case MJX_RW_TRACK_ANG: case MJX_RW_POSE: case MJX_RW_FEET_AIR_TIME:
+      case MJX_RW_FEET_CLEARANCE: case MJX_RW_FEET_SWING: case MJX_RW_FEET_SLIP:
+      case MJX_RW_SOFT_LANDING:  // read (or gate on) the twist command [nworld, 3]
+        if (t.command_kind != MJX_CMD_TWIST)
+          return err("reward %d: kind %d reads the twist command, command_kind is not MJX_CMD_TWIST", k, kind);
+        break;
+      case MJX_RW_ANGMOM:
+        if (t.angmom_adr < 0) return err("reward %d: kind %d needs angmom_adr", k, kind);
+        break;
+      case MJX_RW_SELF_COLLISION:
+        if (t.selfcol_found_adr < 0) return err("reward %d: kind %d needs selfcol_found_adr", k, kind);
+        break;
+      case MJX_RW_JUMP_HEIGHT:
+        if (!t.jump_peak || !t.jump_initial || !t.jump_initialized)
+          return err("reward %d: kind %d needs the jump_height state buffers", k, kind);
+        break;
+      case MJX_RW_LANDING_BALANCE:
+        if (!t.landing_timer || !t.was_in_air)
+          return err("reward %d: kind %d needs landing_timer / was_in_air", k, kind);
+        break;
+      default: break;
+    }
+    if ((kind == MJX_RW_EXPLOSIVE_TAKEOFF || kind == MJX_RW_JOINT_TORQUES || kind == MJX_RW_ACTION_ACC ||
+         kind == MJX_RW_SYNC_EXTENSION) && !t.actuator_force)
+      return err("reward %d: kind %d reads actuator_force, which is null", k, kind);
+  }
+  if (t.actuator_force)
+    for (int j = 0; j < t.njoint; j++)
+      if (!in(t.act_ctrl[j], t.nu)) return err("actuator %d ctrl index outside [0, nu=%d)", j, t.nu);
+  for (int k = 0; k < t.ntermination; k++) {
+    const int kind = t.termination_kind[k];
+    if (!in(kind, MJX_TM_EXCESSIVE_FORCE + 1)) return err("termination %d: unknown kind %d", k, kind);
+    if (kind == MJX_TM_ILLEGAL_CONTACT && t.nillegal == 0)
+      return err("termination %d: illegal_contact with no contact slots (%d)", k, t.nillegal);
+  }
+  // observation layouts (k_observe_obs writes exactly these widths)
+  const int nj = t.njoint, nf = t.nfeet;
+  if (t.command_kind == MJX_CMD_JUMP) {
+    if (t.npolicy != 9 + 3 * nj + 3 + 2 * nf || t.ncritic != t.npolicy + 4 * nf)
+      return err("observation widths (%d, %d) do not match the jump task layout", t.npolicy, t.ncritic);
+  } else {
+    const int nput = 9 + 3 * nj + 3;
+    if (t.npolicy != nput || t.ncritic != nput + (t.critic_extras ? 6 * nf : 0))
+      return err("observation widths (%d, %d) do not match the velocity task layout", t.npolicy, t.ncritic);
+    if (t.critic_extras && nf == 0) return "critic_extras with no feet";
+  }
+  return "";
+}
+
+extern "C" {
+
 int mjx_task_create(const mjxTaskDesc* desc, mjxTask** out) {
   if (!desc || !out) return task_fail("null argument");
   if (desc->njoint > MJX_TASK_MAX_JOINTS || desc->nfeet > MJX_TASK_MAX_FEET ||
       desc->nreward > MJX_TASK_MAX_TERMS || desc->ntermination > MJX_TASK_MAX_TERMS ||
       desc->nillegal > MJX_TASK_MAX_CONTACT_SLOTS)
     return task_fail("task descriptor exceeds compiled capacities");
+  {
+    const std::string why = validate_task(*desc);
+    if (!why.empty()) return task_fail("mjx_task_create: " + why);
+  }
   auto* t = new mjxTask_();
   t->host = *desc;
   t->nworld = desc->nworld;

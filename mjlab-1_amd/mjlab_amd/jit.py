@@ -12,8 +12,9 @@ library, caches it by a hash of the entry and of the kernel sources, and
 dimensions runs the specialised kernels.
 
 Cache: MJX355_JIT_DIR, default `mjlab_amd/jit_cache/` in the tree (so a library built here
-travels with the repository).  A compile takes a few minutes (the whole step pipeline for
-one model and capacity); a cache hit costs a dlopen.
+travels with the repository), or ~/.cache/mjlab_amd/jit_cache when that is read-only.  A
+compile takes about 40 s (the whole step pipeline for one model and capacity; measured on
+the edited G1 scene); a cache hit costs a dlopen.
 """
 
 from __future__ import annotations
@@ -126,26 +127,83 @@ def library_path(model, nconmax: int, njmax: int, role: int) -> tuple[str, str, 
   return os.path.join(CACHE, f"spec_{key}.so"), text, sid
 
 
-def ensure_library(model, nconmax: int, njmax: int, role: int, compile_ok: bool = True) -> str | None:
+def _user_cache() -> str:
+  base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+  return os.path.join(base, "mjlab_amd", "jit_cache")
+
+
+def _writable_cache() -> str:
+  """The in-tree cache when it can be written, else a per-user cache dir."""
+  for d in (CACHE, _user_cache()):
+    try:
+      os.makedirs(d, exist_ok=True)
+      if os.access(d, os.W_OK):
+        return d
+    except OSError:
+      continue
+  raise OSError(f"mjlab_amd.jit: no writable kernel cache ({CACHE}, {_user_cache()})")
+
+
+def _lookup(path: str) -> str | None:
+  """`path` (in CACHE) or the same file name in the user cache, if either exists."""
+  for p in (path, os.path.join(_user_cache(), os.path.basename(path))):
+    if os.path.exists(p):
+      return p
+  return None
+
+
+def _local_rank() -> int:
+  return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def ensure_library(model, nconmax: int, njmax: int, role: int, compile_ok: bool = True,
+                   wait_s: float = 900.0) -> str | None:
   """The cached library for this model and capacity, compiled first if `compile_ok` (None when
-  it is absent and may not be built, or hipcc is missing)."""
+  it is absent and may not be built, or hipcc is missing).
+
+  One process per GPU builds each key once: the compile runs under an exclusive lock file
+  next to the library, so ranks that ask for the same key at once wait for the first one's
+  result instead of compiling it again (and a rank that is not local rank 0 only waits, up to
+  `wait_s`).  The library goes to the in-tree cache, or to ~/.cache/mjlab_amd/jit_cache when
+  the package directory is read-only.  Raises RuntimeError when hipcc fails, OSError when no
+  cache directory can be written."""
   path, text, sid = library_path(model, nconmax, njmax, role)
-  if os.path.exists(path):
-    return path
+  hit = _lookup(path)
+  if hit is not None:
+    return hit
   if not compile_ok or not os.path.exists(HIPCC):
     return None
-  os.makedirs(CACHE, exist_ok=True)
-  with tempfile.TemporaryDirectory(dir=CACHE) as tmp:
-    inc = os.path.join(tmp, "jit_specs.inc")
-    with open(inc, "w") as fh:
-      fh.write(text)
-    out = os.path.join(tmp, "lib.so")
-    cmd = [HIPCC, *FLAGS, f"-I{CSRC}", f'-DMJX_SPECS_FILE="{inc}"', f"-DMJX_JIT_ID={sid}",
-           os.path.join(CSRC, "jit.hip"), "-o", out]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-      raise RuntimeError(f"mjlab_amd.jit: hipcc failed for {path}:\n{r.stderr[-4000:]}")
-    os.replace(out, path)  # atomic: a concurrent reader sees the whole library or none
+  import fcntl
+  import time
+  cache = _writable_cache()
+  path = os.path.join(cache, os.path.basename(path))
+  with open(path + ".lock", "w") as lock:
+    if _local_rank() != 0:
+      # another local rank compiles; poll its lock so a crash there does not hang this one
+      t0 = time.monotonic()
+      while True:
+        try:
+          fcntl.flock(lock, fcntl.LOCK_EX | fcntl.LOCK_NB)
+          break
+        except BlockingIOError:
+          if time.monotonic() - t0 > wait_s:
+            raise RuntimeError(f"mjlab_amd.jit: timed out waiting for {path}")
+          time.sleep(1.0)
+    else:
+      fcntl.flock(lock, fcntl.LOCK_EX)
+    if os.path.exists(path):  # built while this process waited
+      return path
+    with tempfile.TemporaryDirectory(dir=cache) as tmp:
+      inc = os.path.join(tmp, "jit_specs.inc")
+      with open(inc, "w") as fh:
+        fh.write(text)
+      out = os.path.join(tmp, "lib.so")
+      cmd = [HIPCC, *FLAGS, f"-I{CSRC}", f'-DMJX_SPECS_FILE="{inc}"', f"-DMJX_JIT_ID={sid}",
+             os.path.join(CSRC, "jit.hip"), "-o", out]
+      r = subprocess.run(cmd, capture_output=True, text=True)
+      if r.returncode != 0:
+        raise RuntimeError(f"mjlab_amd.jit: hipcc failed for {path}:\n{r.stderr[-4000:]}")
+      os.replace(out, path)  # atomic: a concurrent reader sees the whole library or none
   return path
 
 

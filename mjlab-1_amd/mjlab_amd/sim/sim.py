@@ -176,7 +176,12 @@ class SimulationCfg:
   at 64, `max_capacity`)."""
   njmax: int | None = None
   """Constraint rows per world: the max capacity a world is re-solved at."""
-  ls_parallel: bool = True  # accepted for API compatibility; the line search is exact
+  ls_parallel: bool = True
+  """Accepted so the reference's configs load (`sim/sim.py:94`, default True there), and
+  documented as not honoured: mujoco_warp's parallel line search evaluates a fixed set of step
+  sizes and keeps the best, while this engine always runs MuJoCo-C's exact (Newton-bracketed)
+  line search, which the north star's MuJoCo-C parity targets (DESIGN.md section 4).  Both
+  values give the same step here; `Simulation.line_search` reports "exact"."""
   contact_sensor_maxmatch: int = 64
   """Contact-sensor matches recorded per sensor and world (`sim/sim.py:95,141`): a sensor
   reduces over its first contact_sensor_maxmatch matching contacts in contact order (the
@@ -297,6 +302,7 @@ class Simulation:
     self.cfg = cfg
     self.device = device
     self.num_envs = int(num_envs)
+    self.line_search = "exact"  # whatever cfg.ls_parallel says (see SimulationCfg.ls_parallel)
     self._default_model_fields: dict[str, torch.Tensor] = {}
     dev = torch.device(device)
     if dev.type != "cuda":
@@ -471,10 +477,14 @@ class Simulation:
 
   @property
   def engine_counters(self) -> torch.Tensor:
-    """[nworld, 8] int32 device view: [0] contacts, [1] constraint rows, [2] contact
+    """[nworld, 6] int32 device view: [0] contacts, [1] constraint rows, [2] contact
     overflow, [3] row overflow, [4] unsupported-pair events (cumulative), [5] Newton
-    iterations.  No host sync (stats() is the synchronising summary)."""
-    return self.field("engine_counters")
+    iterations.  No host sync (stats() is the synchronising summary).  The engine's columns
+    [6] (contact output slots the last output touched) and [7] (contacts it held) are its
+    private output bookkeeping and are left out of the view, so zeroing the counters to reset
+    statistics cannot leave stale contact entries past ncon (reset() clears both with the
+    contact slots)."""
+    return self.field("engine_counters")[:, :6]
 
   def overflow_events(self) -> torch.Tensor:
     """Device [3] int32 view: total contact-overflow, row-overflow and unsupported-pair
@@ -545,7 +555,18 @@ class Simulation:
     compile_ok = policy == "always" or self.num_envs >= JIT_MIN_WORLDS
     loaded = False
     for ncon, rows, role in want:
-      path = jit.ensure_library(model, ncon, rows, role, compile_ok=compile_ok)
+      try:
+        path = jit.ensure_library(model, ncon, rows, role, compile_ok=compile_ok)
+      except (RuntimeError, OSError) as e:
+        # "always" asked for the specialisation: its failure is the caller's error.  "auto"
+        # only wanted speed: the generic kernels compute the same step (GenericKernelWarning
+        # fires below), so a failed compile or an unwritable cache does not abort the sim.
+        if policy == "always":
+          raise
+        import warnings
+        warnings.warn(f"mjlab_amd.Simulation: run-time specialisation unavailable ({e}); "
+                      "using the generic kernels", GenericKernelWarning, stacklevel=3)
+        continue
       if path is not None:
         jit.register(path)
         loaded = True
