@@ -141,6 +141,7 @@ static mjx::Params host_params(const mjxSim_* s) {
   p.m = s->dm;
   p.D = s->dd;
   for (int i = 0; i < 3 + mjx::kRowClasses; i++) p.LP[i] = s->lds_ph[i];
+  p.LPJ = mjx::make_lds(s->d, 1, true);
   p.nrowclass = s->nrowclass;
   for (int k = 0; k < mjx::kRowClasses; k++) p.row_cap[k] = s->row_cap[k];
   p.gscr = s->gscr;
@@ -182,6 +183,7 @@ static mjx::Params host_params_big(const mjxSim_* s) {
   p.d = s->dbig;
   for (int i = 0; i < 3; i++) p.LP[i] = s->lds_big[i];
   for (int k = 0; k < mjx::kRowClasses; k++) p.LP[3 + k] = s->lds_big[1];
+  p.LPJ = mjx::make_lds(s->dbig, 1, true);
   p.nrowclass = 0;
   p.gscr = s->gscr_big;
   p.gC = s->gC_big;
@@ -716,6 +718,11 @@ int mjx_sim_create_ex(const mjxModel* model, int nworld, int nconmax, int njmax,
   MJX_DATA_INT_FIELDS(X_INT)
 #undef X_FLT
 #undef X_INT
+  // an unused contact slot holds geoms (-1, -1), as the outputs leave every slot past ncon
+  // (a slot never written must read the same as one cleared: fused and single steps write
+  // outputs on different substeps)
+  e = hipMemset(s->dd.contact_geom, 0xff, sizeof(int32_t) * (size_t)nworld * d.nconmax * 2);
+  if (e != hipSuccess) { delete s; return fail(std::string("hipMemset: ") + hipGetErrorString(e)); }
   s->dd.stats = (int32_t*)(base + offs[k++].second);
   s->dd.wstats = (int32_t*)(base + offs[k++].second);
   // per-world engine counters [nworld, 8] (phase C, last substep): [0] contacts found,
@@ -956,6 +963,17 @@ int mjx_spec_register(const char* path) {
   auto kern = reinterpret_cast<KernFn>(dlsym(h, "mjx_jit_kernel"));
   if (!abi || !dims || !tree || !kern) return fail(std::string(path) + ": not a jit.hip library");
   if (abi() != (int)sizeof(mjx::Dims)) return fail(std::string(path) + ": Dims layout mismatch (stale build)");
+  // the kernels read Params / Lds / DData through this library's layout: the JIT library must
+  // come from the same kernel headers (csrc/Makefile MJX_HDR_HASH), else a stale cache entry or
+  // a header edited after the last engine build would fault the device instead of failing here
+  using HdrFn = unsigned long long (*)(void);
+  auto hdr = reinterpret_cast<HdrFn>(dlsym(h, "mjx_jit_hdr"));
+#ifdef MJX_HDR_HASH
+  if (!hdr || hdr() != (unsigned long long)MJX_HDR_HASH)
+    return fail(std::string(path) + ": built from other kernel headers than libmjx355.so (rebuild one of them)");
+#else
+  if (!hdr) return fail(std::string(path) + ": not a jit.hip library of this engine");
+#endif
   mjx::Dims d{};
   dims(&d);
   int par[64];

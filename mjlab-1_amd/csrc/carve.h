@@ -39,7 +39,10 @@ constexpr int ltr_size(int nvp) { return 8 * (nvp >> 2) * ((nvp >> 2) + 1); }
 // so only the live rows are copied; M's slot holds M in LTR form, the rest of the slot is
 // neither written nor read), C pack = [A outputs | B outputs].  Each phase then fills its
 // inputs with one or two bulk copies.
-constexpr Lds make_lds(const Dims& d, int ph) {
+// jglobal (phase B only): the Newton reads the constraint Jacobian straight from the B pack in
+// global memory (L2) instead of an LDS copy -- the carve of the latency Newton kernel's heavy
+// worlds, whose J (up to njmax x nvp floats) is most of the full-capacity carve
+constexpr Lds make_lds(const Dims& d, int ph, bool jglobal = false) {
   Lds L{};
   const int nb = d.nbody, nv = (d.nv + 3) & ~3, C = d.nconmax, R = d.njmax;  // nv padded
   constexpr int A = 1, B = 2, Cp = 4;
@@ -79,7 +82,7 @@ constexpr Lds make_lds(const Dims& d, int ph) {
     {&Lds::con_n, 3 * C, A | Cp},  // unit normals: cframe() rebuilds the frame where used
     {&Lds::con_mu, 2 * C, A | Cp}, {&Lds::con_kb, 2 * C, A}, {&Lds::con_imp, C, A},
     {&Lds::con_imargin, C, A}, {&Lds::con_dim, C, A | Cp}, {&Lds::con_efc, C, A | Cp},
-    {&Lds::efc_J, R * nv, B},  // phase A writes J rows straight into the B pack
+    {&Lds::efc_J, ph == 1 && jglobal ? 0 : R * nv, B},  // phase A writes J rows straight into the B pack
     {&Lds::efc_aref, R, A | B}, {&Lds::efc_D, R, A | B}, {&Lds::efc_jar, R, B},
     {&Lds::efc_Js, R, B}, {&Lds::efc_force, R, B | Cp}, {&Lds::efc_cid, R > nb ? R : nb, A},
     {&Lds::efc_act, R, B}, {&Lds::hdiag, nv, 0},

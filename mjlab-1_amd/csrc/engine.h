@@ -166,6 +166,7 @@ struct Params {
   // class k.  Worlds whose nefc fits class k's capacity run Newton in its smaller carve (more
   // resident worlds per CU); classes run concurrently (launch_step).
   Lds LP[3 + kRowClasses];
+  Lds LPJ;  // phase B at full capacity with J read from the B pack in global memory (kLdsJG)
   int nrowclass;                 // row classes in use (0 = every world in LP[1])
   int row_cap[kRowClasses];      // ascending row capacities of the classes
   // Newton work lists (classify_kernel, every substep between phases A and B): worlds sorted

@@ -46,6 +46,7 @@ __global__ void reset_kernel(Dims d, DModel m, DData D, const uint8_t* mask, int
     D.contact_geom[(wc + c) * 2 + 1] = -1;
     for (int t = 0; t < 3; t++) D.contact_pos[(wc + c) * 3 + t] = 0.f;
     for (int t = 0; t < 9; t++) D.contact_frame[(wc + c) * 9 + t] = 0.f;
+    for (int t = 0; t < 3; t++) D.contact_force[(wc + c) * 3 + t] = 0.f;
   }
   __syncthreads();
   if (lane == 0) { D.time[w] = 0; D.ncon[w] = 0; D.nefc[w] = 0; wsv[6] = 0; wsv[7] = 0; }
@@ -192,6 +193,16 @@ static bool newton_lat() {
   }();
   return on;
 }
+// The full-capacity row class (the heavy worlds of the fast carve) reads the constraint
+// Jacobian from the B pack in global memory (phase code 9, carve kLdsJG) instead of an LDS
+// copy.  MJX355_NEWTON_JG=0/1 (A/B).
+static bool newton_jg() {
+  static const bool on = [] {
+    const char* e = getenv("MJX355_NEWTON_JG");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
 
 int find_spec(const Dims& d, const int* dof_parentid) {
   if (const char* e = getenv("MJX355_NO_SPEC"))  // diagnostic: force the generic kernels
@@ -235,7 +246,8 @@ static size_t lds_bytes(const Params& host, int ph) {
     return e ? atol(e) : 0L;
   }();
   const long p = pad_all + pad[ph >= 3 ? 1 : ph];
-  return (size_t)host.LP[ph].total * 4 + (size_t)(p > 0 ? p : 0);
+  const Lds& L = ph == kLdsJG ? host.LPJ : host.LP[ph];
+  return (size_t)L.total * 4 + (size_t)(p > 0 ? p : 0);
 }
 
 // dynamic LDS of step_resolve: the largest of the three phase carves
@@ -592,8 +604,10 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
                                selx, last, integrate, mask);
             return;
           }
-          hipLaunchKernelGGL(cls ? fB : fBL, dim3(n), dim3(kWave), lds_bytes(host, cls ? 2 + cls : 1),
-                             cs, dev, w0, w1, k, last, cls, mask);
+          const StepFn fJ = cls == 0 && newton_lat() && newton_jg() ? step_fn(host, 9) : nullptr;
+          hipLaunchKernelGGL(cls ? fB : fJ ? fJ : fBL, dim3(n), dim3(kWave),
+                             lds_bytes(host, cls ? 2 + cls : fJ ? kLdsJG : 1), cs, dev, w0, w1, k, last,
+                             cls, mask);
           if (!piped) return;
           hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
                              k | (cls + 1) << 8, last, integrate, mask);

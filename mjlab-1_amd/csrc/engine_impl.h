@@ -1285,9 +1285,11 @@ template <int SP> constexpr bool kBoxBox = SP == 0 || ModelSpec<SP>::dims().nbox
 // 64 contacts (sim.max_capacity: the reference's njmax bounds a world's contacts too) takes
 // the multi-round forms (rank sort, contacts lane + 64 r)
 template <int SP> constexpr bool kCon1 = SP != 0 && ModelSpec<SP>::dims().nconmax <= kWave;
+// carve index kLdsJG: phase B at full capacity with J in global memory (make_lds jglobal)
+constexpr int kLdsJG = 9;
 template <int SP, int K> struct SpecLds {
   static constexpr Lds get() {
-    constexpr Lds v = make_lds(ModelSpec<SP>::dims(), K);
+    constexpr Lds v = make_lds(ModelSpec<SP>::dims(), K == kLdsJG ? 1 : K, K == kLdsJG);
     return v;
   }
 };
@@ -1301,6 +1303,7 @@ __device__ __forceinline__ decltype(auto) dims_of(const Params* P) {
 template <int SP, int K>
 __device__ __forceinline__ decltype(auto) lds_of(const Params* P) {
   if constexpr (SP > 0) return SpecLds<SP, K>::get();
+  else if constexpr (K == kLdsJG) return static_cast<const Lds&>(P->LPJ);
   else return static_cast<const Lds&>(P->LP[K]);
 }
 
@@ -1721,7 +1724,9 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 #define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(PH == 1 && NR <= 48 ? 3 : 1)))
 // LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
 // more registers in flight, for the launch that holds the heavy worlds.
-template <int NR, int PH, int SP, bool LAT>
+// LAT: 0 the throughput form, 1 the latency form, 2 the latency form reading the constraint
+// Jacobian from the B pack in global memory (phase B only; carve kLdsJG)
+template <int NR, int PH, int SP, int LAT>
 __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* __restrict__ P, int w0,
                                           int w1, int sel, int last, int integrate,
                                           const uint8_t* __restrict__ mask, const int bid) {
@@ -1730,7 +1735,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   const DModel& m = P->m;
   const DData& D = P->D;
   // phase B: `integrate` carries the Newton row class (0 = full capacity, k > 0 = LP[2 + k])
-  const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate] : lds_of<SP, PH>(P);
+  constexpr bool JG = PH == 1 && LAT == 2;
+  const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate]
+                                            : lds_of<SP, JG ? kLdsJG : PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
   int w = w0 + bid;
@@ -3199,7 +3206,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       // B pack: carve offsets == pack offsets; M's slot holds M in LTR form (the rest of the
       // slot is neither written nor read)
       cp_pack(S, gw, L.M + ltr_size(nvp), lane);
-      if (cls <= 0) {
+      if (JG) {
+        // the pack up to J (its offsets equal this carve's); J stays in global memory
+        cp_pack(S + L.qacc_smooth, gw + LB.qacc_smooth, LB.efc_J - LB.qacc_smooth, lane);
+      } else if (cls <= 0) {
         cp_pack(S + L.qacc_smooth, gw + L.qacc_smooth, L.efc_J + nefc_in * nvp - L.qacc_smooth, lane);
       } else {
         // the pack is laid out with the full-capacity carve LB: [ints M qacc_smooth
@@ -3241,7 +3251,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
       float* Js = S + L.efc_Js;
       float* wv = S + L.efc_force;
       const float* Dv = S + L.efc_D;
-      const float* J = S + L.efc_J;
+      // (JG: the B pack's rows in global memory, written by this world's phase A in an earlier
+      // launch -- a kernel boundary, so no stale vector-L1 line)
+      const float* J = JG ? gw + LB.efc_J : S + L.efc_J;
       int* act = Si + L.efc_act;
       float* Lm = S + L.H;
       const float scale = 1.0f / (o.meaninertia * (float)max(nv, 1));
@@ -3390,14 +3402,14 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           if (refactor) {
 #if MJX_JTDJ_MFMA
             rows_load<NR>(R, Lm, nvp, lane);
-            rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);
+            rows_chol<NR, (LAT != 0)>(R, rd, S + LB.chol, nvp, lane);
             rows_store_strict<NR>(R, rd, Lm, nvp, lane);
 #else
             rows_load_ltr<NR>(R, Lm, nvp, lane);  // the reversed matrix's rows when tree_h
             if (tree_h) {
               if constexpr (kTree<SP>) rows_chol_tree<NR, SP>(R, rd, S + LB.chol, lane);
             } else {
-              rows_chol<NR, LAT>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
+              rows_chol<NR, (LAT != 0)>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
             }
             rows_store_strict_ltr<NR>(R, rd, Lm, nvp, lane);
 #endif
@@ -3880,12 +3892,15 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
 // one wave per SIMD at most, so its span is one world's latency, not throughput: the kernel
 // may take 256 VGPRs (2 waves / SIMD, still above its LDS-bound residency) and spends them
 // on loads issued ahead of their use (rows_chol<NR, true>).
-template <int NR, int SP>
+// JGL = 2: the constraint Jacobian read from the B pack in global memory (carve kLdsJG): the
+// heavy worlds' full-capacity carve shrinks by njmax x nvp floats, so they hold a fraction of
+// the LDS the concurrent bulk class needs, and more of them fit a CU where they are many.
+template <int NR, int SP, int JGL = 1>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_newton_lat(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
-  step_body<NR, 1, SP, true>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
+  step_body<NR, 1, SP, JGL>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
 }
 
 // The overflow re-solve launches (sel & kSelOvf; ovf_chain): a fixed grid of kOvfGrid
@@ -3906,7 +3921,7 @@ __device__ __forceinline__ void ovf_clear_on_exit(const Params* __restrict__ P, 
   }
 }
 
-template <int NR, int PH, int SP, bool LAT>
+template <int NR, int PH, int SP, int LAT>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_ovf(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
@@ -3957,7 +3972,7 @@ __device__ __forceinline__ void chain_handoff() {
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-template <int NR, int SP, bool LAT>
+template <int NR, int SP, int LAT>
 __global__ __launch_bounds__(kWave)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : (NR <= 48 ? 3 : 1), LAT ? 2 : 8))) void step_chain(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
@@ -3968,10 +3983,10 @@ __attribute__((amdgpu_waves_per_eu(LAT ? 1 : (NR <= 48 ? 3 : 1), LAT ? 2 : 8))) 
   const int cls1 = (sel >> 8) & 0xff;  // class + 1
   step_body<NR, 1, SP, LAT>(S, P, w0, w1, split, last, cls1 - 1, mask, bid);
   chain_handoff();
-  step_body<NR, 2, SP, false>(S, P, w0, w1, split | cls1 << 8, last, integrate, mask, bid);
+  step_body<NR, 2, SP, 0>(S, P, w0, w1, split | cls1 << 8, last, integrate, mask, bid);
   if (sel & kSelChainA) {
     chain_handoff();
-    step_body<NR, 0, SP, false>(S, P, w0, w1, split | cls1 << 8 | (sel & kSelAPar) | kSelFusedA,
+    step_body<NR, 0, SP, 0>(S, P, w0, w1, split | cls1 << 8 | (sel & kSelAPar) | kSelFusedA,
                                 (sel & kSelNextLast) ? 1 : 0, integrate, mask, bid);
   }
 }
@@ -4025,6 +4040,9 @@ StepFn phase_kernel(int ph) {
       else return nullptr;
     case 8:
       if constexpr ((role & 2) != 0) return step_masked<NR, SP>;
+      else return nullptr;
+    case 9:
+      if constexpr ((role & 1) != 0) return step_newton_lat<NR, SP, 2>;
       else return nullptr;
     default:
       return nullptr;

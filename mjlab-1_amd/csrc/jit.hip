@@ -15,7 +15,14 @@ namespace mjx {
 static_assert(ModelSpec<MJX_JIT_ID>::on, "the generated specs file lacks the entry");
 }  // namespace mjx
 
+#ifndef MJX_HDR_HASH
+#error "MJX_HDR_HASH must be the kernel-header hash (mjlab_amd/jit.py, csrc/Makefile)"
+#endif
 extern "C" __attribute__((visibility("default"))) int mjx_jit_abi(void) { return (int)sizeof(mjx::Dims); }
+// the kernel headers this library was compiled from (must equal libmjx355's own)
+extern "C" __attribute__((visibility("default"))) unsigned long long mjx_jit_hdr(void) {
+  return MJX_HDR_HASH;
+}
 extern "C" __attribute__((visibility("default"))) void mjx_jit_dims(mjx::Dims* out) {
   *out = mjx::ModelSpec<MJX_JIT_ID>::dims();
 }

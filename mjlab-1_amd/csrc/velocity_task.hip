@@ -985,13 +985,15 @@ static std::string validate_task(const mjxTaskDesc& t) {
                         t.command_counter, t.metric_err_xy, t.metric_err_yaw, t.episode_sums,
                         t.step_reward, t.reward_buf, t.reset_buf, t.terminated, t.time_outs,
                         t.term_dones, t.obs_policy, t.obs_critic, t.log_reward, t.log_termination,
-                        t.log_command, t.log_metric, t.step_counter, t.is_standing_env};
+                        t.log_command, t.log_metric, t.step_counter};
   for (size_t i = 0; i < sizeof need / sizeof need[0]; i++)
     if (!need[i]) return err("required buffer %d of the descriptor is null", (int)i, 0);
   if (t.nfeet > 0 && (!t.site_xpos || !t.cur_air || !t.last_air || !t.cur_contact ||
                       !t.last_contact || !t.last_time || !t.peak_heights))
     return "feet declared but a foot buffer (site_xpos, air / contact times, peak heights) is null";
   if (t.has_push && !t.push_time_left) return "has_push without push_time_left";
+  if (t.command_kind == MJX_CMD_TWIST && !t.is_standing_env)
+    return "twist command without is_standing_env";
   if (t.command_kind == MJX_CMD_TWIST && t.heading_command &&
       (!t.heading_target || !t.heading_error || !t.is_heading_env))
     return "heading_command without its heading buffers";
@@ -1030,9 +1032,9 @@ static std::string validate_task(const mjxTaskDesc& t) {
     const int kind = t.reward_kind[k];
     if (!in(kind, MJX_RW_IS_ALIVE + 1)) return err("reward %d: unknown kind %d", k, kind);
     switch (kind) {
-      case MJX_RW_TRACK_LIN: case MJX_RW_TRACK_ANG: case MJX_RW_POSE: case MJX_RW_FEET_AIR_TIME:
-      case MJX_RW_FEET_CLEARANCE: case MJX_RW_FEET_SWING: case MJX_RW_FEET_SLIP:
-      case MJX_RW_SOFT_LANDING:  // read (or gate on) the twist command [nworld, 3]
+      // read the twist command [nworld, 3] (the feet terms only gate on it, and command_gate
+      // passes them ungated under another command kind: the jump task's soft_landing)
+      case MJX_RW_TRACK_LIN: case MJX_RW_TRACK_ANG: case MJX_RW_POSE:
         if (t.command_kind != MJX_CMD_TWIST)
           return err("reward %d: kind %d reads the twist command, command_kind is not MJX_CMD_TWIST", k, kind);
         break;

@@ -104,6 +104,20 @@ def entry_lines(sid: int, name: str, dims: dict, par: tuple, role: int | None = 
   return out
 
 
+HEADERS = ("engine.h", "engine_impl.h", "carve.h", "fields.h")  # csrc/Makefile HDR_HASH
+
+
+def header_hash() -> str:
+  """The kernel-header hash csrc/Makefile compiles into libmjx355.so (MJX_HDR_HASH): sha1 of
+  the concatenated headers, 15 hex digits.  mjx_spec_register refuses a JIT library whose hash
+  differs from the engine's (a Params layout mismatch would fault the device)."""
+  h = hashlib.sha1()
+  for f in HEADERS:
+    with open(os.path.join(CSRC, f), "rb") as fh:
+      h.update(fh.read())
+  return h.hexdigest()[:15]
+
+
 def _source_hash() -> str:
   h = hashlib.sha1()
   for f in SOURCES:
@@ -199,11 +213,15 @@ def ensure_library(model, nconmax: int, njmax: int, role: int, compile_ok: bool 
         fh.write(text)
       out = os.path.join(tmp, "lib.so")
       cmd = [HIPCC, *FLAGS, f"-I{CSRC}", f'-DMJX_SPECS_FILE="{inc}"', f"-DMJX_JIT_ID={sid}",
-             os.path.join(CSRC, "jit.hip"), "-o", out]
+             f"-DMJX_HDR_HASH=0x{header_hash()}ULL", os.path.join(CSRC, "jit.hip"), "-o", out]
       r = subprocess.run(cmd, capture_output=True, text=True)
       if r.returncode != 0:
         raise RuntimeError(f"mjlab_amd.jit: hipcc failed for {path}:\n{r.stderr[-4000:]}")
       os.replace(out, path)  # atomic: a concurrent reader sees the whole library or none
+    try:  # a waiter holding the lock finds the library once it gets the lock
+      os.unlink(path + ".lock")
+    except OSError:
+      pass
   return path
 
 

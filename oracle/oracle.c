@@ -1887,4 +1887,40 @@ int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const do
   return ov;
 }
 
+/* fp32 evaluation scale of the Newton cost (orc_cost_scale) */
+int orc_cost_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                   const double* qvel, const double* qacc_warmstart, const double* ctrl, double time,
+                   double* out_scale) {
+  orcData* d = orc_data_new(m, nconmax, njmax);
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_warmstart, sizeof(double) * m->nv);
+  memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+  d->time = time;
+  orc_forward(m, d);
+  const int nv = m->nv;
+  const double* x = d->qacc;
+  double s = 0;
+  /* Gauss term 1/2 (x - a0)' (M x - f), eval_cost's form: each factor's terms in magnitude */
+  for (int i = 0; i < nv; i++) {
+    double mx = fabs(d->qfrc_smooth[i]);
+    for (int k = 0; k < nv; k++) mx += fabs(d->qM[i * nv + k] * x[k]);
+    s += 0.5 * (fabs(x[i]) + fabs(d->qacc_smooth[i])) * mx;
+  }
+  /* active rows: 1/2 D (J x - aref)^2 with J x - aref in term magnitudes */
+  for (int r = 0; r < d->nefc; r++) {
+    const double* J = d->efc_J + (size_t)r * nv;
+    double v = -d->efc_aref[r], va = fabs(d->efc_aref[r]);
+    for (int i = 0; i < nv; i++) {
+      v += J[i] * x[i];
+      va += fabs(J[i] * x[i]);
+    }
+    if (v < 0) s += 0.5 * d->efc_D[r] * va * va;
+  }
+  *out_scale = s;
+  int ov = d->overflow;
+  orc_data_free(d);
+  return ov;
+}
+
 size_t orc_model_desc_size(void) { return sizeof(mjxModelDesc); }

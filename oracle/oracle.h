@@ -124,6 +124,16 @@ int orc_qacc_error_scale(const mjxModelDesc* m, int nconmax, int njmax, const do
  * (an ankle roll) is a small difference of O(m d^2) terms. */
 int orc_mass_matrix_scale(const mjxModelDesc* m, const double* qpos, double* out_Mabs);
 
+/* fp32 evaluation scale of the Newton cost at the fp64 solution x (mj_forward first): the
+ * magnitude of the terms eval_cost sums, 1/2 sum_i (|x_i| + |qacc_smooth_i|)(sum_k |M_ik x_k| +
+ * |qfrc_smooth_i|) + sum_{active r} 1/2 D_r (sum_i |J_ri x_i| + |aref_r|)^2.  An fp32 solver
+ * cannot tell costs apart closer than eps times this, so a cost gap between the engine's and
+ * the oracle's qacc is judged in units of eps * out_scale -- not relative to the cost itself,
+ * which is ~0 in a contact-free world (x = qacc_smooth minimises the Gauss term exactly). */
+int orc_cost_scale(const mjxModelDesc* m, int nconmax, int njmax, const double* qpos,
+                   const double* qvel, const double* qacc_warmstart, const double* ctrl, double time,
+                   double* out_scale);
+
 #ifdef __cplusplus
 }
 #endif

@@ -137,6 +137,19 @@ def qacc_error_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256,
   return out, vout
 
 
+def cost_scale(model, qpos, qvel, qacc_warmstart, ctrl, time, nconmax=256, njmax=1024) -> float:
+  """fp32 evaluation scale of the Newton cost at the fp64 solution (orc_cost_scale): the
+  magnitude of the terms the cost sums; a cost gap is judged in units of eps32 times it."""
+  desc, keep = make_desc(model)
+  f64 = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), dtype=np.float64)
+  a = [f64(qpos, model.nq), f64(qvel, model.nv), f64(qacc_warmstart, model.nv), f64(ctrl, model.nu)]
+  out = ctypes.c_double()
+  lib().orc_cost_scale(ctypes.byref(desc), nconmax, njmax, *(_p(x) for x in a), ctypes.c_double(time),
+                       ctypes.byref(out))
+  del keep
+  return out.value
+
+
 def rollout(model, qpos, qvel, qacc_warmstart, ctrl, time, nstep, nconmax=256, njmax=1024,
             nthreads=0, outputs=True):
   """Batched independent worlds, `nstep` mj_steps each (state arrays updated in place)."""

@@ -67,3 +67,84 @@ def world_model(sim, w: int, fields=None):
     shape = np.asarray(base.arrays[f]).shape
     arrays[f] = getattr(sim.model, f)[w].double().cpu().numpy().reshape(shape)
   return dataclasses.replace(base, arrays=arrays)
+
+
+# mjData fields the caller writes (inputs of a step); every other data field the engine exposes
+# is an output (csrc/fields.h MJX_DATA_*_FIELDS)
+DATA_INPUTS = ("ctrl", "qfrc_applied", "xfrc_applied", "mocap_pos", "mocap_quat")
+DATA_FIELDS = ("qpos", "qvel", "qacc", "qacc_warmstart", "qacc_smooth", "time", "xpos", "xquat",
+               "xmat", "xipos", "ximat", "cvel", "cacc", "subtree_com", "subtree_linvel",
+               "subtree_angmom", "geom_xpos", "geom_xmat", "site_xpos", "site_xmat", "sensordata",
+               "actuator_force", "actuator_length", "actuator_velocity", "qfrc_actuator",
+               "qfrc_bias", "qfrc_passive", "qfrc_constraint", "qfrc_smooth", "contact_dist",
+               "contact_pos", "contact_frame", "contact_force", "ncon", "nefc", "solver_niter",
+               "contact_geom")
+
+
+def air_time_buffers(env) -> dict:
+  """The contact air-time tensors the engine updates every substep for a fused env
+  (mjx_sim_track_air_time), by name; {} when the env has none."""
+  fused = getattr(env, "_fused", None)
+  sensor = getattr(fused, "_feet_sensor", None) if fused is not None else None
+  air = getattr(sensor, "_air", None) if sensor is not None else None
+  if not air or not getattr(sensor, "engine_owned", False):
+    return {}
+  return {f"air_{k}": v for k, v in air.items() if isinstance(v, __import__("torch").Tensor)}
+
+
+def output_snapshot(sim, extra: dict | None = None) -> dict:
+  """Clones of every mjData output field of the sim (all of DATA_FIELDS), the engine's per-world
+  counters that describe the last substep (contacts, rows, Newton iterations) and the extra
+  tensors (e.g. air_time_buffers), for bit-for-bit comparisons of two step paths."""
+  d = sim.data
+  out = {k: getattr(d, k).clone() for k in DATA_FIELDS}
+  out["engine_counters[0,1,5]"] = sim.engine_counters[:, [0, 1, 5]].clone()
+  for k, v in (extra or {}).items():
+    out[k] = v.clone()
+  return out
+
+
+def restore_state(sim, state: dict, extra: dict | None = None) -> None:
+  for k, v in state.items():
+    if k in (extra or {}):
+      extra[k].copy_(v)
+    else:
+      getattr(sim.data, k).copy_(v)
+
+
+def differing_outputs(a: dict, b: dict) -> dict:
+  """{field: number of worlds whose entries differ} for the fields of two output snapshots that
+  are not bit-identical (NaN never appears in a finite step; compared as raw values)."""
+  bad = {}
+  for k, v in a.items():
+    w = b[k]
+    if v.shape != w.shape:
+      bad[k] = -1
+      continue
+    ne = v != w
+    if bool(ne.any()):
+      bad[k] = int(ne.reshape(ne.shape[0], -1).any(dim=1).sum()) if ne.dim() > 0 else 1
+  return bad
+
+
+def diff_detail(a: dict, b: dict, bad: dict, nmax: int = 3) -> str:
+  """A readable account of the first differing worlds of each field in `bad`: world, its
+  ncon / nefc in both snapshots, the first differing flat indices and their values."""
+  import torch
+  lines = []
+  for k in bad:
+    v, w = a[k], b[k]
+    if v.shape != w.shape:
+      lines.append(f"{k}: shapes {tuple(v.shape)} vs {tuple(w.shape)}")
+      continue
+    ne = (v != w).reshape(v.shape[0], -1)
+    worlds = ne.any(dim=1).nonzero().flatten().tolist()[:nmax]
+    for wd in worlds:
+      idx = ne[wd].nonzero().flatten().tolist()[:6]
+      va = v.reshape(v.shape[0], -1)[wd][idx].tolist()
+      vb = w.reshape(w.shape[0], -1)[wd][idx].tolist()
+      nc = (int(a["ncon"].reshape(-1)[wd]), int(b["ncon"].reshape(-1)[wd])) if "ncon" in a else None
+      ne_ = (int(a["nefc"].reshape(-1)[wd]), int(b["nefc"].reshape(-1)[wd])) if "nefc" in a else None
+      lines.append(f"{k} world {wd} ncon {nc} nefc {ne_}: idx {idx} {va} vs {vb}")
+  del torch
+  return "; ".join(lines)

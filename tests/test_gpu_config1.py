@@ -19,6 +19,7 @@ import pytest
 import torch
 
 import oracle_lib as ol
+from parity_util import diff_detail, differing_outputs, output_snapshot
 from parity_util import expanded_fields, world_model
 from test_gpu_rollout_parity import _OUT, _STATE, _check_step, _snap, write_stats
 
@@ -31,7 +32,7 @@ NSTEPS = 200
 def _stats():
   return dict(checked=0, ties=0, heavy_checked=0, max_nefc=0, qacc_ratio=0.0, qacc_abs=0.0,
               qacc_rel_world=0.0, qvel_ratio=0.0, sens_ratio=0.0, qacc_worst=[], niter_maxdiff=0,
-              capped=0, qpos_ratio=0.0, qacc_energy_rel=0.0, cost_gap_rel=-1.0,
+              capped=0, qpos_ratio=0.0, qacc_energy_rel=0.0, cost_gap_fp32=-1.0,
               qacc_fp32_ratio=0.0, qacc_fp32_ratio_p99=[], in_model=0, out_of_model=[],
               per_dof_within=0, e2e_qvel_abs=0.0, e2e_qpos_abs=0.0, niter_equal=0)
 
@@ -124,6 +125,7 @@ def test_config1_captured_every_substep(gpu_device):
     torch.cuda.synchronize()
     s1 = {n: getattr(d, n).clone() for n in keys}
     a1 = {n: t.clone() for n, t in air.items()}
+    o1 = output_snapshot(sim)
     reset = bool((env.episode_length_buf == 0).any())
     # re-run this env step's physics from the pre-step state as single steps (ctrl holds the
     # value the graph's action kernel wrote for all of its substeps)
@@ -153,6 +155,12 @@ def test_config1_captured_every_substep(gpu_device):
         assert torch.equal(d.qvel[:, 6:], s1["qvel"][:, 6:]), f"step {k}: joint qvel after a push"
       for n in ("current_air_time", "last_air_time", "current_contact_time", "last_contact_time"):
         assert torch.equal(air[n], a1[n]), f"step {k}: engine air time {n}"
+      # every other mjData output the graph's last substep wrote (frames, velocities,
+      # subtree quantities, sites, geoms, forces, contacts, sensors, counters): the
+      # post-physics managers write only qvel (a push), compared above
+      bad = differing_outputs(o1, output_snapshot(sim))
+      bad.pop("qvel", None)
+      assert not bad, f"step {k}: graph step outputs != single steps in {bad}: {diff_detail(o1, output_snapshot(sim), bad)}"
     # continue the graph's trajectory (post-physics events and resets included)
     for n in keys:
       getattr(d, n).copy_(s1[n])
