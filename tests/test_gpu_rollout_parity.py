@@ -88,22 +88,29 @@ QACC_FLOOR, QACC_EPS_MUL = 1e-4, 1024.0
 QVEL_FLOOR, QVEL_EPS_MUL = 1e-6, 24.0
 OUT_OF_MODEL_FRACTION = 0.0
 # the cost gap, in units of eps32 x the magnitude of the terms the cost sums (orc_cost_scale),
-# that still counts as the same fp32 minimiser; round-6 maximum over every config 0.035
-COST_GAP_EPS = 8.0
+# that still counts as the same fp32 minimiser -- the discriminator of a world-step outside the
+# fp32 qacc model (none is).  Measured (profiles/r06_rollout_parity.json): <= 0.035 on config 1,
+# G1, Go1 and jump hfield; 11.5 on one 118-row tracking world-step inside the qacc model (ratio
+# 0.23), where the gap is second order in the accepted qacc error, 1/2 dq' H dq with H carrying
+# stiff contact rows (D ~ 1e5).  The gate sits above that
+COST_GAP_EPS = 64.0
 QPOS_ABS = 1e-6
 QPOS_ULPS = 2.0 ** -21  # 4 fp32 ulps of the coordinate
 SENS_ABS, SENS_REL = 1e-2, 1e-3
 # The sensor check's kinematic term (check (4)): the fp32 forward kinematics as the exact
-# kinematics of a perturbed state.  KIN_DELTA is the measured per-coordinate perturbation, in
-# units of eps32 (|x_k| + 1) plus the output's own rounding, that explains the engine's body
-# frames / com velocities / subtree coms against the oracle's at the same state (check (5);
-# profiles/r06_rollout_parity.json, kin_eps_mul_max over every config); the test fails if a
-# world-step needs more.  The sensors are formed from those kinematics through about three
+# kinematics of a perturbed state.  KIN_DELTA is the per-coordinate perturbation, in units of
+# eps32 (|x_k| + 1) plus the output's own rounding, that explains the engine's body frames /
+# com velocities / subtree coms against the oracle's at the same state (check (5)).  Measured
+# over every GPU parity test (profiles/r06_rollout_parity.json, kin_eps_mul_max: 1.015, the
+# overflow re-solve test; 0.79 config 1, 0.92 G1, 0.92 Go1, 0.91 tracking, 1.01 jump hfield;
+# 288 decomposed world-steps); KIN_DELTA takes that with 23 % headroom, and a world-step that
+# needs more fails the test.  The sensors are formed from those kinematics through about three
 # further fp32 stages (contact geometry and parameters, the constraint forces D (J a - aref),
 # their per-sensor reduction), each adding rounding of its own terms, so their term allows
-# KIN_HEADROOM = 2^3 times that perturbation.
-KIN_DELTA = 8.0  # provisional (measurement run)
-KIN_HEADROOM = 1.0
+# KIN_HEADROOM = 2^3 times that perturbation (the largest sensor error against this full bound:
+# 0.50 of it at 8 eps, G1 4,096).
+KIN_DELTA = 1.25
+KIN_HEADROOM = 8.0
 KIN_EPS_MUL = KIN_HEADROOM * KIN_DELTA
 QM_EPS_MUL = 4.0  # the engine's M: within 4 eps x the magnitude of the terms it sums
 QFRC_ABS, QFRC_REL = 4e-5, 4e-6
