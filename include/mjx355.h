@@ -205,7 +205,9 @@ int mjx_sim_spec(const mjxSim* sim);
  * compiled csrc/specs.inc entry, and caches it).  Returns the specialisation id (>= 1000; a sim
  * created afterwards with those dims runs its kernels, mjx_sim_spec) or -1.  No reference
  * counterpart: mujoco_warp specialises kernels for any model by tracing at graph-capture
- * time (sim/sim.py:164-191); this is the AOT-compiled equivalent. */
+ * time (sim/sim.py:164-191); this is the AOT-compiled equivalent.  A library built from other
+ * kernel headers than this engine (its mjx_jit_hdr differs from csrc/Makefile's MJX_HDR_HASH)
+ * is refused (-1): its kernels would read the launch parameters through another layout. */
 int mjx_spec_register(const char* path);
 /* Diagnostics: enqueue one empty kernel (`mjx::marker_kernel`, one wave, argument `tag`) on
  * `stream`.  bench.py brackets its timed region with tags 1 and 2 outside the timing, so a

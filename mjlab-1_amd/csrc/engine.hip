@@ -194,14 +194,15 @@ static bool newton_lat() {
   return on;
 }
 // The full-capacity row class (the heavy worlds of the fast carve) reads the constraint
-// Jacobian from the B pack in global memory (phase code 9, carve kLdsJG) instead of an LDS
-// copy.  MJX355_NEWTON_JG=0/1 (A/B).
-static bool newton_jg() {
-  static const bool on = [] {
+// Jacobian from the B pack in global memory (carve kLdsJG) instead of an LDS copy.
+// MJX355_NEWTON_JG (A/B): 0 off, 1 the latency kernel (phase code 9), 2 the throughput kernel
+// (phase code 10); with MJX355_CHAIN covering the full-capacity class, its chain (code 11).
+static int newton_jg() {
+  static const int mode = [] {
     const char* e = getenv("MJX355_NEWTON_JG");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : -1;
   }();
-  return on;
+  return mode;
 }
 
 int find_spec(const Dims& d, const int* dof_parentid) {
@@ -256,8 +257,8 @@ static size_t lds_resolve(const Params& host) {
 }
 // dynamic LDS of a class chain (step_chain): the class's Newton carve, phase C's and, when it
 // runs the next phase A, phase A's
-static size_t lds_chain(const Params& host, int cls, bool with_a) {
-  size_t b = std::max(lds_bytes(host, cls ? 2 + cls : 1), lds_bytes(host, 2));
+static size_t lds_chain(const Params& host, int cls, bool with_a, bool jg = false) {
+  size_t b = std::max(lds_bytes(host, cls ? 2 + cls : jg ? kLdsJG : 1), lds_bytes(host, 2));
   return with_a ? std::max(b, lds_bytes(host, 0)) : b;
 }
 // Which class chains run as one launch (step_chain).  Default: the bulk class (the fewest
@@ -269,6 +270,15 @@ static size_t lds_chain(const Params& host, int cls, bool with_a) {
 // none 4.54 M, bulk 4.52 M, all 4.44 M.  MJX355_CHAIN (A/B diagnostic): 0 none, 1 every
 // class, 2 the bulk class at any batch size, 3 only the others.
 constexpr int kChainMaxWorlds = 8192;
+// J-in-global mode of the full-capacity class (newton_jg): by default the throughput form past
+// kChainMaxWorlds worlds, where that class holds thousands of worlds and its launch is
+// throughput-bound by its LDS carve (jump hfield 16,384: ~5,400 worlds at 84-137 rows, 4 per CU
+// with J in LDS, 12 per CU without; 4.64 -> 4.80 M env-steps/s, two interleaved rounds), and
+// off below (G1 4,096: ~670 heavy worlds, one per SIMD at most: +-0.5 %; tracking -1 %)
+static int jg_mode(int nworld) {
+  const int m = newton_jg();
+  return m >= 0 ? m : nworld > kChainMaxWorlds ? 2 : 0;
+}
 static bool chain_env(int cls, int nworld) {
   static const int mode = [] {
     const char* e = getenv("MJX355_CHAIN");
@@ -595,16 +605,20 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
         // class c's stream: B, then (piped) C and the next substep's A of the same worlds --
         // as one launch (step_chain) unless MJX355_CHAIN=0
         auto class_chain = [&](hipStream_t cs, int cls) {
-          const StepFn fX = piped && chain_env(cls, nworld) ? step_fn(host, cls == 0 && newton_lat() ? 7 : 6) : nullptr;
+          const bool cjg = cls == 0 && newton_lat() && jg_mode(nworld) == 1;
+          const StepFn fX = piped && chain_env(cls, nworld)
+                                ? step_fn(host, cls == 0 && newton_lat() ? (cjg ? 11 : 7) : 6)
+                                : nullptr;
           if (fX) {
             const int selx = k | (cls + 1) << 8 | (last ? 0 : kSelChainA) |
                              (((sub + 1) & 1) ? kSelAPar : 0) |
                              (sub + 1 == nsubstep - 1 ? kSelNextLast : 0);
-            hipLaunchKernelGGL(fX, dim3(n), dim3(kWave), lds_chain(host, cls, !last), cs, dev, w0, w1,
-                               selx, last, integrate, mask);
+            hipLaunchKernelGGL(fX, dim3(n), dim3(kWave), lds_chain(host, cls, !last, cjg), cs, dev,
+                               w0, w1, selx, last, integrate, mask);
             return;
           }
-          const StepFn fJ = cls == 0 && newton_lat() && newton_jg() ? step_fn(host, 9) : nullptr;
+          const int jg = cls == 0 ? jg_mode(nworld) : 0;
+          const StepFn fJ = jg == 1 && newton_lat() ? step_fn(host, 9) : jg == 2 ? step_fn(host, 10) : nullptr;
           hipLaunchKernelGGL(cls ? fB : fJ ? fJ : fBL, dim3(n), dim3(kWave),
                              lds_bytes(host, cls ? 2 + cls : fJ ? kLdsJG : 1), cs, dev, w0, w1, k, last,
                              cls, mask);
@@ -651,8 +665,10 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       } else {
         if ((e = ovf_record()) != hipSuccess) return e;
         if (!mfirst && (e = ovf_launch()) != hipSuccess) return e;
-        hipLaunchKernelGGL(fB, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k, last,
-                           0, mask);
+        // (MJX355_NEWTON_JG=2 on a model without row classes: J from global memory as well)
+        const StepFn fBJ = newton_jg() == 2 ? step_fn(host, 10) : nullptr;  // (A/B only)
+        hipLaunchKernelGGL(fBJ ? fBJ : fB, dim3(n), dim3(kWave), lds_bytes(host, fBJ ? kLdsJG : 1), st,
+                           dev, w0, w1, k, last, 0, mask);
         if (mfirst && (e = ovf_launch()) != hipSuccess) return e;
       }
       hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), st, dev, w0, w1, k, last,

@@ -1722,10 +1722,11 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 // small code changes (G1 161 -> 177 with the LTR Hessian; no spill at 168) and the bulk row
 // class's residency is set by it.  Not for the generic NR 56 / 64 rows (they would spill).
 #define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(PH == 1 && NR <= 48 ? 3 : 1)))
+#define MJX_PHASE_ATTR_B __attribute__((amdgpu_waves_per_eu(NR <= 48 ? 3 : 1)))
 // LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
 // more registers in flight, for the launch that holds the heavy worlds.
-// LAT: 0 the throughput form, 1 the latency form, 2 the latency form reading the constraint
-// Jacobian from the B pack in global memory (phase B only; carve kLdsJG)
+// LAT: bit 0 the latency form of phase B (else the throughput form), bit 1 (phase B only) the
+// constraint Jacobian read from the B pack in global memory (carve kLdsJG)
 template <int NR, int PH, int SP, int LAT>
 __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* __restrict__ P, int w0,
                                           int w1, int sel, int last, int integrate,
@@ -1735,7 +1736,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
   const DModel& m = P->m;
   const DData& D = P->D;
   // phase B: `integrate` carries the Newton row class (0 = full capacity, k > 0 = LP[2 + k])
-  constexpr bool JG = PH == 1 && LAT == 2;
+  constexpr bool JG = PH == 1 && (LAT & 2) != 0;
   const Lds& L = (PH == 1 && integrate > 0) ? P->LP[2 + integrate]
                                             : lds_of<SP, JG ? kLdsJG : PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
@@ -3402,14 +3403,14 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
           if (refactor) {
 #if MJX_JTDJ_MFMA
             rows_load<NR>(R, Lm, nvp, lane);
-            rows_chol<NR, (LAT != 0)>(R, rd, S + LB.chol, nvp, lane);
+            rows_chol<NR, (LAT & 1) != 0>(R, rd, S + LB.chol, nvp, lane);
             rows_store_strict<NR>(R, rd, Lm, nvp, lane);
 #else
             rows_load_ltr<NR>(R, Lm, nvp, lane);  // the reversed matrix's rows when tree_h
             if (tree_h) {
               if constexpr (kTree<SP>) rows_chol_tree<NR, SP>(R, rd, S + LB.chol, lane);
             } else {
-              rows_chol<NR, (LAT != 0)>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
+              rows_chol<NR, (LAT & 1) != 0>(R, rd, S + LB.chol, nvp, lane);  // M / chol offsets are the same in every row-class carve
             }
             rows_store_strict_ltr<NR>(R, rd, Lm, nvp, lane);
 #endif
@@ -3892,7 +3893,7 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
 // one wave per SIMD at most, so its span is one world's latency, not throughput: the kernel
 // may take 256 VGPRs (2 waves / SIMD, still above its LDS-bound residency) and spends them
 // on loads issued ahead of their use (rows_chol<NR, true>).
-// JGL = 2: the constraint Jacobian read from the B pack in global memory (carve kLdsJG): the
+// JGL = 3: the constraint Jacobian read from the B pack in global memory (carve kLdsJG): the
 // heavy worlds' full-capacity carve shrinks by njmax x nvp floats, so they hold a fraction of
 // the LDS the concurrent bulk class needs, and more of them fit a CU where they are many.
 template <int NR, int SP, int JGL = 1>
@@ -3901,6 +3902,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) v
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
   step_body<NR, 1, SP, JGL>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
+}
+// The full-capacity class's Newton in the throughput form (3 waves / SIMD) with J in global
+// memory: for batches whose heavy worlds are many (jump hfield: ~5,400 of 16,384 at 84-137
+// rows), where that launch is throughput-bound, not one world's latency.
+template <int NR, int SP>
+__global__ __launch_bounds__(kWave) MJX_PHASE_ATTR_B void step_phase_jg(
+    const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
+    const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float S[];
+  step_body<NR, 1, SP, 2>(S, P, w0, w1, sel, last, integrate, mask, (int)blockIdx.x);
 }
 
 // The overflow re-solve launches (sel & kSelOvf; ovf_chain): a fixed grid of kOvfGrid
@@ -3974,7 +3985,7 @@ __device__ __forceinline__ void chain_handoff() {
 }
 template <int NR, int SP, int LAT>
 __global__ __launch_bounds__(kWave)
-__attribute__((amdgpu_waves_per_eu(LAT ? 1 : (NR <= 48 ? 3 : 1), LAT ? 2 : 8))) void step_chain(
+__attribute__((amdgpu_waves_per_eu((LAT & 1) ? 1 : (NR <= 48 ? 3 : 1), (LAT & 1) ? 2 : 8))) void step_chain(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
@@ -4042,7 +4053,13 @@ StepFn phase_kernel(int ph) {
       if constexpr ((role & 2) != 0) return step_masked<NR, SP>;
       else return nullptr;
     case 9:
-      if constexpr ((role & 1) != 0) return step_newton_lat<NR, SP, 2>;
+      if constexpr ((role & 1) != 0) return step_newton_lat<NR, SP, 3>;
+      else return nullptr;
+    case 10:  // the full-capacity class's Newton, throughput form, J in global memory
+      if constexpr ((role & 1) != 0) return step_phase_jg<NR, SP>;
+      else return nullptr;
+    case 11:  // the full-capacity class's B -> C -> next A chain, latency form, J in global memory
+      if constexpr ((role & 1) != 0) return step_chain<NR, SP, 3>;
       else return nullptr;
     default:
       return nullptr;
