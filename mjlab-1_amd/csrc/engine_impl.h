@@ -1721,7 +1721,11 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 // Phase B at most 168 registers (3 waves / SIMD): the Newton kernel's allocation drifts with
 // small code changes (G1 161 -> 177 with the LTR Hessian; no spill at 168) and the bulk row
 // class's residency is set by it.  Not for the generic NR 56 / 64 rows (they would spill).
-#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(PH == 1 && NR <= 48 ? 3 : 1)))
+// Phase A at most 168 registers too: with terrain collision (heightfields, box terrains) its
+// natural allocation is 182-189 VGPRs (2 waves / SIMD, 8 worlds per CU) while its LDS admits 12;
+// capped it spills a few dozen bytes per lane (-Rpass-analysis=kernel-resource-usage), as the
+// chain kernel that inlines the same code already does.  The flat models sit at 126-135.
+#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu((PH == 1 || PH == 0) && NR <= 48 ? 3 : 1)))
 #define MJX_PHASE_ATTR_B __attribute__((amdgpu_waves_per_eu(NR <= 48 ? 3 : 1)))
 // LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
 // more registers in flight, for the launch that holds the heavy worlds.
