@@ -3924,10 +3924,15 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR_B void step_phase_jg(
 // VGPRs and phase C 64); its few worlds need no residency.
 // The launch flagged kSelClr is the list's last reader: its last workgroup out empties the
 // list (count and done counter) for the substep after next -- no launch of its own.
+// An empty list (the common case: nothing overflowed the fast carve) was read by nobody and
+// needs no clearing: its workgroups skip the agent-scope fence, whose L2 write-back made each
+// near-empty launch cost ~15 us (in line on the critical path of split batches, Go1 8,192).
 __device__ __forceinline__ void ovf_clear_on_exit(const Params* __restrict__ P, int sel) {
   if (!(sel & kSelClr)) return;
   const int li = 2 * (sel & 0xff) + ((sel & kSelRPar) ? 1 : 0);
   if (threadIdx.x == 0) {
+    // (the count is fixed for the whole launch: only its last workgroup out clears it)
+    if (P->ovf_n[li] == 0) return;
     __threadfence();  // this workgroup's reads of the list precede the count
     if (atomicAdd(P->ovf_done + li, 1) == (int)gridDim.x - 1) {
       P->ovf_n[li] = 0;
@@ -3957,6 +3962,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
+  if (sel & kSelOvf) {  // a workgroup past the listed count: no world, no fences
+    const int li = 2 * (sel & 0xff) + ((sel & kSelRPar) ? 1 : 0);
+    if ((int)blockIdx.x >= min(P->ovf_n[li], P->ovf_cap)) {
+      ovf_clear_on_exit(P, sel);
+      return;
+    }
+  }
   for (int bid = (int)blockIdx.x;; bid += (int)gridDim.x) {
     step_body<NR, 0, SP, false>(S, P, w0, w1, sel, last, integrate, mask, bid);
     __threadfence();  // the packs this wave stored are read back by the next phase

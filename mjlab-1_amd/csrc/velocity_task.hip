@@ -866,10 +866,41 @@ __device__ void obs_elem(const mjxTaskDesc& t, int e, int i) {
 // (which read the updated command and velocities).  Each env touches only its own state, so
 // the wave-level hand-off replaces the launch boundary of two kernels (observe, then
 // observations), one dispatch and gap fewer on the env step's critical path.
+// Block 0 first folds k_post's block partials into the accumulators (the work of a separate
+// k_accum launch, one dispatch and launch gap fewer on the env step's critical path; the
+// partials are complete, k_post ran before this launch), then writes the logs.
 constexpr int kObsEnvs = 4;
 __global__ __launch_bounds__(64 * kObsEnvs, 8) void k_observe_obs(const mjxTaskDesc* __restrict__ T,
-                                                               Acc* __restrict__ acc) {
+                                                               Acc* __restrict__ acc,
+                                                               const float* __restrict__ part,
+                                                               int nblock) {
   const mjxTaskDesc& t = *T;
+  if (blockIdx.x == 0 && nblock > 0) {
+    constexpr int kCh = 64 * kObsEnvs / 128;  // row chunks: 128 field lanes each
+    __shared__ float red[kCh][128];
+    const int i = threadIdx.x & 127, c = threadIdx.x >> 7;
+    float sum = 0.f;
+    if (i < kAccN) {
+      const int per = (nblock + kCh - 1) / kCh;
+      const int b0 = c * per, b1 = min(nblock, b0 + per);
+      float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int b = b0;
+      for (; b + 7 < b1; b += 8)
+#pragma unroll
+        for (int u = 0; u < 8; u++) sv[u] += part[(size_t)(b + u) * kAccN + i];
+      for (; b < b1; b++) sv[0] += part[(size_t)b * kAccN + i];
+      sum = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
+    }
+    red[c][i] = sum;
+    __syncthreads();
+    if (c == 0 && i < kAccN) {
+      float tot = 0.f;
+#pragma unroll
+      for (int k = 0; k < kCh; k++) tot += red[k][i];
+      reinterpret_cast<float*>(acc)[i] += tot;
+    }
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) observe_logs(t, acc);
   const int e = blockIdx.x * kObsEnvs + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (e >= t.nworld) return;
@@ -941,6 +972,9 @@ struct mjxTask_ {
   mjxt::Acc* acc = nullptr;
   float* part = nullptr;  // [nblock][kAccN] k_post block partials
   int nworld = 0;
+  // k_post's partials not yet folded into acc (k_observe_obs folds them; a second post before
+  // an observe folds the first's with a k_accum launch of its own)
+  int pending_nblock = 0;
   int ncu = 256;  // compute units of the device the task was created on
 };
 
@@ -1149,14 +1183,16 @@ int mjx_task_substep(mjxTask* t, void* stream) { TASK_LAUNCH(mjxt::k_substep, t-
 int mjx_task_post(mjxTask* t, void* stream) {
   if (!t) return task_fail("null task");
   const int nblock = (t->nworld + mjxt::kPostEnvs - 1) / mjxt::kPostEnvs;
+  if (t->pending_nblock > 0)  // a post without an observe since: fold its partials first
+    hipLaunchKernelGGL(mjxt::k_accum, dim3(1), dim3(128 * mjxt::kAccChunks), 0, (hipStream_t)stream,
+                       t->part, t->pending_nblock, t->acc);
   if (nblock > t->ncu)
     hipLaunchKernelGGL(mjxt::k_post<8>, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
                        t->dev, t->part);
   else
     hipLaunchKernelGGL(mjxt::k_post<1>, dim3(nblock), dim3(64 * mjxt::kPostEnvs), 0, (hipStream_t)stream,
                        t->dev, t->part);
-  hipLaunchKernelGGL(mjxt::k_accum, dim3(1), dim3(128 * mjxt::kAccChunks), 0, (hipStream_t)stream,
-                     t->part, nblock, t->acc);
+  t->pending_nblock = nblock;  // folded by the next mjx_task_observe (k_observe_obs block 0)
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : task_fail(std::string("k_post: ") + hipGetErrorString(e));
 }
@@ -1176,7 +1212,9 @@ int mjx_task_observe(mjxTask* t, void* stream) {
   }
   (void)nel;
   hipLaunchKernelGGL(mjxt::k_observe_obs, dim3((t->nworld + mjxt::kObsEnvs - 1) / mjxt::kObsEnvs),
-                     dim3(64 * mjxt::kObsEnvs), 0, (hipStream_t)stream, t->dev, t->acc);
+                     dim3(64 * mjxt::kObsEnvs), 0, (hipStream_t)stream, t->dev, t->acc, t->part,
+                     t->pending_nblock);
+  t->pending_nblock = 0;
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : task_fail(std::string("k_observe: ") + hipGetErrorString(e));
 }
