@@ -1725,7 +1725,25 @@ __device__ __forceinline__ void contact_sensors_wave(const float* S, const int* 
 // natural allocation is 182-189 VGPRs (2 waves / SIMD, 8 worlds per CU) while its LDS admits 12;
 // capped it spills a few dozen bytes per lane (-Rpass-analysis=kernel-resource-usage), as the
 // chain kernel that inlines the same code already does.  The flat models sit at 126-135.
-#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu((PH == 1 || PH == 0) && NR <= 48 ? 3 : 1)))
+// "Lean" specialisations: a small-robot (NR <= 20) model without terrain collision whose phase
+// carves all fit 16 worlds per CU (<= 10,240 B: Go1 at its 16 / 64 fast carve).  Their phase B
+// and chain kernels are held to 128 VGPRs (4 waves / SIMD; naturally 145-147, capped they spill
+// ~40 B per lane), so the LDS residency is the register residency too.  Elsewhere 4 waves
+// would only add spill (Go1 at 24 / 96, whose phase-B carve admits 12 per CU: -0.5 %; rough
+// Go1, whose chain inlines the box-box arrays: -20 %).
+template <int SP>
+constexpr bool lean_spec() {
+  if constexpr (SP <= 0) {
+    return false;
+  } else {
+    constexpr Dims d = ModelSpec<SP>::dims();
+    return nr_for_nv(d.nv) <= 20 && d.nstatic == 0 && d.nboxbox == 0 &&
+           make_lds(d, 0).total * 4 <= 10240 && make_lds(d, 1).total * 4 <= 10240 &&
+           make_lds(d, 2).total * 4 <= 10240;
+  }
+}
+template <int SP> constexpr bool kLean = lean_spec<SP>();
+#define MJX_PHASE_ATTR __attribute__((amdgpu_waves_per_eu(PH == 1 && kLean<SP> ? 4 : (PH == 1 || PH == 0) && NR <= 48 ? 3 : 1)))
 #define MJX_PHASE_ATTR_B __attribute__((amdgpu_waves_per_eu(NR <= 48 ? 3 : 1)))
 // LAT selects the latency form of phase B (step_newton_lat below): the same algorithm with
 // more registers in flight, for the launch that holds the heavy worlds.
@@ -4001,7 +4019,7 @@ __device__ __forceinline__ void chain_handoff() {
 }
 template <int NR, int SP, int LAT>
 __global__ __launch_bounds__(kWave)
-__attribute__((amdgpu_waves_per_eu((LAT & 1) ? 1 : (NR <= 48 ? 3 : 1), (LAT & 1) ? 2 : 8))) void step_chain(
+__attribute__((amdgpu_waves_per_eu((LAT & 1) ? 1 : (kLean<SP> ? 4 : NR <= 48 ? 3 : 1), (LAT & 1) ? 2 : 8))) void step_chain(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];

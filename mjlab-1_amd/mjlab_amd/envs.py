@@ -591,12 +591,13 @@ def _g1_velocity_cfg(play: bool) -> ManagerBasedRlEnvCfg:
 def unitree_go1_flat_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/go1/env_cfgs.py:15-127` (flat).
 
-  Engine carve (not a reference field): 24 contacts / 96 rows per world in the fast LDS
-  carve (Go1 flat sees at most 6 / 24), so phase B holds 12 worlds per CU instead of 9; a
-  world past it is re-solved at the max capacity (64 / njmax), nothing is dropped.
-  Measured Go1 8,192: 6.83 -> 7.73 M env-steps/s before the in-line re-solve."""
+  Engine carve (not a reference field): 16 contacts / 64 rows per world in the fast LDS
+  carve (Go1 flat sees at most 6 / 24), so every phase's carve holds 16 worlds per CU (its
+  phase B at 4 waves per SIMD: engine_impl.h kLean); a world past it is re-solved at the max
+  capacity (njmax rows), nothing is dropped.  Measured Go1 8,192: 24 / 96 7.96 / 8.00 M,
+  16 / 64 8.66 / 8.65 M env-steps/s (round 6)."""
   cfg = _flat(_go1_velocity_cfg(play))
-  cfg.sim.engine_capacity = (24, 96)
+  cfg.sim.engine_capacity = (16, 64)
   return cfg
 
 
@@ -604,7 +605,9 @@ def unitree_go1_rough_env_cfg(play: bool = False) -> ManagerBasedRlEnvCfg:
   """`tasks/velocity/config/go1/env_cfgs.py:15-112` (rough): the Go1 task on the curriculum
   box-stair grid with the terrain-level curriculum."""
   cfg = _rough(_go1_velocity_cfg(play), play)
-  cfg.sim.engine_capacity = (24, 96)  # engine carve, as unitree_go1_flat_env_cfg
+  # engine carve: 24 / 96 (its chain inlines the box-box narrowphase; 16 / 64 with phase B at 4
+  # waves per SIMD measured -20 %, round 6)
+  cfg.sim.engine_capacity = (24, 96)
   return cfg
 
 

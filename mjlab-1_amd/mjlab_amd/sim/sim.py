@@ -557,6 +557,11 @@ class Simulation:
     for ncon, rows, role in want:
       try:
         path = jit.ensure_library(model, ncon, rows, role, compile_ok=compile_ok)
+        if path is not None:
+          # (refused -- MjxError, a RuntimeError -- when built from other kernel headers than
+          # the loaded engine library)
+          jit.register(path)
+          loaded = True
       except (RuntimeError, OSError) as e:
         # "always" asked for the specialisation: its failure is the caller's error.  "auto"
         # only wanted speed: the generic kernels compute the same step (GenericKernelWarning
@@ -567,9 +572,6 @@ class Simulation:
         warnings.warn(f"mjlab_amd.Simulation: run-time specialisation unavailable ({e}); "
                       "using the generic kernels", GenericKernelWarning, stacklevel=3)
         continue
-      if path is not None:
-        jit.register(path)
-        loaded = True
     return loaded
 
   def info(self) -> dict:

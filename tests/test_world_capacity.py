@@ -63,11 +63,12 @@ def test_specs_carry_the_task_capacities():
   assert caps["g1_tracking"] == [(56, 200), (48, 160), (250, 250)]
   for name in ("g1_velocity", "g1_jump", "g1_velocity_rough", "g1_jump_hfield"):
     assert caps[name] == [(48, 160), (300, 300)], name
-  # Go1: its tasks' engine_capacity (24, 96) first, the default and the max carve
+  # Go1: its tasks' engine_capacity first (flat 16 / 64, rough 24 / 96), the default and the
+  # max carve
   from mjlab_amd.envs import unitree_go1_flat_env_cfg, unitree_go1_rough_env_cfg
-  for name, make in (("go1_velocity", unitree_go1_flat_env_cfg),
-                     ("go1_velocity_rough", unitree_go1_rough_env_cfg)):
-    assert caps[name] == [(24, 96), (48, 160), (300, 300)], name
+  for name, make, cap in (("go1_velocity", unitree_go1_flat_env_cfg, (16, 64)),
+                          ("go1_velocity_rough", unitree_go1_rough_env_cfg, (24, 96))):
+    assert caps[name] == [cap, (48, 160), (300, 300)], name
     sim, go1 = make().sim, load_scene(name)
-    assert world_capacity(sim, go1) == (24, 96)
+    assert world_capacity(sim, go1) == cap
     assert max_capacity(sim, go1) == (300, 300)
