@@ -228,6 +228,9 @@ constexpr int kSelClr = 1 << 19;  // the re-solve launch that empties its list o
 constexpr int kSelChainA = 1 << 20;
 constexpr int kSelNextLast = 1 << 21;
 constexpr int kSelFusedA = 1 << 22;
+// the full-capacity class's launches (engine.hip heavy_cap): its waves raise their issue
+// priority (s_setprio) over the bulk-class waves sharing their SIMDs
+constexpr int kSelPrio = 1 << 23;
 
 // Launchers (enqueue on `stream`; never synchronise).  `dev` points to a device copy of
 // `host`; `host` is used only for the launch geometry.

@@ -193,6 +193,20 @@ static bool newton_lat() {
   }();
   return on;
 }
+// The full-capacity class's latency Newton kernel at the throughput kernels' 168 VGPRs (phase
+// code 12; naturally ~193, 68 B per lane spilled when capped), its waves at raised issue
+// priority (kSelPrio): a SIMD running a heavy world keeps two bulk-class waves beside it instead
+// of one, and the heavy wave still issues first.  Measured (three interleaved rounds on one
+// box): G1 velocity 4,096 +0.4 / +0.7 / +1.2 %, rough G1 +0.4 / +0.2 / +0.8 %; tracking (its
+// 56 / 200 carve, heavy worlds up to ~190 rows) -0.7 / -0.3 / -0.6 %: on for fast carves of at
+// most 160 rows.  MJX355_HEAVY_CAP=0/1 forces.
+static bool heavy_cap(const Params& host) {
+  static const int mode = [] {
+    const char* e = getenv("MJX355_HEAVY_CAP");
+    return e ? atoi(e) : -1;
+  }();
+  return mode >= 0 ? mode != 0 : host.d.njmax <= 160;
+}
 // The full-capacity row class (the heavy worlds of the fast carve) reads the constraint
 // Jacobian from the B pack in global memory (carve kLdsJG) instead of an LDS copy.
 // MJX355_NEWTON_JG (A/B): 0 off, 1 the latency kernel (phase code 9), 2 the throughput kernel
@@ -619,15 +633,17 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
           }
           const int jg = cls == 0 ? jg_mode(nworld) : 0;
           const StepFn fJ = jg == 1 && newton_lat() ? step_fn(host, 9) : jg == 2 ? step_fn(host, 10) : nullptr;
-          hipLaunchKernelGGL(cls ? fB : fJ ? fJ : fBL, dim3(n), dim3(kWave),
-                             lds_bytes(host, cls ? 2 + cls : fJ ? kLdsJG : 1), cs, dev, w0, w1, k, last,
+          const StepFn fBH = cls == 0 && !fJ && heavy_cap(host) && newton_lat() ? step_fn(host, 12) : fBL;
+          const int pr = fBH != fBL ? kSelPrio : 0;
+          hipLaunchKernelGGL(cls ? fB : fJ ? fJ : fBH, dim3(n), dim3(kWave),
+                             lds_bytes(host, cls ? 2 + cls : fJ ? kLdsJG : 1), cs, dev, w0, w1, k | pr, last,
                              cls, mask);
           if (!piped) return;
           hipLaunchKernelGGL(fC, dim3(n), dim3(kWave), lds_bytes(host, 2), cs, dev, w0, w1,
-                             k | (cls + 1) << 8, last, integrate, mask);
+                             k | (cls + 1) << 8 | pr, last, integrate, mask);
           if (!last)
             hipLaunchKernelGGL(fA, dim3(n), dim3(kWave), lds_bytes(host, 0), cs, dev, w0, w1,
-                               k | (cls + 1) << 8 | (((sub + 1) & 1) ? kSelAPar : 0),
+                               k | (cls + 1) << 8 | (((sub + 1) & 1) ? kSelAPar : 0) | pr,
                                sub + 1 == nsubstep - 1, integrate, mask);
         };
         for (int c = 0; c < nc; c++) {

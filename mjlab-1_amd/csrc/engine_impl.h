@@ -1763,6 +1763,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ S, const Params* _
                                             : lds_of<SP, JG ? kLdsJG : PH>(P);
   const auto& LB = lds_of<SP, 1>(P);
   const auto& LC = lds_of<SP, 2>(P);
+  if (sel & kSelPrio) __builtin_amdgcn_s_setprio(3);
   int w = w0 + bid;
   const int sel_arg = sel;  // (phase C's contact-sensor code has a local `sel`)
   (void)sel_arg;
@@ -3918,8 +3919,10 @@ __global__ __launch_bounds__(kWave) MJX_PHASE_ATTR void step_phase(const Params*
 // JGL = 3: the constraint Jacobian read from the B pack in global memory (carve kLdsJG): the
 // heavy worlds' full-capacity carve shrinks by njmax x nvp floats, so they hold a fraction of
 // the LDS the concurrent bulk class needs, and more of them fit a CU where they are many.
-template <int NR, int SP, int JGL = 1>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 2))) void step_newton_lat(
+// CAP: the same code at the throughput kernels' register budget (3 waves / SIMD), so that a
+// SIMD running a heavy world keeps two bulk-class waves beside it instead of one
+template <int NR, int SP, int JGL = 1, int CAP = 0>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(CAP ? 3 : 1, CAP ? 8 : 2))) void step_newton_lat(
     const Params* __restrict__ P, int w0, int w1, int sel, int last, int integrate,
     const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float S[];
@@ -4094,6 +4097,9 @@ StepFn phase_kernel(int ph) {
       else return nullptr;
     case 11:  // the full-capacity class's B -> C -> next A chain, latency form, J in global memory
       if constexpr ((role & 1) != 0) return step_chain<NR, SP, 3>;
+      else return nullptr;
+    case 12:  // the latency Newton kernel at the throughput register budget (heavy_cap)
+      if constexpr ((role & 1) != 0) return step_newton_lat<NR, SP, 1, 1>;
       else return nullptr;
     default:
       return nullptr;
