@@ -212,11 +212,19 @@ struct Params {
 // 20-contact / 80-row fast carve, 3.5 % of world-substeps re-solved): 64 workgroups 1.43 M
 // env-steps/s, 256 1.69 M, 512 1.65 M; with nothing listed the grid size is not measurable.
 constexpr int kOvfGrid = 256;
-// ... and where the chain runs in line on a split stream (the critical path): Go1 flat 8,192
-// worlds at 256 / 64 / 32 / 16 workgroups 6.73 / 7.32 / 7.40 / 7.41 M env-steps/s; under
-// forced overflow (G1 at a 20 / 80 fast carve, 3.5 % of world-substeps re-solved) 64 / 32 /
-// 16 workgroups 1.49 / 1.17 / 0.81 M
-constexpr int kOvfGridInline = 32;
+// ... and where the chain runs in line behind a range chain or on a split stream (the critical
+// path).  There the launch dispatches while the other range's chain holds every CU (Go1 16 / 64:
+// 16 worlds per CU, the register file full at 4 waves per SIMD), and each max-carve workgroup
+// (32 KB of LDS, 256 VGPRs) waits for several of that chain's waves to retire: the empty launch
+// spans 20-34 us (kernel trace, profiles/r06_go1_step_timeline.txt).  Go1 flat 8,192, two
+// interleaved rounds: 32 workgroups 8.71 / 8.68 M env-steps/s, 1 workgroup 8.93 / 8.88 M, no
+// re-solve at all (MJX355_RESOLVE=0, the bound) 9.24 / 9.13 M; round 4 (24 / 96 carve): 256 /
+// 64 / 32 / 16 workgroups 6.73 / 7.32 / 7.40 / 7.41 M.  The price: the one workgroup re-solves
+// the listed worlds one after another (forced overflow, G1 split at a 20 / 80 carve, round 4:
+// 64 / 32 / 16 workgroups 1.49 / 1.17 / 0.81 M), so a range-chained batch whose fast carve
+// overflows often should get a larger carve (Simulation.fast_capacity, the bench's
+// overflow.resolved_events); MJX355_OVF_GRID overrides.
+constexpr int kOvfGridInline = 1;
 constexpr int kSelOvf = 1 << 16;
 constexpr int kSelAPar = 1 << 17;
 constexpr int kSelRPar = 1 << 18;
