@@ -468,12 +468,16 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
   // fast carve with the re-solve in line behind them.  The max-carve grid is the whole batch,
   // and at 64 KiB of LDS per workgroup even the unmasked workgroups dispatch two per CU; the
   // in-line re-solve is a fixed launch on the critical path.  Measured: G1 4,096 worlds max
-  // carve +1.1 %, jump hfield 16,384 worlds fast carve +9.5 %.  MJX355_MASKED_BIG=0/1 forces.
+  // carve +1.1 %, jump hfield 16,384 worlds fast carve +9.5 % (round 6, two interleaved rounds:
+  // +14 %); round 6, max carve (fused, step_masked): Go1 8,192 +1.5 %, rough Go1 +2.0 %, jump
+  // flat 16,384 +0.8 %.  So the max carve unless a heightfield model has more than 4,096
+  // worlds (its reset worlds' phase A at the max carve's 300 contacts is the slow part there).
+  // MJX355_MASKED_BIG=0/1 forces.
   static const int masked_big_env = [] {
     const char* e = getenv("MJX355_MASKED_BIG");
     return e ? atoi(e) : -1;
   }();
-  const bool masked_big = masked_big_env >= 0 ? masked_big_env != 0 : nworld <= 4096;
+  const bool masked_big = masked_big_env >= 0 ? masked_big_env != 0 : nworld <= 4096 || host.d.nhfield == 0;
   if (mask && hbig && masked_big) {
     // masked forward (a few reset worlds): at full capacity throughout -- nothing to re-solve;
     // A -> B -> C as one launch (step_masked) unless MJX355_MASKED_FUSED=0
