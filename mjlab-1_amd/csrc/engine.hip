@@ -602,8 +602,17 @@ hipError_t launch_step(const Params& host, const Params* dev, int nworld, int ns
       if (nc > 0 && mask) {
         // masked forward (a few reset worlds): one Newton launch at full capacity over the
         // masked worlds -- no classify launch, no fork/join latency on this short critical path
-        hipLaunchKernelGGL(fBL, dim3(n), dim3(kWave), lds_bytes(host, 1), st, dev, w0, w1, k,
-                           last, -1, mask);
+        // The grid is the whole batch and nearly every workgroup exits at once, so the launch
+        // costs its dispatch rounds: with J read from the B pack in global memory (carve kLdsJG,
+        // ~8 KB instead of the full fast carve's 31.8 KB) 16 workgroups fit a CU instead of 4.
+        // MJX355_MASKED_JG=0: J in LDS (A/B)
+        static const bool masked_jg = [] {
+          const char* e = getenv("MJX355_MASKED_JG");
+          return !e || atoi(e) != 0;
+        }();
+        const StepFn fMJ = masked_jg && newton_lat() ? step_fn(host, 9) : nullptr;
+        hipLaunchKernelGGL(fMJ ? fMJ : fBL, dim3(n), dim3(kWave), lds_bytes(host, fMJ ? kLdsJG : 1), st,
+                           dev, w0, w1, k, last, -1, mask);
         // (MJX355_MASKED_BIG=0) masked worlds past the fast carve: re-solved in line
         if (ovf) ovf_chain(host, dev, *hbig, dbig, st, k, w0, w1, sub, nsubstep, integrate, false, true);
       } else if (nc > 0) {
