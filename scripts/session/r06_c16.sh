@@ -1,0 +1,11 @@
+#!/bin/bash
+# k_accum folded into k_observe_obs + empty re-solve launches without agent-scope fences:
+# fused / overflow tests, then A/B against the previous build
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T="--timeout 300 --timeout-method thread"
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf $T -k "fused or curriculum or jump or overflow or config1 or split" > gpurun_out/r06c16_gpu.log 2>&1
+rc=$?; grep -E "^FAILED|passed|failed|^E  " gpurun_out/r06c16_gpu.log | tail -20 | cut -c1-600; [ $rc -eq 0 ] || exit $rc
+ROUNDS="1 2" STEPS=100 LIBS="libmjx355_base.so libmjx355.so" \
+TASKS="Mjlab-Velocity-Flat-Unitree-G1:4096 Mjlab-Velocity-Flat-Unitree-Go1:8192 Mjlab-Tracking-Flat-Unitree-G1:4096" timeout -k 10 800 bash scripts/lib_ab.sh

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 6: the register-capped heavy Newton with and without raised priority, three rounds
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+line() {  # tag task n env...
+  local tag=$1 task=$2 n=$3; shift 3
+  env "$@" timeout -k 10 200 python3 bench.py --task $task --num-envs $n --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/r06c30_$tag.log 2>&1 || exit $?
+  grep '^{' gpurun_out/r06c30_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', round(d['value']), round(d['ms_per_step'],4), d['overflow']['resolved_events'])"
+}
+for r in 1 2 3; do
+  line g1_def_$r Mjlab-Velocity-Flat-Unitree-G1 4096 MJX355_X=0
+  line g1_cap_$r Mjlab-Velocity-Flat-Unitree-G1 4096 MJX355_HEAVY_CAP=1
+  line g1_capprio_$r Mjlab-Velocity-Flat-Unitree-G1 4096 MJX355_HEAVY_PRIO=1 MJX355_HEAVY_CAP=1
+  line tr_def_$r Mjlab-Tracking-Flat-Unitree-G1 4096 MJX355_X=0
+  line tr_cap_$r Mjlab-Tracking-Flat-Unitree-G1 4096 MJX355_HEAVY_CAP=1
+  line tr_capprio_$r Mjlab-Tracking-Flat-Unitree-G1 4096 MJX355_HEAVY_PRIO=1 MJX355_HEAVY_CAP=1
+  line rg1_def_$r Mjlab-Velocity-Rough-Unitree-G1 4096 MJX355_X=0
+  line rg1_capprio_$r Mjlab-Velocity-Rough-Unitree-G1 4096 MJX355_HEAVY_PRIO=1 MJX355_HEAVY_CAP=1
+done

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6: Go1 8,192 upper bound without the in-line re-solve (MJX355_RESOLVE=0) vs default / grid 1
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+line() {  # tag task n env...
+  local tag=$1 task=$2 n=$3; shift 3
+  env "$@" timeout -k 10 200 python3 bench.py --task $task --num-envs $n --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/r06c33_$tag.log 2>&1 || exit $?
+  grep '^{' gpurun_out/r06c33_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', round(d['value']), round(d['ms_per_step'],4), d['overflow']['resolved_events'])"
+}
+for r in 1 2; do
+  line go1_def_$r Mjlab-Velocity-Flat-Unitree-Go1 8192 MJX355_X=0
+  line go1_nores_$r Mjlab-Velocity-Flat-Unitree-Go1 8192 MJX355_RESOLVE=0
+  line go1_g1_$r Mjlab-Velocity-Flat-Unitree-Go1 8192 MJX355_OVF_GRID=1
+  line go1_split1_$r Mjlab-Velocity-Flat-Unitree-Go1 8192 MJX355_SPLIT=1
+done
